@@ -1,0 +1,748 @@
+/*
+ * hgref.c -- CPU restatement of the reference FOBE/HOBE hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY. This file is the parity ORACLE: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and
+ * only as the checker / the timed CPU baseline. The product
+ * (hypergraphembedding_amd + libhgx.so) never links or calls it.
+ *
+ * Every function restates the algorithm of the reference file:line it cites
+ * (JSybrandt/HypergraphEmbedding, read-only at /root/reference). Parity
+ * pinning: the RNG, CSR/SpGEMM ordering, alg-dist, FOBE/HOBE samplers and
+ * SamplesToModelInput are checked BIT-EXACT against golden vectors produced by
+ * importing the reference's own modules (tests/golden/make_golden.py). The
+ * trainer (hgref_train) restates Keras-2.x Adagrad semantics; keras/tensorflow
+ * are absent from the image, so the trainer is "parity unpinned".
+ *
+ * Compile with -ffp-contract=off: the restatement must round exactly like
+ * numpy (no fused multiply-adds).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------- */
+/* numpy legacy RandomState (MT19937) -- numpy/random/_mt19937.pyx,           */
+/* distributions.c. Used by the reference via np.random.* (global state).    */
+/* ------------------------------------------------------------------------- */
+#define MT_N 624
+#define MT_M 397
+typedef struct {
+  uint32_t mt[MT_N];
+  int pos;
+} hgref_rng;
+
+hgref_rng *hgref_rng_create(uint32_t seed) {
+  hgref_rng *s = (hgref_rng *)malloc(sizeof(hgref_rng));
+  s->mt[0] = seed;
+  for (int i = 1; i < MT_N; i++)
+    s->mt[i] = 1812433253u * (s->mt[i - 1] ^ (s->mt[i - 1] >> 30)) + (uint32_t)i;
+  s->pos = MT_N;
+  return s;
+}
+void hgref_rng_destroy(hgref_rng *s) { free(s); }
+void hgref_rng_copy(hgref_rng *dst, const hgref_rng *src) { *dst = *src; }
+int hgref_rng_sizeof(void) { return (int)sizeof(hgref_rng); }
+
+static void mt_twist(hgref_rng *s) {
+  static const uint32_t mag01[2] = {0u, 0x9908b0dfu};
+  int i;
+  uint32_t y;
+  for (i = 0; i < MT_N - MT_M; i++) {
+    y = (s->mt[i] & 0x80000000u) | (s->mt[i + 1] & 0x7fffffffu);
+    s->mt[i] = s->mt[i + MT_M] ^ (y >> 1) ^ mag01[y & 1u];
+  }
+  for (; i < MT_N - 1; i++) {
+    y = (s->mt[i] & 0x80000000u) | (s->mt[i + 1] & 0x7fffffffu);
+    s->mt[i] = s->mt[i + (MT_M - MT_N)] ^ (y >> 1) ^ mag01[y & 1u];
+  }
+  y = (s->mt[MT_N - 1] & 0x80000000u) | (s->mt[0] & 0x7fffffffu);
+  s->mt[MT_N - 1] = s->mt[MT_M - 1] ^ (y >> 1) ^ mag01[y & 1u];
+  s->pos = 0;
+}
+
+uint32_t hgref_rng_next32(hgref_rng *s) {
+  if (s->pos == MT_N) mt_twist(s);
+  uint32_t y = s->mt[s->pos++];
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+static uint64_t next64(hgref_rng *s) {
+  uint64_t hi = hgref_rng_next32(s);
+  return (hi << 32) | hgref_rng_next32(s);
+}
+
+/* np.random.random(): ((a>>5)*2^26 + (b>>6)) / 2^53 */
+double hgref_rng_double(hgref_rng *s) {
+  int32_t a = (int32_t)(hgref_rng_next32(s) >> 5);
+  int32_t b = (int32_t)(hgref_rng_next32(s) >> 6);
+  return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+
+void hgref_rng_random(hgref_rng *s, int64_t n, double *out) {
+  for (int64_t i = 0; i < n; i++) out[i] = hgref_rng_double(s);
+}
+
+static uint64_t gen_mask(uint64_t max) {
+  uint64_t m = max;
+  m |= m >> 1; m |= m >> 2; m |= m >> 4; m |= m >> 8; m |= m >> 16; m |= m >> 32;
+  return m;
+}
+
+/* random_interval(max): used by legacy shuffle/permutation. */
+static uint64_t rng_interval(hgref_rng *s, uint64_t max) {
+  if (max == 0) return 0;
+  uint64_t mask = gen_mask(max), v;
+  if (max <= 0xffffffffull) {
+    while ((v = (hgref_rng_next32(s) & mask)) > max) {}
+  } else {
+    while ((v = (next64(s) & mask)) > max) {}
+  }
+  return v;
+}
+
+/* legacy randint(0, n): random_bounded_uint64_fill(off=0, rng=n-1, masked). */
+static int64_t rng_randint(hgref_rng *s, int64_t n) {
+  uint64_t rng = (uint64_t)(n - 1);
+  if (rng == 0) return 0;
+  if (rng <= 0xffffffffull) {
+    if (rng == 0xffffffffull) return (int64_t)hgref_rng_next32(s);
+    uint32_t mask = (uint32_t)gen_mask(rng), v;
+    while ((v = (hgref_rng_next32(s) & mask)) > rng) {}
+    return (int64_t)v;
+  }
+  uint64_t mask = gen_mask(rng), v;
+  while ((v = (next64(s) & mask)) > rng) {}
+  return (int64_t)v;
+}
+
+int64_t hgref_rng_randint(hgref_rng *s, int64_t n) { return rng_randint(s, n); }
+
+/* legacy permutation(n) = arange + shuffle: reversed Fisher-Yates, i=n-1..1 */
+void hgref_rng_permutation(hgref_rng *s, int64_t n, int64_t *out) {
+  for (int64_t i = 0; i < n; i++) out[i] = i;
+  for (int64_t i = n - 1; i >= 1; i--) {
+    int64_t j = (int64_t)rng_interval(s, (uint64_t)i);
+    int64_t t = out[j]; out[j] = out[i]; out[i] = t;
+  }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Sparse pattern products in scipy's SMMP column order.                     */
+/* scipy csr_matmat emits each row's columns in REVERSE first-discovery order */
+/* (linked list, head insertion). The reference samples from rows of these  */
+/* products (hg2v_sample.py:154,167,659,679,698,703) via .nonzero()[1], so   */
+/* the column order decides which element np.random.choice picks.           */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  int64_t nrow;
+  int64_t *p;  /* nrow+1 */
+  int32_t *j;  /* p[nrow] */
+} pat;
+
+static void pat_free(pat *c) { free(c->p); free(c->j); c->p = NULL; c->j = NULL; }
+
+static pat spgemm_pattern(int64_t nrow, const int64_t *Ap, const int32_t *Aj,
+                          int64_t ncolB, const int64_t *Bp, const int32_t *Bj) {
+  pat C;
+  C.nrow = nrow;
+  C.p = (int64_t *)malloc(sizeof(int64_t) * (nrow + 1));
+  int64_t *next = (int64_t *)malloc(sizeof(int64_t) * (ncolB > 0 ? ncolB : 1));
+  for (int64_t k = 0; k < ncolB; k++) next[k] = -1;
+  int64_t cap = 1024, nnz = 0;
+  C.j = (int32_t *)malloc(sizeof(int32_t) * cap);
+  C.p[0] = 0;
+  for (int64_t i = 0; i < nrow; i++) {
+    int64_t head = -2, len = 0;
+    for (int64_t jj = Ap[i]; jj < Ap[i + 1]; jj++) {
+      int32_t j = Aj[jj];
+      for (int64_t kk = Bp[j]; kk < Bp[j + 1]; kk++) {
+        int32_t k = Bj[kk];
+        if (next[k] == -1) { next[k] = head; head = k; len++; }
+      }
+    }
+    if (nnz + len > cap) {
+      while (nnz + len > cap) cap *= 2;
+      C.j = (int32_t *)realloc(C.j, sizeof(int32_t) * cap);
+    }
+    for (int64_t t = 0; t < len; t++) {
+      C.j[nnz++] = (int32_t)head;
+      int64_t tmp = head; head = next[head]; next[tmp] = -1;
+    }
+    C.p[i + 1] = nnz;
+  }
+  free(next);
+  return C;
+}
+
+static pat pat_view(int64_t nrow, const int32_t *rp32, const int32_t *col) {
+  pat P;
+  P.nrow = nrow;
+  P.p = (int64_t *)malloc(sizeof(int64_t) * (nrow + 1));
+  for (int64_t i = 0; i <= nrow; i++) P.p[i] = rp32[i];
+  int64_t nnz = P.p[nrow];
+  P.j = (int32_t *)malloc(sizeof(int32_t) * (nnz > 0 ? nnz : 1));
+  memcpy(P.j, col, sizeof(int32_t) * nnz);
+  return P;
+}
+
+/* Exposed for tests: row pointer + columns of A*B in SMMP order. Call with
+ * cols=NULL to get nnz. */
+int64_t hgref_spgemm(int64_t nrowA, const int32_t *Ap, const int32_t *Aj,
+                     int64_t nrowB, int64_t ncolB, const int32_t *Bp,
+                     const int32_t *Bj, int64_t *out_p, int32_t *out_j) {
+  pat A = pat_view(nrowA, Ap, Aj), B = pat_view(nrowB, Bp, Bj);
+  pat C = spgemm_pattern(nrowA, A.p, A.j, ncolB, B.p, B.j);
+  int64_t nnz = C.p[nrowA];
+  if (out_p) memcpy(out_p, C.p, sizeof(int64_t) * (nrowA + 1));
+  if (out_j) memcpy(out_j, C.j, sizeof(int32_t) * nnz);
+  pat_free(&A); pat_free(&B); pat_free(&C);
+  return nnz;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Algebraic distance -- algebraic_distance.py:34-51 (_update_alg_dist),      */
+/* 54-91 (node half then edge half using NEW node coords), 97-123 (joint     */
+/* per-dim min-max rescale), 126-175 (driver). float64, same op order as the */
+/* reference: b = (sum_e y_e*(1/|e|)) / (sum_e 1/|e|) accumulated in CSR     */
+/* column order (sorted), then (a+b)/2, then (x-min)/(max-min).              */
+/* Returns 0, or -1 for an isolated row (the reference raises                */
+/* ZeroDivisionError at algebraic_distance.py:49).                            */
+/* ------------------------------------------------------------------------- */
+static int algdist_half(int64_t R, int k, const int32_t *rp, const int32_t *col,
+                        const int32_t *rp_src, const double *self_in,
+                        const double *src, double *out) {
+  double *acc = (double *)malloc(sizeof(double) * k);
+  for (int64_t a = 0; a < R; a++) {
+    if (rp[a + 1] == rp[a]) { free(acc); return -1; }
+    for (int d = 0; d < k; d++) acc[d] = 0.0;
+    double wsum = 0.0;
+    for (int32_t t = rp[a]; t < rp[a + 1]; t++) {
+      int32_t b = col[t];
+      double w = 1.0 / (double)(rp_src[b + 1] - rp_src[b]);
+      for (int d = 0; d < k; d++) acc[d] = acc[d] + src[(int64_t)b * k + d] * w;
+      wsum = wsum + w;
+    }
+    for (int d = 0; d < k; d++) {
+      double bd = acc[d] / wsum;
+      out[a * k + d] = (self_in[a * k + d] + bd) / 2.0;
+    }
+  }
+  free(acc);
+  return 0;
+}
+
+int hgref_algdist(int64_t N, int64_t E, int k, int iters, const int32_t *rp_n,
+                  const int32_t *col_n, const int32_t *rp_e,
+                  const int32_t *col_e, double *x, double *y) {
+  double *xn = (double *)malloc(sizeof(double) * N * k);
+  double *yn = (double *)malloc(sizeof(double) * E * k);
+  double *mn = (double *)malloc(sizeof(double) * k);
+  double *mx = (double *)malloc(sizeof(double) * k);
+  int rc = 0;
+  for (int it = 0; it < iters && rc == 0; it++) {
+    rc = algdist_half(N, k, rp_n, col_n, rp_e, x, y, xn);
+    if (rc) break;
+    rc = algdist_half(E, k, rp_e, col_e, rp_n, y, xn, yn);
+    if (rc) break;
+    /* np.min(axis=0) of edges / nodes, then the min of the two (exact). */
+    for (int d = 0; d < k; d++) { mn[d] = INFINITY; mx[d] = -INFINITY; }
+    for (int64_t i = 0; i < N; i++)
+      for (int d = 0; d < k; d++) {
+        double v = xn[i * k + d];
+        if (v < mn[d]) mn[d] = v;
+        if (v > mx[d]) mx[d] = v;
+      }
+    for (int64_t i = 0; i < E; i++)
+      for (int d = 0; d < k; d++) {
+        double v = yn[i * k + d];
+        if (v < mn[d]) mn[d] = v;
+        if (v > mx[d]) mx[d] = v;
+      }
+    for (int64_t i = 0; i < N; i++)
+      for (int d = 0; d < k; d++) {
+        double v = xn[i * k + d] - mn[d];
+        x[i * k + d] = v / (mx[d] - mn[d]);
+      }
+    for (int64_t i = 0; i < E; i++)
+      for (int d = 0; d < k; d++) {
+        double v = yn[i * k + d] - mn[d];
+        y[i * k + d] = v / (mx[d] - mn[d]);
+      }
+  }
+  free(xn); free(yn); free(mn); free(mx);
+  return rc;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Record layout = SamplesToModelInput(records, K, weighted=False)           */
+/* (hg2v_sample.py:751-797): int32 [ln, le, rn, re, nn_0..K-1, ne_0..K-1],   */
+/* each id +1 and 0 when absent/padded; float32 [nn_prob, ee_prob, ne_prob], */
+/* unset -> 0. Records are emitted in the reference's generation order.      */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  int K;
+  int64_t n, cap;
+  int32_t *idx;
+  float *tgt;
+} recbuf;
+
+static int32_t *rec_slot(recbuf *rb) {
+  if (rb->n >= rb->cap) return NULL;
+  int R = 4 + 2 * rb->K;
+  int32_t *r = rb->idx + rb->n * R;
+  for (int i = 0; i < R; i++) r[i] = 0;
+  float *t = rb->tgt + rb->n * 3;
+  t[0] = t[1] = t[2] = 0.0f;
+  return r;
+}
+
+/* _sample_adj_matrix (hg2v_sample.py:53-86), one row. Appends chosen column
+ * ids to out (capacity >= max(q, rowlen)). Returns the count. */
+static int64_t sample_row(hgref_rng *s, const int32_t *cols, int64_t len,
+                          int64_t q, int negative, int64_t ncols, int32_t *out,
+                          int64_t *perm_scratch) {
+  if (negative) {
+    for (int64_t t = 0; t < q; t++) out[t] = (int32_t)rng_randint(s, ncols);
+    return q;
+  }
+  if (len == 0) return 0;
+  int64_t m = q < len ? q : len;
+  /* np.random.choice(cols, m, replace=False) = cols[permutation(len)[:m]] */
+  hgref_rng_permutation(s, len, perm_scratch);
+  for (int64_t t = 0; t < m; t++) out[t] = cols[perm_scratch[t]];
+  return m;
+}
+
+/* _sample_neighbors (hg2v_sample.py:49-51): K draws with replacement. */
+static void sample_neighbors(hgref_rng *s, const int32_t *cols, int64_t len,
+                             int K, int32_t *out_plus1) {
+  /* np.random.choice(cols, K, replace=True) = cols[randint(0, len, K)].
+   * len==0 raises in numpy; rows reached here always have len>0. */
+  for (int t = 0; t < K; t++)
+    out_plus1[t] = cols[rng_randint(s, len)] + 1;
+}
+
+/* Pair list (row, col) for every row of pattern P with quota q[row]. */
+typedef struct {
+  int64_t n, cap;
+  int32_t *a, *b;
+} pairs;
+
+static void pairs_push(pairs *P, int32_t a, int32_t b) {
+  if (P->n == P->cap) {
+    P->cap = P->cap ? P->cap * 2 : 4096;
+    P->a = (int32_t *)realloc(P->a, sizeof(int32_t) * P->cap);
+    P->b = (int32_t *)realloc(P->b, sizeof(int32_t) * P->cap);
+  }
+  P->a[P->n] = a; P->b[P->n] = b; P->n++;
+}
+
+static void sample_pattern(hgref_rng *s, const pat *P, int64_t ncols,
+                           const int32_t *quota, int32_t quota_all, int negative,
+                           pairs *out, int swap) {
+  int64_t maxlen = 1;
+  for (int64_t r = 0; r < P->nrow; r++) {
+    int64_t l = P->p[r + 1] - P->p[r];
+    int64_t q = quota ? quota[r] : quota_all;
+    if (l > maxlen) maxlen = l;
+    if (q > maxlen) maxlen = q;
+  }
+  int32_t *buf = (int32_t *)malloc(sizeof(int32_t) * maxlen);
+  int64_t *perm = (int64_t *)malloc(sizeof(int64_t) * maxlen);
+  for (int64_t r = 0; r < P->nrow; r++) {
+    int64_t q = quota ? quota[r] : quota_all;
+    int64_t m = sample_row(s, P->j + P->p[r], P->p[r + 1] - P->p[r], q,
+                           negative, ncols, buf, perm);
+    for (int64_t t = 0; t < m; t++) {
+      if (swap) pairs_push(out, buf[t], (int32_t)r);
+      else pairs_push(out, (int32_t)r, buf[t]);
+    }
+  }
+  free(buf); free(perm);
+}
+
+/* ------------------------------------------------------------------------- */
+/* FOBE: BooleanSamples (hg2v_sample.py:125-242).                             */
+/* Quotas are int(weight*num_samples) computed by the caller (:138-146).     */
+/* ------------------------------------------------------------------------- */
+int64_t hgref_fobe_sample(hgref_rng *s, int64_t N, int64_t E,
+                          const int32_t *rp_n, const int32_t *col_n,
+                          const int32_t *rp_e, const int32_t *col_e,
+                          const int32_t *node_q, const int32_t *edge_q,
+                          const int32_t *neg_node_q, const int32_t *neg_edge_q,
+                          int K, int64_t cap, int32_t *idx, float *tgt) {
+  recbuf rb = {K, 0, cap, idx, tgt};
+  int R = 4 + 2 * K;
+  pat A = pat_view(N, rp_n, col_n), AT = pat_view(E, rp_e, col_e);
+  pat NN = spgemm_pattern(N, A.p, A.j, N, AT.p, AT.j);   /* :154 */
+  pat EE = spgemm_pattern(E, AT.p, AT.j, E, A.p, A.j);   /* :167 */
+  pairs P = {0, 0, NULL, NULL};
+  int64_t overflow = 0;
+
+  sample_pattern(s, &NN, N, node_q, 0, 0, &P, 0);        /* :157 */
+  for (int64_t t = 0; t < P.n; t++) {
+    int32_t *r = rec_slot(&rb);
+    if (!r) { overflow = 1; break; }
+    r[0] = P.a[t] + 1; r[2] = P.b[t] + 1; rb.tgt[rb.n * 3 + 0] = 1.0f; rb.n++;
+  }
+  P.n = 0;
+  sample_pattern(s, &EE, E, edge_q, 0, 0, &P, 0);        /* :170 */
+  for (int64_t t = 0; t < P.n; t++) {
+    int32_t *r = rec_slot(&rb);
+    if (!r) { overflow = 1; break; }
+    r[1] = P.a[t] + 1; r[3] = P.b[t] + 1; rb.tgt[rb.n * 3 + 1] = 1.0f; rb.n++;
+  }
+  P.n = 0;
+  sample_pattern(s, &A, E, node_q, 0, 0, &P, 0);         /* :178 */
+  sample_pattern(s, &AT, N, edge_q, 0, 0, &P, 1);        /* :181 swapped */
+  for (int64_t t = 0; t < P.n; t++) {                    /* :183-194 */
+    int32_t v = P.a[t], e = P.b[t];
+    int32_t *r = rec_slot(&rb);
+    if (!r) { overflow = 1; break; }
+    r[0] = v + 1; r[3] = e + 1;
+    sample_neighbors(s, A.j + A.p[v], A.p[v + 1] - A.p[v], K, r + 4 + K);
+    sample_neighbors(s, AT.j + AT.p[e], AT.p[e + 1] - AT.p[e], K, r + 4);
+    rb.tgt[rb.n * 3 + 2] = 1.0f;
+    rb.n++;
+  }
+  if (neg_node_q && neg_edge_q) {                        /* :198-240 */
+    P.n = 0;
+    sample_pattern(s, &NN, N, neg_node_q, 0, 1, &P, 0);
+    for (int64_t t = 0; t < P.n; t++) {
+      int32_t *r = rec_slot(&rb);
+      if (!r) { overflow = 1; break; }
+      r[0] = P.a[t] + 1; r[2] = P.b[t] + 1; rb.n++;
+    }
+    for (int rep = 0; rep < 2; rep++) {  /* edge-edge, and the :215-221 copy */
+      P.n = 0;
+      sample_pattern(s, &EE, E, neg_edge_q, 0, 1, &P, 0);
+      for (int64_t t = 0; t < P.n; t++) {
+        int32_t *r = rec_slot(&rb);
+        if (!r) { overflow = 1; break; }
+        r[1] = P.a[t] + 1; r[3] = P.b[t] + 1; rb.n++;
+      }
+    }
+    P.n = 0;
+    sample_pattern(s, &A, E, neg_node_q, 0, 1, &P, 0);
+    sample_pattern(s, &AT, N, neg_edge_q, 0, 1, &P, 1);
+    for (int64_t t = 0; t < P.n; t++) {
+      int32_t v = P.a[t], e = P.b[t];
+      int32_t *r = rec_slot(&rb);
+      if (!r) { overflow = 1; break; }
+      r[0] = v + 1; r[3] = e + 1;
+      sample_neighbors(s, A.j + A.p[v], A.p[v + 1] - A.p[v], K, r + 4 + K);
+      sample_neighbors(s, AT.j + AT.p[e], AT.p[e + 1] - AT.p[e], K, r + 4);
+      rb.n++;
+    }
+  }
+  (void)R;
+  free(P.a); free(P.b);
+  pat_free(&A); pat_free(&AT); pat_free(&NN); pat_free(&EE);
+  return overflow ? -1 : rb.n;
+}
+
+/* ------------------------------------------------------------------------- */
+/* HOBE probabilities.                                                        */
+/* _same_type_dist_calc (hg2v_sample.py:527-543): for pair (i,j) over the    */
+/* shared targets t: w = (sqrt(k) - ||a_i - a_t||_2)/sqrt(k) in float32,      */
+/* prob = max_t min(w_it, w_jt), 0 when nothing is shared. numpy's norm of a */
+/* float32 vector with k<32 is OpenBLAS sdot's tail loop: float products     */
+/* accumulated in a double, then cast to float; sqrt in float32.             */
+/* ------------------------------------------------------------------------- */
+static float dist_weight(const float *a, const float *b, int k) {
+  double acc = 0.0;
+  for (int d = 0; d < k; d++) {
+    float df = a[d] - b[d];
+    float pr = df * df;
+    acc += (double)pr;
+  }
+  float nrm = sqrtf((float)acc);
+  float md = (float)sqrt((double)k);
+  return (md - nrm) / md;
+}
+
+float hgref_dist_weight(const float *a, const float *b, int k) {
+  return dist_weight(a, b, k);
+}
+
+/* sorted-list intersection of rows i and j of P; src/tgt coords */
+static float same_type_prob(const int32_t *rp, const int32_t *col, int32_t i,
+                            int32_t j, const float *src, const float *tgt,
+                            int k) {
+  int32_t a = rp[i], ae = rp[i + 1], b = rp[j], be = rp[j + 1];
+  float prob = 0.0f;  /* prob = 0; prob = max(prob, min(w_ik, w_jk)) */
+  while (a < ae && b < be) {
+    if (col[a] < col[b]) a++;
+    else if (col[a] > col[b]) b++;
+    else {
+      int32_t t = col[a];
+      float wi = dist_weight(src + (int64_t)i * k, tgt + (int64_t)t * k, k);
+      float wj = dist_weight(src + (int64_t)j * k, tgt + (int64_t)t * k, k);
+      float m = wj < wi ? wj : wi;
+      if (m > prob) prob = m;
+      a++; b++;
+    }
+  }
+  return prob;
+}
+
+/* kind 0: node-node over A (rp_n/col_n), 1: edge-edge over A^T,
+ * 2: node-edge (DiffTypeDistanceSample, hg2v_sample.py:588-629):
+ *    max over e' in E(v) of edge-edge prob(e, e'). */
+void hgref_hobe_probs(int kind, int64_t n, const int32_t *pa, const int32_t *pb,
+                      const int32_t *rp_n, const int32_t *col_n,
+                      const int32_t *rp_e, const int32_t *col_e,
+                      const float *alg_node, const float *alg_edge, int k,
+                      float *out) {
+  for (int64_t t = 0; t < n; t++) {
+    float p = 0.0f;
+    if (kind == 0) {
+      p = same_type_prob(rp_n, col_n, pa[t], pb[t], alg_node, alg_edge, k);
+    } else if (kind == 1) {
+      p = same_type_prob(rp_e, col_e, pa[t], pb[t], alg_edge, alg_node, k);
+    } else {
+      int32_t v = pa[t], e = pb[t];
+      for (int32_t q = rp_n[v]; q < rp_n[v + 1]; q++) {
+        float pe = same_type_prob(rp_e, col_e, e, col_n[q], alg_edge, alg_node, k);
+        if (pe > p) p = pe;
+      }
+    }
+    out[t] = p;
+  }
+}
+
+/* ------------------------------------------------------------------------- */
+/* HOBE: AlgebraicDistanceSamples (hg2v_sample.py:632-717),                   */
+/* run_in_parallel=False semantics: pair draws in the parent; the ne         */
+/* neighbour draws happen in the single forked Pool worker, i.e. they        */
+/* continue from a COPY of the parent RNG state after the last pair draw,    */
+/* in record order (:604-605); the parent state is not advanced by them.     */
+/* ------------------------------------------------------------------------- */
+int64_t hgref_hobe_sample(hgref_rng *s, int64_t N, int64_t E,
+                          const int32_t *rp_n, const int32_t *col_n,
+                          const int32_t *rp_e, const int32_t *col_e,
+                          const float *alg_node, const float *alg_edge, int k,
+                          int S, int K, int64_t cap, int32_t *idx, float *tgt) {
+  recbuf rb = {K, 0, cap, idx, tgt};
+  pat A = pat_view(N, rp_n, col_n), AT = pat_view(E, rp_e, col_e);
+  pairs P = {0, 0, NULL, NULL};
+  int64_t overflow = 0;
+  float pr;
+
+  pat NN = spgemm_pattern(N, A.p, A.j, N, AT.p, AT.j);           /* :659 */
+  sample_pattern(s, &NN, N, NULL, S, 0, &P, 0);
+  pat_free(&NN);
+  for (int64_t t = 0; t < P.n; t++) {
+    int32_t *r = rec_slot(&rb);
+    if (!r) { overflow = 1; break; }
+    hgref_hobe_probs(0, 1, P.a + t, P.b + t, rp_n, col_n, rp_e, col_e,
+                     alg_node, alg_edge, k, &pr);
+    r[0] = P.a[t] + 1; r[2] = P.b[t] + 1; rb.tgt[rb.n * 3 + 0] = pr; rb.n++;
+  }
+  P.n = 0;
+  pat EE = spgemm_pattern(E, AT.p, AT.j, E, A.p, A.j);           /* :679 */
+  sample_pattern(s, &EE, E, NULL, S, 0, &P, 0);
+  pat_free(&EE);
+  for (int64_t t = 0; t < P.n; t++) {
+    int32_t *r = rec_slot(&rb);
+    if (!r) { overflow = 1; break; }
+    hgref_hobe_probs(1, 1, P.a + t, P.b + t, rp_n, col_n, rp_e, col_e,
+                     alg_node, alg_edge, k, &pr);
+    r[1] = P.a[t] + 1; r[3] = P.b[t] + 1; rb.tgt[rb.n * 3 + 1] = pr; rb.n++;
+  }
+  P.n = 0;
+  pat NN2 = spgemm_pattern(N, A.p, A.j, N, AT.p, AT.j);
+  pat NNE = spgemm_pattern(N, NN2.p, NN2.j, E, A.p, A.j);        /* :698 */
+  pat_free(&NN2);
+  sample_pattern(s, &NNE, E, NULL, S, 0, &P, 0);
+  pat_free(&NNE);
+  pat EE2 = spgemm_pattern(E, AT.p, AT.j, E, A.p, A.j);
+  pat EEN = spgemm_pattern(E, EE2.p, EE2.j, N, AT.p, AT.j);      /* :703 */
+  pat_free(&EE2);
+  sample_pattern(s, &EEN, N, NULL, S, 0, &P, 1);
+  pat_free(&EEN);
+  hgref_rng w;  /* forked worker's copy */
+  hgref_rng_copy(&w, s);
+  for (int64_t t = 0; t < P.n; t++) {
+    int32_t v = P.a[t], e = P.b[t];
+    int32_t *r = rec_slot(&rb);
+    if (!r) { overflow = 1; break; }
+    r[0] = v + 1; r[3] = e + 1;
+    sample_neighbors(&w, A.j + A.p[v], A.p[v + 1] - A.p[v], K, r + 4 + K);
+    sample_neighbors(&w, AT.j + AT.p[e], AT.p[e + 1] - AT.p[e], K, r + 4);
+    hgref_hobe_probs(2, 1, &v, &e, rp_n, col_n, rp_e, col_e, alg_node,
+                     alg_edge, k, &pr);
+    rb.tgt[rb.n * 3 + 2] = pr;
+    rb.n++;
+  }
+  free(P.a); free(P.b);
+  pat_free(&A); pat_free(&AT);
+  return overflow ? -1 : rb.n;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Trainer: BooleanModel (hg2v_model.py:51-125, sigmoid heads + KLD) and      */
+/* UnweightedFloatModel (:129-203, relu heads + MSE), fit loop of            */
+/* embedding.py:269-305 -- Keras 2.x semantics restated (PARITY UNPINNED:    */
+/* keras/tensorflow are absent):                                             */
+/*   heads nn = act(N[ln].N[rn]), ee = act(E[le].E[re]),                      */
+/*         ne = mean_k act(N[nn_k].N[ln]) * mean_k act(E[ne_k].E[re]);       */
+/*   loss = sum over heads of batch-mean; KLD = yt'*log(yt'/yp') with         */
+/*   clip(.,eps,1); MSE = (yp-yt)^2;                                          */
+/*   Adagrad: a += g^2; p -= lr*g/(sqrt(a)+eps), duplicate rows summed.       */
+/* perms: n_epochs x n permutation (Keras np.random.shuffle per epoch) or    */
+/* NULL for in-order. EarlyStopping(monitor=loss, min_delta, patience=0).    */
+/* ------------------------------------------------------------------------- */
+static float act_f(int act, float z) {
+  if (act == 0) return 1.0f / (1.0f + expf(-z));
+  return z > 0.0f ? z : 0.0f;
+}
+static float act_d(int act, float z, float y) {
+  if (act == 0) return y * (1.0f - y);
+  return z > 0.0f ? 1.0f : 0.0f;
+}
+static float dot_f(const float *a, const float *b, int d) {
+  float s = 0.0f;
+  for (int i = 0; i < d; i++) s += a[i] * b[i];
+  return s;
+}
+
+/* per-head loss value and dL/dyhat for ONE sample (not yet / batch) */
+static void head_loss(int loss, float y, float yt, float *lv, float *g) {
+  const float eps = 1e-7f;
+  if (loss == 0) {
+    float ytc = yt < eps ? eps : (yt > 1.0f ? 1.0f : yt);
+    float ypc = y < eps ? eps : (y > 1.0f ? 1.0f : y);
+    *lv = ytc * logf(ytc / ypc);
+    *g = (y >= eps && y <= 1.0f) ? -ytc / ypc : 0.0f;
+  } else {
+    float df = y - yt;
+    *lv = df * df;
+    *g = 2.0f * df;
+  }
+}
+
+int hgref_train(int64_t n, int K, const int32_t *idx, const float *tgt, int d,
+                int64_t n_node_rows, int64_t n_edge_rows, float *ntab,
+                float *etab, float *nacc, float *eacc, int loss, int act,
+                int batch, float lr, float eps, int max_epochs,
+                const int64_t *perms, float min_delta, float *epoch_loss,
+                int *epochs_run) {
+  int R = 4 + 2 * K;
+  float *gn = (float *)calloc((size_t)n_node_rows * d, sizeof(float));
+  float *ge = (float *)calloc((size_t)n_edge_rows * d, sizeof(float));
+  char *tn = (char *)calloc((size_t)n_node_rows, 1);
+  char *te = (char *)calloc((size_t)n_edge_rows, 1);
+  int64_t *touched_n = (int64_t *)malloc(sizeof(int64_t) * (size_t)batch * R + 8);
+  int64_t *touched_e = (int64_t *)malloc(sizeof(int64_t) * (size_t)batch * R + 8);
+  float *a_k = (float *)malloc(sizeof(float) * (K + 1));
+  float *b_k = (float *)malloc(sizeof(float) * (K + 1));
+  float *sa = (float *)malloc(sizeof(float) * (K + 1));
+  float *sb = (float *)malloc(sizeof(float) * (K + 1));
+  double best = INFINITY;
+  int ep;
+  for (ep = 0; ep < max_epochs; ep++) {
+    const int64_t *perm = perms ? perms + (int64_t)ep * n : NULL;
+    double loss_sum = 0.0;
+    for (int64_t b0 = 0; b0 < n; b0 += batch) {
+      int64_t b1 = b0 + batch < n ? b0 + batch : n;
+      float inv_b = 1.0f / (float)(b1 - b0);
+      int64_t ntn = 0, nte = 0;
+      double bl = 0.0;
+      for (int64_t q = b0; q < b1; q++) {
+        int64_t rec = perm ? perm[q] : q;
+        const int32_t *r = idx + rec * R;
+        const float *yt = tgt + rec * 3;
+        int32_t ln = r[0], le = r[1], rn = r[2], re = r[3];
+        const int32_t *nnk = r + 4, *nek = r + 4 + K;
+        const float *Nl = ntab + (int64_t)ln * d, *Nr = ntab + (int64_t)rn * d;
+        const float *El = etab + (int64_t)le * d, *Er = etab + (int64_t)re * d;
+        float z1 = dot_f(Nl, Nr, d), y1 = act_f(act, z1);
+        float z2 = dot_f(El, Er, d), y2 = act_f(act, z2);
+        float P = 0.0f, Q = 0.0f;
+        for (int t = 0; t < K; t++) {
+          a_k[t] = dot_f(ntab + (int64_t)nnk[t] * d, Nl, d);
+          sa[t] = act_f(act, a_k[t]);
+          P += sa[t];
+          b_k[t] = dot_f(etab + (int64_t)nek[t] * d, Er, d);
+          sb[t] = act_f(act, b_k[t]);
+          Q += sb[t];
+        }
+        P = P / (float)K;
+        Q = Q / (float)K;
+        float y3 = P * Q;
+        float l1, l2, l3, g1, g2, g3;
+        head_loss(loss, y1, yt[0], &l1, &g1);
+        head_loss(loss, y2, yt[1], &l2, &g2);
+        head_loss(loss, y3, yt[2], &l3, &g3);
+        bl += (double)l1 + (double)l2 + (double)l3;
+        g1 *= inv_b; g2 *= inv_b; g3 *= inv_b;
+        float dz1 = g1 * act_d(act, z1, y1);
+        float dz2 = g2 * act_d(act, z2, y2);
+        float dP = g3 * Q / (float)K, dQ = g3 * P / (float)K;
+#define TOUCH_N(row) do { if (!tn[row]) { tn[row] = 1; touched_n[ntn++] = row; } } while (0)
+#define TOUCH_E(row) do { if (!te[row]) { te[row] = 1; touched_e[nte++] = row; } } while (0)
+        float *gl = gn + (int64_t)ln * d, *gr = gn + (int64_t)rn * d;
+        TOUCH_N(ln); TOUCH_N(rn);
+        for (int i = 0; i < d; i++) { gl[i] += dz1 * Nr[i]; gr[i] += dz1 * Nl[i]; }
+        float *hl = ge + (int64_t)le * d, *hr = ge + (int64_t)re * d;
+        TOUCH_E(le); TOUCH_E(re);
+        for (int i = 0; i < d; i++) { hl[i] += dz2 * Er[i]; hr[i] += dz2 * El[i]; }
+        for (int t = 0; t < K; t++) {
+          float da = dP * act_d(act, a_k[t], sa[t]);
+          float *gk = gn + (int64_t)nnk[t] * d;
+          const float *Nk = ntab + (int64_t)nnk[t] * d;
+          TOUCH_N(nnk[t]);
+          for (int i = 0; i < d; i++) { gk[i] += da * Nl[i]; gl[i] += da * Nk[i]; }
+          float db = dQ * act_d(act, b_k[t], sb[t]);
+          float *hk = ge + (int64_t)nek[t] * d;
+          const float *Ek = etab + (int64_t)nek[t] * d;
+          TOUCH_E(nek[t]);
+          for (int i = 0; i < d; i++) { hk[i] += db * Er[i]; hr[i] += db * Ek[i]; }
+        }
+      }
+      /* Adagrad over touched rows (untouched rows have g == 0: no-op). */
+      for (int64_t u = 0; u < ntn; u++) {
+        int64_t row = touched_n[u];
+        float *p = ntab + row * d, *a = nacc + row * d, *g = gn + row * d;
+        for (int i = 0; i < d; i++) {
+          float na = a[i] + g[i] * g[i];
+          a[i] = na;
+          p[i] = p[i] - (lr * g[i]) / (sqrtf(na) + eps);
+          g[i] = 0.0f;
+        }
+        tn[row] = 0;
+      }
+      for (int64_t u = 0; u < nte; u++) {
+        int64_t row = touched_e[u];
+        float *p = etab + row * d, *a = eacc + row * d, *g = ge + row * d;
+        for (int i = 0; i < d; i++) {
+          float na = a[i] + g[i] * g[i];
+          a[i] = na;
+          p[i] = p[i] - (lr * g[i]) / (sqrtf(na) + eps);
+          g[i] = 0.0f;
+        }
+        te[row] = 0;
+      }
+      loss_sum += bl;  /* = batch_mean * batch_size summed (BaseLogger) */
+    }
+    double cur = loss_sum / (double)n;
+    if (epoch_loss) epoch_loss[ep] = (float)cur;
+    if (cur < best - (double)min_delta) {
+      best = cur;
+    } else {
+      ep++;
+      break;
+    }
+  }
+  if (epochs_run) *epochs_run = ep;
+  free(gn); free(ge); free(tn); free(te); free(touched_n); free(touched_e);
+  free(a_k); free(b_k); free(sa); free(sb);
+  return 0;
+}

@@ -1,0 +1,214 @@
+"""ctypes/numpy front-end of the CPU oracle (oracle/hgref.c).
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the CHECKER or the timed CPU baseline, never by
+the product package. See hgref.c for the reference file:line each routine
+restates and for the parity-pinning status (trainer: parity unpinned).
+"""
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+
+
+def build():
+  src = os.path.join(_HERE, "hgref.c")
+  if (not os.path.exists(_LIB_PATH) or
+      os.path.getmtime(_LIB_PATH) < os.path.getmtime(src)):
+    subprocess.run(["make", "-C", _HERE, "-s"], check=True)
+  return _LIB_PATH
+
+
+def lib():
+  global _lib
+  if _lib is None:
+    build()
+    L = ctypes.CDLL(_LIB_PATH)
+    L.hgref_rng_create.restype = _vp
+    L.hgref_rng_create.argtypes = [ctypes.c_uint32]
+    L.hgref_rng_destroy.argtypes = [_vp]
+    L.hgref_rng_copy.argtypes = [_vp, _vp]
+    L.hgref_rng_next32.restype = ctypes.c_uint32
+    L.hgref_rng_next32.argtypes = [_vp]
+    L.hgref_rng_random.argtypes = [_vp, _i64, _f64p]
+    L.hgref_rng_randint.restype = _i64
+    L.hgref_rng_randint.argtypes = [_vp, _i64]
+    L.hgref_rng_permutation.argtypes = [_vp, _i64, _i64p]
+    L.hgref_spgemm.restype = _i64
+    L.hgref_spgemm.argtypes = [_i64, _i32p, _i32p, _i64, _i64, _i32p, _i32p,
+                               _vp, _vp]
+    L.hgref_algdist.restype = _int
+    L.hgref_algdist.argtypes = [_i64, _i64, _int, _int, _i32p, _i32p, _i32p,
+                                _i32p, _f64p, _f64p]
+    L.hgref_fobe_sample.restype = _i64
+    L.hgref_fobe_sample.argtypes = [_vp, _i64, _i64, _i32p, _i32p, _i32p,
+                                    _i32p, _i32p, _i32p, _vp, _vp, _int, _i64,
+                                    _i32p, _f32p]
+    L.hgref_hobe_sample.restype = _i64
+    L.hgref_hobe_sample.argtypes = [_vp, _i64, _i64, _i32p, _i32p, _i32p,
+                                    _i32p, _f32p, _f32p, _int, _int, _int, _i64,
+                                    _i32p, _f32p]
+    L.hgref_hobe_probs.argtypes = [_int, _i64, _i32p, _i32p, _i32p, _i32p,
+                                   _i32p, _i32p, _f32p, _f32p, _int, _f32p]
+    L.hgref_dist_weight.restype = ctypes.c_float
+    L.hgref_dist_weight.argtypes = [_f32p, _f32p, _int]
+    L.hgref_train.restype = _int
+    L.hgref_train.argtypes = [_i64, _int, _i32p, _f32p, _int, _i64, _i64,
+                              _f32p, _f32p, _f32p, _f32p, _int, _int, _int,
+                              ctypes.c_float, ctypes.c_float, _int, _vp,
+                              ctypes.c_float, _f32p,
+                              ctypes.POINTER(ctypes.c_int)]
+    _lib = L
+  return _lib
+
+
+class Rng:
+  """numpy legacy RandomState(seed) stream (MT19937), restated in C."""
+
+  def __init__(self, seed):
+    self.h = lib().hgref_rng_create(seed & 0xFFFFFFFF)
+
+  def __del__(self):
+    if getattr(self, "h", None) and _lib is not None:
+      _lib.hgref_rng_destroy(self.h)
+      self.h = None
+
+  def next32(self):
+    return lib().hgref_rng_next32(self.h)
+
+  def random(self, shape):
+    out = np.empty(int(np.prod(shape)), dtype=np.float64)
+    lib().hgref_rng_random(self.h, out.size, out)
+    return out.reshape(shape)
+
+  def randint(self, n):
+    return lib().hgref_rng_randint(self.h, n)
+
+  def permutation(self, n):
+    out = np.empty(n, dtype=np.int64)
+    lib().hgref_rng_permutation(self.h, n, out)
+    return out
+
+
+def spgemm(ap, aj, nrow_b, ncol_b, bp, bj):
+  """Pattern of A*B with scipy's SMMP column order: (indptr int64, indices)."""
+  ap = np.ascontiguousarray(ap, np.int32)
+  aj = np.ascontiguousarray(aj, np.int32)
+  bp = np.ascontiguousarray(bp, np.int32)
+  bj = np.ascontiguousarray(bj, np.int32)
+  nrow = ap.size - 1
+  nnz = lib().hgref_spgemm(nrow, ap, aj, nrow_b, ncol_b, bp, bj, None, None)
+  outp = np.empty(nrow + 1, np.int64)
+  outj = np.empty(max(nnz, 1), np.int32)
+  lib().hgref_spgemm(nrow, ap, aj, nrow_b, ncol_b, bp, bj,
+                     outp.ctypes.data, outj.ctypes.data)
+  return outp, outj[:nnz]
+
+
+def algdist(inc, x, y, iters):
+  """In-place float64 relaxation; returns (x, y). Raises ZeroDivisionError on
+  an isolated row like algebraic_distance.py:49."""
+  x = np.ascontiguousarray(x, np.float64).copy()
+  y = np.ascontiguousarray(y, np.float64).copy()
+  k = x.shape[1]
+  rc = lib().hgref_algdist(inc.N, inc.E, k, iters, inc.rp_n, inc.col_n,
+                           inc.rp_e, inc.col_e, x, y)
+  if rc != 0:
+    raise ZeroDivisionError("isolated node or edge in algebraic distance")
+  return x, y
+
+
+def _q(a):
+  return None if a is None else np.ascontiguousarray(a, np.int32)
+
+
+def fobe_sample(rng, inc, node_q, edge_q, K, neg_node_q=None, neg_edge_q=None):
+  """BooleanSamples -> SamplesToModelInput arrays (idx (n,4+2K), tgt (n,3))."""
+  node_q, edge_q = _q(node_q), _q(edge_q)
+  nnq, neq = _q(neg_node_q), _q(neg_edge_q)
+  cap = 2 * int(node_q.sum()) + 2 * int(edge_q.sum()) + 1
+  if nnq is not None:
+    cap += int(nnq.sum()) * 2 + int(neq.sum()) * 3
+  idx = np.zeros((cap, 4 + 2 * K), np.int32)
+  tgt = np.zeros((cap, 3), np.float32)
+  n = lib().hgref_fobe_sample(
+      rng.h, inc.N, inc.E, inc.rp_n, inc.col_n, inc.rp_e, inc.col_e, node_q,
+      edge_q, None if nnq is None else nnq.ctypes.data,
+      None if neq is None else neq.ctypes.data, K, cap, idx, tgt)
+  assert n >= 0
+  return idx[:n].copy(), tgt[:n].copy()
+
+
+def hobe_sample(rng, inc, alg_node, alg_edge, S, K):
+  """AlgebraicDistanceSamples (run_in_parallel=False) -> model input arrays."""
+  alg_node = np.ascontiguousarray(alg_node, np.float32)
+  alg_edge = np.ascontiguousarray(alg_edge, np.float32)
+  cap = 2 * S * (inc.N + inc.E) + 1
+  idx = np.zeros((cap, 4 + 2 * K), np.int32)
+  tgt = np.zeros((cap, 3), np.float32)
+  n = lib().hgref_hobe_sample(rng.h, inc.N, inc.E, inc.rp_n, inc.col_n,
+                              inc.rp_e, inc.col_e, alg_node, alg_edge,
+                              alg_node.shape[1], S, K, cap, idx, tgt)
+  assert n >= 0
+  return idx[:n].copy(), tgt[:n].copy()
+
+
+HOBE_NN, HOBE_EE, HOBE_NE = 0, 1, 2
+
+
+def hobe_probs(kind, a, b, inc, alg_node, alg_edge):
+  a = np.ascontiguousarray(a, np.int32)
+  b = np.ascontiguousarray(b, np.int32)
+  alg_node = np.ascontiguousarray(alg_node, np.float32)
+  alg_edge = np.ascontiguousarray(alg_edge, np.float32)
+  out = np.empty(a.size, np.float32)
+  lib().hgref_hobe_probs(kind, a.size, a, b, inc.rp_n, inc.col_n, inc.rp_e,
+                         inc.col_e, alg_node, alg_edge, alg_node.shape[1], out)
+  return out
+
+
+LOSS_KLD, LOSS_MSE = 0, 1
+ACT_SIGMOID, ACT_RELU = 0, 1
+
+
+def train(idx, tgt, K, node_tab, edge_tab, loss, act, batch=256, lr=0.01,
+          eps=1e-7, max_epochs=10, perms=None, min_delta=1e-3, node_acc=None,
+          edge_acc=None):
+  """Keras-semantics Adagrad restatement. Tables are float32 (rows = max+2,
+  row 0 = padding). Returns (node_tab, edge_tab, epoch_losses)."""
+  idx = np.ascontiguousarray(idx, np.int32)
+  tgt = np.ascontiguousarray(tgt, np.float32)
+  nt = np.ascontiguousarray(node_tab, np.float32).copy()
+  et = np.ascontiguousarray(edge_tab, np.float32).copy()
+  na = (np.zeros_like(nt) if node_acc is None
+        else np.ascontiguousarray(node_acc, np.float32).copy())
+  ea = (np.zeros_like(et) if edge_acc is None
+        else np.ascontiguousarray(edge_acc, np.float32).copy())
+  n = idx.shape[0]
+  d = nt.shape[1]
+  pp = None
+  if perms is not None:
+    perms = np.ascontiguousarray(perms, np.int64)
+    assert perms.shape[1] == n and perms.shape[0] >= 1
+    max_epochs = min(max_epochs, perms.shape[0])
+    pp = perms.ctypes.data
+  losses = np.zeros(max(max_epochs, 1), np.float32)
+  ran = ctypes.c_int(0)
+  lib().hgref_train(n, K, idx, tgt, d, nt.shape[0], et.shape[0], nt, et, na,
+                    ea, loss, act, batch, lr, eps, max_epochs, pp, min_delta,
+                    losses, ctypes.byref(ran))
+  return nt, et, losses[:ran.value].copy(), na, ea
