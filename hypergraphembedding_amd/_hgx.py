@@ -1,0 +1,289 @@
+"""ctypes binding of libhgx.so (include/hgx.h) -- the only way the package
+reaches the GPU. There is no CPU fallback: if the library or a HIP device is
+missing, every entry point raises.
+"""
+
+import ctypes
+import os
+import re
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhgx.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "hgx.h")
+
+HGX_OK, HGX_EINVAL, HGX_EHIP, HGX_ENOMEM = 0, -1, -2, -3
+HGX_EZERODIV, HGX_ESTATE, HGX_EUNSUP = -4, -5, -6
+LOSS_KLD, LOSS_MSE = 0, 1
+ACT_SIGMOID, ACT_RELU = 0, 1
+HOBE_NN, HOBE_EE, HOBE_NE = 0, 1, 2
+WEIGHT_UNIFORM, WEIGHT_NEIGHBORHOOD, WEIGHT_DISTANCE = 0, 1, 2
+
+_lib = None
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_u64 = ctypes.c_uint64
+_int = ctypes.c_int
+_f32 = ctypes.c_float
+_pi64 = ctypes.POINTER(ctypes.c_int64)
+_pint = ctypes.POINTER(ctypes.c_int)
+_pdbl = ctypes.POINTER(ctypes.c_double)
+
+# name -> (restype, argtypes); mirrors include/hgx.h one to one.
+SIGNATURES = {
+    "hgx_create": (_int, [_int, ctypes.POINTER(_vp)]),
+    "hgx_destroy": (_int, [_vp]),
+    "hgx_last_error": (ctypes.c_char_p, [_vp]),
+    "hgx_version": (_int, []),
+    "hgx_set_stream": (_int, [_vp, _vp]),
+    "hgx_synchronize": (_int, [_vp]),
+    "hgx_upload_incidence": (_int, [_vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]),
+    "hgx_alg_dist": (_int, [_vp, _int, _int, _vp, _vp]),
+    "hgx_alg_set": (_int, [_vp, _int, _vp, _vp]),
+    "hgx_alg_run": (_int, [_vp, _int]),
+    "hgx_alg_get": (_int, [_vp, _vp, _vp]),
+    "hgx_alg_last_stats": (_int, [_vp, _pdbl, _pdbl]),
+    "hgx_alg_shard_begin": (_int, [_vp, _i32, _i32, _vp, _vp, _int, _pint]),
+    "hgx_alg_shard_node": (_int, [_vp, _int]),
+    "hgx_alg_shard_edge_partial": (_int, [_vp, _int]),
+    "hgx_alg_shard_edge_final": (_int, [_vp, _int]),
+    "hgx_alg_shard_end": (_int, [_vp]),
+    "hgx_hobe_probs": (_int, [_vp, _int, _i64, _vp, _vp, _vp]),
+    "hgx_incidence_weights": (_int, [_vp, _int, ctypes.c_double, _vp, _vp]),
+    "hgx_sample_fobe": (_int, [_vp, _u64, _int, _vp, _vp, _vp, _vp, _pi64]),
+    "hgx_sample_hobe": (_int, [_vp, _u64, _int, _int, _pi64]),
+    "hgx_records_set": (_int, [_vp, _i64, _int, _vp, _vp]),
+    "hgx_records_info": (_int, [_vp, _pi64, _pint]),
+    "hgx_records_get": (_int, [_vp, _vp, _vp]),
+    "hgx_model_init": (_int, [_vp, _int, _i64, _i64, _u64, _vp, _vp]),
+    "hgx_model_get": (_int, [_vp, _vp, _vp]),
+    "hgx_train": (_int, [_vp, _int, _int, _f32, _f32, _int, _int, _f32, _u64,
+                         _vp, _vp, _pint]),
+    "hgx_train_last_stats": (_int, [_vp, _pdbl, _pi64, _pi64]),
+}
+
+
+def header_symbols():
+  """Function names declared in include/hgx.h."""
+  with open(HEADER) as f:
+    text = f.read()
+  text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+  return sorted(set(re.findall(r"\b(hgx_[a-z0-9_]+)\s*\(", text)))
+
+
+def lib():
+  """Load libhgx.so (raises if it was not built)."""
+  global _lib
+  if _lib is None:
+    if not os.path.exists(LIB_PATH):
+      raise ImportError(
+          f"{LIB_PATH} missing: run hypergraphembedding_amd.build.build() "
+          "(there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+      fn = getattr(L, name)
+      fn.restype = res
+      fn.argtypes = args
+    _lib = L
+  return _lib
+
+
+class HgxError(RuntimeError):
+  pass
+
+
+def _raise(rc, msg):
+  if rc == HGX_EINVAL:
+    raise AssertionError(msg)
+  if rc == HGX_EZERODIV:
+    raise ZeroDivisionError(msg)
+  raise HgxError(f"libhgx error {rc}: {msg}")
+
+
+def _ptr(a):
+  return None if a is None else a.ctypes.data
+
+
+def _c(a, dtype):
+  return None if a is None else np.ascontiguousarray(a, dtype=dtype)
+
+
+class Context:
+  """One device context (owns device memory and one HIP stream)."""
+
+  def __init__(self, device=0):
+    h = _vp()
+    rc = lib().hgx_create(device, ctypes.byref(h))
+    if rc != HGX_OK:
+      _raise(rc, f"hgx_create(device={device}) failed: no usable HIP device")
+    self.h = h
+    self.device = device
+
+  def close(self):
+    if getattr(self, "h", None):
+      lib().hgx_destroy(self.h)
+      self.h = None
+
+  def __del__(self):
+    try:
+      self.close()
+    except Exception:
+      pass
+
+  def _chk(self, rc):
+    if rc != HGX_OK:
+      _raise(rc, lib().hgx_last_error(self.h).decode(errors="replace"))
+
+  # ---- plumbing ----
+  def set_stream(self, stream_ptr):
+    self._chk(lib().hgx_set_stream(self.h, stream_ptr))
+
+  def synchronize(self):
+    self._chk(lib().hgx_synchronize(self.h))
+
+  # ---- incidence ----
+  def upload(self, inc):
+    self.inc = inc
+    self._keep = (_c(inc.rp_n, np.int32), _c(inc.col_n, np.int32),
+                  _c(inc.rp_e, np.int32), _c(inc.col_e, np.int32))
+    a, b, c, d = self._keep
+    self._chk(lib().hgx_upload_incidence(self.h, inc.N, inc.E, inc.nnz,
+                                         _ptr(a), _ptr(b), _ptr(c), _ptr(d)))
+
+  # ---- algebraic distance ----
+  def alg_set(self, x, y):
+    x = _c(x, np.float32)
+    y = _c(y, np.float32)
+    assert x.ndim == 2 and y.ndim == 2 and x.shape[1] == y.shape[1]
+    self.k = x.shape[1]
+    self._chk(lib().hgx_alg_set(self.h, self.k, _ptr(x), _ptr(y)))
+
+  def alg_run(self, iters):
+    self._chk(lib().hgx_alg_run(self.h, iters))
+
+  def alg_get(self):
+    x = np.empty((self.inc.N, self.k), np.float32)
+    y = np.empty((self.inc.E, self.k), np.float32)
+    self._chk(lib().hgx_alg_get(self.h, _ptr(x), _ptr(y)))
+    return x, y
+
+  def alg_dist(self, x, y, iters):
+    self.alg_set(x, y)
+    self.alg_run(iters)
+    return self.alg_get()
+
+  def alg_stats(self):
+    ms, by = ctypes.c_double(), ctypes.c_double()
+    self._chk(lib().hgx_alg_last_stats(self.h, ctypes.byref(ms),
+                                       ctypes.byref(by)))
+    return ms.value, by.value
+
+  # sharded relaxation (exchange buffers are caller-owned device pointers)
+  def alg_shard_begin(self, row0, row1, d_partial, d_mm, iters):
+    ks = ctypes.c_int()
+    self._chk(lib().hgx_alg_shard_begin(self.h, row0, row1, d_partial, d_mm,
+                                        iters, ctypes.byref(ks)))
+    return ks.value
+
+  def alg_shard_node(self, it):
+    self._chk(lib().hgx_alg_shard_node(self.h, it))
+
+  def alg_shard_edge_partial(self, it):
+    self._chk(lib().hgx_alg_shard_edge_partial(self.h, it))
+
+  def alg_shard_edge_final(self, it):
+    self._chk(lib().hgx_alg_shard_edge_final(self.h, it))
+
+  def alg_shard_end(self):
+    self._chk(lib().hgx_alg_shard_end(self.h))
+
+  # ---- HOBE probabilities / incidence weights ----
+  def hobe_probs(self, kind, a, b):
+    a = _c(a, np.int32)
+    b = _c(b, np.int32)
+    out = np.empty(a.size, np.float32)
+    self._chk(lib().hgx_hobe_probs(self.h, kind, a.size, _ptr(a), _ptr(b),
+                                   _ptr(out)))
+    return out
+
+  def incidence_weights(self, which, alpha=0.0):
+    n = np.empty(self.inc.nnz, np.float32)
+    e = np.empty(self.inc.nnz, np.float32)
+    self._chk(lib().hgx_incidence_weights(self.h, which, alpha, _ptr(n),
+                                          _ptr(e)))
+    return n, e
+
+  # ---- samplers / records ----
+  def sample_fobe(self, seed, K, node_q, edge_q, neg_node_q=None,
+                  neg_edge_q=None):
+    nq, eq = _c(node_q, np.int32), _c(edge_q, np.int32)
+    nnq, neq = _c(neg_node_q, np.int32), _c(neg_edge_q, np.int32)
+    n = ctypes.c_int64()
+    self._chk(lib().hgx_sample_fobe(self.h, seed & (2**64 - 1), K, _ptr(nq),
+                                    _ptr(eq), _ptr(nnq), _ptr(neq),
+                                    ctypes.byref(n)))
+    return n.value
+
+  def sample_hobe(self, seed, K, S):
+    n = ctypes.c_int64()
+    self._chk(lib().hgx_sample_hobe(self.h, seed & (2**64 - 1), K, S,
+                                    ctypes.byref(n)))
+    return n.value
+
+  def records_set(self, idx, tgt):
+    idx = _c(idx, np.int32)
+    tgt = _c(tgt, np.float32)
+    n, R = idx.shape
+    assert R % 2 == 0 and R >= 4 and tgt.shape == (n, 3)
+    self._chk(lib().hgx_records_set(self.h, n, (R - 4) // 2, _ptr(idx),
+                                    _ptr(tgt)))
+
+  def records_info(self):
+    n, K = ctypes.c_int64(), ctypes.c_int()
+    self._chk(lib().hgx_records_info(self.h, ctypes.byref(n), ctypes.byref(K)))
+    return n.value, K.value
+
+  def records_get(self):
+    n, K = self.records_info()
+    idx = np.empty((n, 4 + 2 * K), np.int32)
+    tgt = np.empty((n, 3), np.float32)
+    self._chk(lib().hgx_records_get(self.h, _ptr(idx), _ptr(tgt)))
+    return idx, tgt
+
+  # ---- model / trainer ----
+  def model_init(self, d, node_rows, edge_rows, seed=0, node_tab=None,
+                 edge_tab=None):
+    nt, et = _c(node_tab, np.float32), _c(edge_tab, np.float32)
+    if nt is not None:
+      assert nt.shape == (node_rows, d) and et.shape == (edge_rows, d)
+    self.d, self.node_rows, self.edge_rows = d, node_rows, edge_rows
+    self._chk(lib().hgx_model_init(self.h, d, node_rows, edge_rows,
+                                   seed & (2**64 - 1), _ptr(nt), _ptr(et)))
+
+  def model_get(self):
+    nt = np.empty((self.node_rows, self.d), np.float32)
+    et = np.empty((self.edge_rows, self.d), np.float32)
+    self._chk(lib().hgx_model_get(self.h, _ptr(nt), _ptr(et)))
+    return nt, et
+
+  def train(self, batch=256, max_epochs=10, lr=0.01, eps=1e-7, loss=LOSS_MSE,
+            act=ACT_RELU, min_delta=1e-3, shuffle_seed=0, perms=None):
+    pp = None
+    if perms is not None:
+      pp = _c(perms, np.int64)
+      max_epochs = min(max_epochs, pp.shape[0])
+    losses = np.zeros(max(max_epochs, 1), np.float32)
+    ran = ctypes.c_int()
+    self._chk(lib().hgx_train(self.h, batch, max_epochs, lr, eps, loss, act,
+                              min_delta, shuffle_seed & (2**64 - 1), _ptr(pp),
+                              _ptr(losses), ctypes.byref(ran)))
+    return losses[:ran.value].copy()
+
+  def train_stats(self):
+    ms, rec, bat = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+    self._chk(lib().hgx_train_last_stats(self.h, ctypes.byref(ms),
+                                         ctypes.byref(rec), ctypes.byref(bat)))
+    return ms.value, rec.value, bat.value

@@ -1,0 +1,735 @@
+// Algebraic-distance relaxation on MI355X.
+//
+// Reference: algebraic_distance.py:126-175 (driver), 34-51 (_update_alg_dist:
+// weighted mean of neighbour coords, weight 1/deg(neighbour), averaged with
+// self), 54-91 (node half, then edge half on the NEW node coords), 97-123
+// (joint per-dim min-max rescale of nodes and edges to [0,1]).
+//
+// HBM layout: coordinates live in rows of KS = round_up(k+1, 4) fp32,
+//   row = [w, c_0 .. c_{k-1}, pad]  with w = 1/len(own CSR row),
+// so the gather of a source row brings its weight in the same 16-byte
+// vectors (no separate random 4-byte load per incidence).
+//
+// Rescale fusion: iteration t writes RAW values and folds their per-dim
+// min/max into mm[t] (order-preserving int32 atomicMax, one set of 2k
+// atomics per workgroup). Iteration t+1 applies s_t(z) = (z - min_t) /
+// (max_t - min_t) when it reads: self rows always; the node half's gathered
+// edge rows as s_t(weighted mean) (the mean is affine); the edge half
+// gathers the NEW node rows unscaled, exactly like the reference. A final
+// pass applies the last affine in place.
+//
+// Sharded mode: rank g owns node rows [row0,row1). Per
+// iteration: node half on own rows -> edge PARTIAL sums over own nodes
+// (local edge sub-CSR, slot 0 = sum of weights) -> caller all-reduces the
+// E x KS partial (SUM) -> edge FINAL on all edges -> caller all-reduces the
+// 2*KS min/max words (MAX).
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "hgx_internal.h"
+
+using hgx::f2ord;
+using hgx::ord2f;
+
+namespace {
+
+constexpr int kBlock = 256;
+enum { MODE_FULL = 0, MODE_PARTIAL = 1 };
+
+__device__ __forceinline__ float4 f4fma(float w, float4 v, float4 a) {
+  return make_float4(fmaf(w, v.x, a.x), fmaf(w, v.y, a.y), fmaf(w, v.z, a.z),
+                     fmaf(w, v.w, a.w));
+}
+__device__ __forceinline__ float f4get(const float4 &v, int c) {
+  return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
+}
+__device__ __forceinline__ void f4set(float4 &v, int c, float x) {
+  if (c == 0) v.x = x;
+  else if (c == 1) v.y = x;
+  else if (c == 2) v.z = x;
+  else v.w = x;
+}
+
+// min and delta of the previous iteration's rescale for slot i (identity
+// when there is none).
+__device__ __forceinline__ void affine_of(const int *mm_prev, int KS, int i,
+                                          float &m, float &dl) {
+  if (mm_prev) {
+    m = ord2f(~mm_prev[KS + i]);
+    dl = ord2f(mm_prev[i]) - m;
+  } else {
+    m = 0.f;
+    dl = 1.f;
+  }
+}
+
+template <int KS>
+__device__ __forceinline__ void load_affine(const int *mm_prev, int k,
+                                            float *s_m, float *s_d) {
+  const int tid = threadIdx.x;
+  if (tid < KS) {
+    float m = 0.f, dl = 1.f;
+    if (tid >= 1 && tid <= k) affine_of(mm_prev, KS, tid, m, dl);
+    s_m[tid] = m;
+    s_d[tid] = dl;
+  }
+}
+
+// Block-wide min/max of per-thread partials -> 2k atomics per workgroup.
+template <int KS>
+__device__ __forceinline__ void flush_minmax(const float (&lmn)[KS],
+                                             const float (&lmx)[KS], int k,
+                                             int *mm_cur) {
+  __shared__ float s_red[2][kBlock / 64][KS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int i = 1; i < KS; i++) {
+    float a = lmn[i], b = lmx[i];
+    if (i <= k) {  // wave-uniform
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        a = fminf(a, __shfl_xor(a, off));
+        b = fmaxf(b, __shfl_xor(b, off));
+      }
+    }
+    if (lane == 0) {
+      s_red[0][wave][i] = a;
+      s_red[1][wave][i] = b;
+    }
+  }
+  __syncthreads();
+  if (tid >= 1 && tid <= k) {
+    float a = INFINITY, b = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; w++) {
+      a = fminf(a, s_red[0][w][tid]);
+      b = fmaxf(b, s_red[1][w][tid]);
+    }
+    if (b >= a) {
+      atomicMax(&mm_cur[tid], f2ord(b));
+      atomicMax(&mm_cur[KS + tid], ~f2ord(a));
+    }
+  }
+}
+
+// One CSR half-sweep over rows [row0, row0+R), narrow rows (KS <= 20):
+// G lanes per destination row; each lane strides the row's incidences with
+// two gathers in flight and keeps all KS accumulators in registers; an
+// xor-shuffle reduction over the G lanes; lane 0 of the group writes.
+//   MODE_FULL:    out[r] = [1/len, (s(self) + s?(sum w*src / sum w)) / 2]
+//   MODE_PARTIAL: out[r] = [sum w, sum w*src]    (no self, no min/max)
+template <int KS, int G, int MODE>
+__global__ __launch_bounds__(kBlock) void algdist_half_narrow(
+    int row0, int R, const int *__restrict__ rp, const int *__restrict__ col,
+    const float *__restrict__ self_in, const float *__restrict__ src,
+    float *__restrict__ out, const int *__restrict__ mm_prev, int src_affine,
+    int *__restrict__ mm_cur, int k) {
+  constexpr int NV = KS / 4;
+  __shared__ float s_m[KS], s_d[KS];
+  load_affine<KS>(mm_prev, k, s_m, s_d);
+  __syncthreads();
+  const int tid = threadIdx.x;
+  const int lg = tid % G;
+  constexpr int GPB = kBlock / G;
+  const int ngroups = gridDim.x * GPB;
+  float lmn[KS], lmx[KS];
+#pragma unroll
+  for (int i = 0; i < KS; i++) {
+    lmn[i] = INFINITY;
+    lmx[i] = -INFINITY;
+  }
+  const float4 *src4 = reinterpret_cast<const float4 *>(src);
+  for (int rr = blockIdx.x * GPB + tid / G; rr < R; rr += ngroups) {
+    const int r = row0 + rr;
+    const int beg = rp[r], end = rp[r + 1];
+    float4 acc[NV];
+#pragma unroll
+    for (int j = 0; j < NV; j++) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float wsum = 0.f;
+    int t = beg + lg;
+    for (; t + G < end; t += 2 * G) {
+      const int c0 = col[t], c1 = col[t + G];
+      float4 v0[NV], v1[NV];
+#pragma unroll
+      for (int j = 0; j < NV; j++) v0[j] = src4[(size_t)c0 * NV + j];
+#pragma unroll
+      for (int j = 0; j < NV; j++) v1[j] = src4[(size_t)c1 * NV + j];
+      const float w0 = v0[0].x, w1 = v1[0].x;
+      wsum += w0;
+      wsum += w1;
+#pragma unroll
+      for (int j = 0; j < NV; j++) acc[j] = f4fma(w1, v1[j], f4fma(w0, v0[j], acc[j]));
+    }
+    if (t < end) {
+      const int c0 = col[t];
+      float4 v0[NV];
+#pragma unroll
+      for (int j = 0; j < NV; j++) v0[j] = src4[(size_t)c0 * NV + j];
+      const float w0 = v0[0].x;
+      wsum += w0;
+#pragma unroll
+      for (int j = 0; j < NV; j++) acc[j] = f4fma(w0, v0[j], acc[j]);
+    }
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) {
+      wsum += __shfl_xor(wsum, off);
+#pragma unroll
+      for (int j = 0; j < NV; j++) {
+        acc[j].x += __shfl_xor(acc[j].x, off);
+        acc[j].y += __shfl_xor(acc[j].y, off);
+        acc[j].z += __shfl_xor(acc[j].z, off);
+        acc[j].w += __shfl_xor(acc[j].w, off);
+      }
+    }
+    if (lg == 0) {
+      float4 *op = reinterpret_cast<float4 *>(out) + (size_t)r * NV;
+      if (MODE == MODE_PARTIAL) {
+        acc[0].x = wsum;
+#pragma unroll
+        for (int j = 0; j < NV; j++) op[j] = acc[j];
+      } else {
+        const float4 *sp = reinterpret_cast<const float4 *>(self_in) + (size_t)r * NV;
+        const float own_w = 1.0f / (float)(end - beg);
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+          const float4 s = sp[j];
+          float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            const int i = 4 * j + c;
+            float v;
+            if (i == 0) {
+              v = own_w;
+            } else if (i <= k) {
+              const float sv = (f4get(s, c) - s_m[i]) / s_d[i];
+              float mv = f4get(acc[j], c) / wsum;
+              if (src_affine) mv = (mv - s_m[i]) / s_d[i];
+              v = (sv + mv) * 0.5f;
+              lmn[i] = fminf(lmn[i], v);
+              lmx[i] = fmaxf(lmx[i], v);
+            } else {
+              v = 0.f;
+            }
+            f4set(o, c, v);
+          }
+          op[j] = o;
+        }
+      }
+    }
+  }
+  if (MODE == MODE_FULL) flush_minmax<KS>(lmn, lmx, k, mm_cur);
+}
+
+// Wide rows (k > 19): one wave per destination row, the row's float4
+// vectors spread over the lanes, incidences walked in order.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void algdist_half_wide(
+    int row0, int R, int KS, const int *__restrict__ rp,
+    const int *__restrict__ col, const float *__restrict__ self_in,
+    const float *__restrict__ src, float *__restrict__ out,
+    const int *__restrict__ mm_prev, int src_affine, int *__restrict__ mm_cur,
+    int k) {
+  const int NV = KS / 4;
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  const int nw = gridDim.x * (kBlock / 64);
+  constexpr int MAXV = 8;  // up to 64*8*4 = 2048 floats per row
+  float lmn[MAXV * 4], lmx[MAXV * 4];
+#pragma unroll
+  for (int i = 0; i < MAXV * 4; i++) {
+    lmn[i] = INFINITY;
+    lmx[i] = -INFINITY;
+  }
+  const float4 *src4 = reinterpret_cast<const float4 *>(src);
+  for (int rr = wid; rr < R; rr += nw) {
+    const int r = row0 + rr;
+    const int beg = rp[r], end = rp[r + 1];
+    float4 acc[MAXV];
+#pragma unroll
+    for (int q = 0; q < MAXV; q++) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float wsum = 0.f;
+    for (int t = beg; t < end; t++) {
+      const int c = col[t];
+      const float w = src[(size_t)c * KS];
+      wsum += w;
+#pragma unroll
+      for (int q = 0; q < MAXV; q++) {
+        const int j = lane + 64 * q;
+        if (j < NV) acc[q] = f4fma(w, src4[(size_t)c * NV + j], acc[q]);
+      }
+    }
+    const float own_w = 1.0f / (float)(end - beg);
+#pragma unroll
+    for (int q = 0; q < MAXV; q++) {
+      const int j = lane + 64 * q;
+      if (j >= NV) continue;
+      float4 o;
+      if (MODE == MODE_PARTIAL) {
+        o = acc[q];
+        if (j == 0) o.x = wsum;
+      } else {
+        const float4 s = reinterpret_cast<const float4 *>(self_in)[(size_t)r * NV + j];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          const int i = 4 * j + c;
+          float v = 0.f;
+          if (i == 0) {
+            v = own_w;
+          } else if (i <= k) {
+            float m, dl;
+            affine_of(mm_prev, KS, i, m, dl);
+            const float sv = (f4get(s, c) - m) / dl;
+            float mv = f4get(acc[q], c) / wsum;
+            if (src_affine) mv = (mv - m) / dl;
+            v = (sv + mv) * 0.5f;
+            lmn[4 * q + c] = fminf(lmn[4 * q + c], v);
+            lmx[4 * q + c] = fmaxf(lmx[4 * q + c], v);
+          }
+          f4set(o, c, v);
+        }
+      }
+      reinterpret_cast<float4 *>(out)[(size_t)r * NV + j] = o;
+    }
+  }
+  if (MODE == MODE_PARTIAL) return;
+#pragma unroll
+  for (int q = 0; q < MAXV; q++) {
+    const int j = lane + 64 * q;
+    if (j >= NV) continue;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int i = 4 * j + c;
+      if (i >= 1 && i <= k && lmx[4 * q + c] >= lmn[4 * q + c]) {
+        atomicMax(&mm_cur[i], f2ord(lmx[4 * q + c]));
+        atomicMax(&mm_cur[KS + i], ~f2ord(lmn[4 * q + c]));
+      }
+    }
+  }
+}
+
+// Sharded edge half, after the caller's SUM all-reduce of the partials:
+// y'_e = (s(y_e) + P[e][1..k] / P[e][0]) / 2, min/max into mm_cur.
+__global__ __launch_bounds__(kBlock) void algdist_edge_final(
+    int E, int KS, int k, const int *__restrict__ rp_e,
+    const float *__restrict__ self_in, const float *__restrict__ part,
+    float *__restrict__ out, const int *__restrict__ mm_prev,
+    int *__restrict__ mm_cur) {
+  __shared__ int s_mm[4096];  // 2 * KS, KS <= 2048
+  for (int i = threadIdx.x; i < 2 * KS; i += blockDim.x) s_mm[i] = INT_MIN;
+  __syncthreads();
+  const int64_t total = (int64_t)E * KS;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < total;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int e = (int)(q / KS), i = (int)(q % KS);
+    float v = 0.f;
+    if (i == 0) {
+      v = 1.0f / (float)(rp_e[e + 1] - rp_e[e]);
+    } else if (i <= k) {
+      float m, dl;
+      affine_of(mm_prev, KS, i, m, dl);
+      const float sv = (self_in[q] - m) / dl;
+      const float mv = part[q] / part[(int64_t)e * KS];
+      v = (sv + mv) * 0.5f;
+      atomicMax(&s_mm[i], f2ord(v));
+      atomicMax(&s_mm[KS + i], ~f2ord(v));
+    }
+    out[q] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * KS; i += blockDim.x) {
+    const int s = i % KS;
+    if (s >= 1 && s <= k && s_mm[i] != INT_MIN) atomicMax(&mm_cur[i], s_mm[i]);
+  }
+}
+
+// dense R x k  ->  rows [1/len, c_0..c_{k-1}, 0...] of KS floats
+__global__ void pack_rows(int R, int k, int KS, const int *__restrict__ rp,
+                          const float *__restrict__ dense,
+                          float *__restrict__ rows) {
+  const int64_t total = (int64_t)R * KS;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / KS), s = (int)(i % KS);
+    float v = 0.f;
+    if (s == 0) v = 1.0f / (float)(rp[r + 1] - rp[r]);
+    else if (s <= k) v = dense[(int64_t)r * k + (s - 1)];
+    rows[i] = v;
+  }
+}
+
+// In place on rows [row0, row0+R): apply the affine of mm to slots 1..k.
+__global__ void apply_affine(int row0, int R, int k, int KS,
+                             float *__restrict__ rows,
+                             const int *__restrict__ mm) {
+  const int64_t total = (int64_t)R * KS;
+  float *base = rows + (int64_t)row0 * KS;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int s = (int)(i % KS);
+    if (s >= 1 && s <= k) {
+      float m, dl;
+      affine_of(mm, KS, s, m, dl);
+      base[i] = (base[i] - m) / dl;
+    }
+  }
+}
+
+__global__ void unpack_rows(int R, int k, int KS, const float *__restrict__ rows,
+                            float *__restrict__ dense) {
+  const int64_t total = (int64_t)R * k;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / k), s = (int)(i % k);
+    dense[i] = rows[(int64_t)r * KS + 1 + s];
+  }
+}
+
+__global__ void count_empty_rows(int R, const int *__restrict__ rp,
+                                 int *__restrict__ out) {
+  int bad = 0;
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < R;
+       r += gridDim.x * blockDim.x)
+    bad |= (rp[r + 1] == rp[r]);
+  if (bad) atomicOr(out, 1);
+}
+
+__global__ void fill_int(int *p, int64_t n, int v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+int grid_for(int64_t work, int per_block) {
+  int64_t g = (work + per_block - 1) / per_block;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, 2048));
+}
+
+int pick_g(double avg) {
+  int g = 1;
+  while (g < 64 && g * 4 < avg) g *= 2;
+  return g;
+}
+
+using HalfFn = void (*)(int, int, const int *, const int *, const float *,
+                        const float *, float *, const int *, int, int *, int);
+
+template <int KS, int MODE>
+HalfFn narrow_for_g(int g) {
+  switch (g) {
+    case 1: return algdist_half_narrow<KS, 1, MODE>;
+    case 2: return algdist_half_narrow<KS, 2, MODE>;
+    case 4: return algdist_half_narrow<KS, 4, MODE>;
+    case 8: return algdist_half_narrow<KS, 8, MODE>;
+    case 16: return algdist_half_narrow<KS, 16, MODE>;
+    case 32: return algdist_half_narrow<KS, 32, MODE>;
+    default: return algdist_half_narrow<KS, 64, MODE>;
+  }
+}
+
+template <int MODE>
+HalfFn narrow_fn(int ks, int g) {
+  switch (ks) {
+    case 4: return narrow_for_g<4, MODE>(g);
+    case 8: return narrow_for_g<8, MODE>(g);
+    case 12: return narrow_for_g<12, MODE>(g);
+    case 16: return narrow_for_g<16, MODE>(g);
+    case 20: return narrow_for_g<20, MODE>(g);
+    default: return nullptr;
+  }
+}
+
+int launch_half(hgx_ctx *ctx, int mode, int row0, int R, const int *rp,
+                const int *col, const float *self_in, const float *src,
+                float *out, const int *mm_prev, int src_affine, int *mm_cur,
+                double avg) {
+  const int k = ctx->k, KS = ctx->ks;
+  if (R <= 0) return HGX_OK;
+  if (KS <= 20) {
+    const int g = pick_g(avg);
+    HalfFn fn = mode == MODE_FULL ? narrow_fn<MODE_FULL>(KS, g)
+                                  : narrow_fn<MODE_PARTIAL>(KS, g);
+    hipLaunchKernelGGL(fn, dim3(grid_for(R, kBlock / g)), dim3(kBlock), 0,
+                       ctx->stream, row0, R, rp, col, self_in, src, out,
+                       mm_prev, src_affine, mm_cur, k);
+  } else {
+    auto fn = mode == MODE_FULL ? algdist_half_wide<MODE_FULL>
+                                : algdist_half_wide<MODE_PARTIAL>;
+    hipLaunchKernelGGL(fn, dim3(grid_for(R, kBlock / 64)), dim3(kBlock), 0,
+                       ctx->stream, row0, R, KS, rp, col, self_in, src, out,
+                       mm_prev, src_affine, mm_cur, k);
+  }
+  HGX_LAUNCH_CHECK(ctx);
+  return HGX_OK;
+}
+
+int check_nonempty(hgx_ctx *ctx) {
+  HGX_TRY(hgx_ensure(ctx, ctx->s0, 16));
+  int *flag = ctx->s0.as<int>();
+  HGX_HIP(ctx, hipMemsetAsync(flag, 0, sizeof(int), ctx->stream));
+  hipLaunchKernelGGL(count_empty_rows, dim3(grid_for(ctx->N, 256)), dim3(256),
+                     0, ctx->stream, ctx->N, ctx->rp_n.as<int>(), flag);
+  hipLaunchKernelGGL(count_empty_rows, dim3(grid_for(ctx->E, 256)), dim3(256),
+                     0, ctx->stream, ctx->E, ctx->rp_e.as<int>(), flag);
+  HGX_LAUNCH_CHECK(ctx);
+  int h = 0;
+  HGX_HIP(ctx, hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  HGX_CHECK(ctx, h == 0, HGX_EZERODIV,
+            "isolated node or edge: 1/|row| weights divide by zero "
+            "(algebraic_distance.py:49)");
+  return HGX_OK;
+}
+
+int init_mm(hgx_ctx *ctx, int *mm, int64_t words) {
+  hipLaunchKernelGGL(fill_int, dim3(grid_for(words, 256)), dim3(256), 0,
+                     ctx->stream, mm, words, INT_MIN);
+  HGX_LAUNCH_CHECK(ctx);
+  return HGX_OK;
+}
+
+int final_affine(hgx_ctx *ctx, int node_row0, int node_rows, const int *last) {
+  const int k = ctx->k, KS = ctx->ks;
+  if (node_rows > 0)
+    hipLaunchKernelGGL(apply_affine,
+                       dim3(grid_for((int64_t)node_rows * KS, 256)), dim3(256),
+                       0, ctx->stream, node_row0, node_rows, k, KS,
+                       ctx->X[ctx->xcur].as<float>(), last);
+  hipLaunchKernelGGL(apply_affine, dim3(grid_for((int64_t)ctx->E * KS, 256)),
+                     dim3(256), 0, ctx->stream, 0, ctx->E, k, KS,
+                     ctx->Y[ctx->ycur].as<float>(), last);
+  HGX_LAUNCH_CHECK(ctx);
+  return HGX_OK;
+}
+
+}  // namespace
+
+extern "C" int hgx_alg_set(hgx_ctx *ctx, int k, const float *node_xy,
+                           const float *edge_xy) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->N > 0, HGX_ESTATE, "no incidence uploaded");
+  HGX_CHECK(ctx, k >= 1 && k <= 2046, HGX_EUNSUP, "k=%d outside [1,2046]", k);
+  HGX_CHECK(ctx, node_xy && edge_xy, HGX_EINVAL, "null coordinate buffer");
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  HGX_TRY(check_nonempty(ctx));
+  const int KS = ((k + 1) + 3) / 4 * 4;
+  ctx->k = k;
+  ctx->ks = KS;
+  for (int b = 0; b < 2; b++) {
+    HGX_TRY(hgx_ensure(ctx, ctx->X[b], sizeof(float) * (size_t)ctx->N * KS));
+    HGX_TRY(hgx_ensure(ctx, ctx->Y[b], sizeof(float) * (size_t)ctx->E * KS));
+  }
+  const size_t dn = sizeof(float) * (size_t)ctx->N * k;
+  const size_t de = sizeof(float) * (size_t)ctx->E * k;
+  HGX_TRY(hgx_ensure(ctx, ctx->s1, std::max(dn, de)));
+  HGX_HIP(ctx, hipMemcpyAsync(ctx->s1.p, node_xy, dn, hipMemcpyHostToDevice,
+                              ctx->stream));
+  hipLaunchKernelGGL(pack_rows, dim3(grid_for((int64_t)ctx->N * KS, 256)),
+                     dim3(256), 0, ctx->stream, ctx->N, k, KS,
+                     ctx->rp_n.as<int>(), ctx->s1.as<float>(),
+                     ctx->X[0].as<float>());
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  HGX_HIP(ctx, hipMemcpyAsync(ctx->s1.p, edge_xy, de, hipMemcpyHostToDevice,
+                              ctx->stream));
+  hipLaunchKernelGGL(pack_rows, dim3(grid_for((int64_t)ctx->E * KS, 256)),
+                     dim3(256), 0, ctx->stream, ctx->E, k, KS,
+                     ctx->rp_e.as<int>(), ctx->s1.as<float>(),
+                     ctx->Y[0].as<float>());
+  HGX_LAUNCH_CHECK(ctx);
+  ctx->xcur = ctx->ycur = 0;
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HGX_OK;
+}
+
+extern "C" int hgx_alg_run(hgx_ctx *ctx, int iters) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->k > 0, HGX_ESTATE, "hgx_alg_set not called");
+  HGX_CHECK(ctx, iters >= 0, HGX_EINVAL, "iterations must be >= 0");
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  if (iters == 0) return HGX_OK;
+  const int KS = ctx->ks;
+  const size_t slot = 2 * (size_t)KS;
+  HGX_TRY(hgx_ensure(ctx, ctx->mm, sizeof(int) * slot * iters));
+  int *mm = ctx->mm.as<int>();
+  HGX_TRY(init_mm(ctx, mm, (int64_t)slot * iters));
+  HGX_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  for (int it = 0; it < iters; it++) {
+    const int *prev = it ? mm + slot * (it - 1) : nullptr;
+    int *cur = mm + slot * it;
+    float *xc = ctx->X[ctx->xcur].as<float>(), *xn = ctx->X[ctx->xcur ^ 1].as<float>();
+    float *yc = ctx->Y[ctx->ycur].as<float>(), *yn = ctx->Y[ctx->ycur ^ 1].as<float>();
+    // node half: self x (scaled), gathered y (scaled)
+    HGX_TRY(launch_half(ctx, MODE_FULL, 0, ctx->N, ctx->rp_n.as<int>(),
+                        ctx->col_n.as<int>(), xc, yc, xn, prev, prev != nullptr,
+                        cur, ctx->avg_deg_n));
+    // edge half: self y (scaled), gathered NEW x (raw)
+    HGX_TRY(launch_half(ctx, MODE_FULL, 0, ctx->E, ctx->rp_e.as<int>(),
+                        ctx->col_e.as<int>(), yc, xn, yn, prev, 0, cur,
+                        ctx->avg_deg_e));
+    ctx->xcur ^= 1;
+    ctx->ycur ^= 1;
+  }
+  HGX_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  HGX_TRY(final_affine(ctx, 0, ctx->N, mm + slot * (iters - 1)));
+  HGX_HIP(ctx, hipEventSynchronize(ctx->ev1));
+  float ms = 0.f;
+  HGX_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  ctx->alg_ms = ms;
+  ctx->alg_bytes = (double)iters * (8.0 * ctx->nnz +
+                                    (8.0 + 12.0 * ctx->k) * (ctx->N + ctx->E));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HGX_OK;
+}
+
+extern "C" int hgx_alg_get(hgx_ctx *ctx, float *node_xy, float *edge_xy) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->k > 0, HGX_ESTATE, "no alg coordinates on device");
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  const int k = ctx->k, KS = ctx->ks;
+  const size_t dn = sizeof(float) * (size_t)ctx->N * k;
+  const size_t de = sizeof(float) * (size_t)ctx->E * k;
+  HGX_TRY(hgx_ensure(ctx, ctx->s1, std::max(dn, de)));
+  if (node_xy) {
+    hipLaunchKernelGGL(unpack_rows, dim3(grid_for((int64_t)ctx->N * k, 256)),
+                       dim3(256), 0, ctx->stream, ctx->N, k, KS,
+                       ctx->X[ctx->xcur].as<float>(), ctx->s1.as<float>());
+    HGX_LAUNCH_CHECK(ctx);
+    HGX_HIP(ctx, hipMemcpyAsync(node_xy, ctx->s1.p, dn, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  if (edge_xy) {
+    hipLaunchKernelGGL(unpack_rows, dim3(grid_for((int64_t)ctx->E * k, 256)),
+                       dim3(256), 0, ctx->stream, ctx->E, k, KS,
+                       ctx->Y[ctx->ycur].as<float>(), ctx->s1.as<float>());
+    HGX_LAUNCH_CHECK(ctx);
+    HGX_HIP(ctx, hipMemcpyAsync(edge_xy, ctx->s1.p, de, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  return HGX_OK;
+}
+
+extern "C" int hgx_alg_dist(hgx_ctx *ctx, int k, int iters, float *node_xy,
+                            float *edge_xy) {
+  HGX_TRY(hgx_alg_set(ctx, k, node_xy, edge_xy));
+  HGX_TRY(hgx_alg_run(ctx, iters));
+  return hgx_alg_get(ctx, node_xy, edge_xy);
+}
+
+extern "C" int hgx_alg_last_stats(hgx_ctx *ctx, double *ms, double *bytes) {
+  if (!ctx) return HGX_EINVAL;
+  if (ms) *ms = ctx->alg_ms;
+  if (bytes) *bytes = ctx->alg_bytes;
+  return HGX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Sharded relaxation: the caller (torch.distributed over RCCL, or gloo in
+// tests) all-reduces `partial` (SUM, float32, E*KS) between edge_partial and
+// edge_final, and mm slot `it` (MAX, int32, 2*KS) after edge_final.
+// ---------------------------------------------------------------------------
+extern "C" int hgx_alg_shard_begin(hgx_ctx *ctx, int32_t row0, int32_t row1,
+                                   void *d_partial, void *d_mm, int iters,
+                                   int *ks_out) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->k > 0, HGX_ESTATE, "hgx_alg_set not called");
+  HGX_CHECK(ctx, 0 <= row0 && row0 <= row1 && row1 <= ctx->N, HGX_EINVAL,
+            "node shard [%d,%d) outside [0,%d)", row0, row1, ctx->N);
+  HGX_CHECK(ctx, d_partial && d_mm && iters > 0, HGX_EINVAL,
+            "null exchange buffer or iters <= 0");
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  // local edge sub-CSR: for every edge, the incidences with node in
+  // [row0,row1) (edge rows are sorted, so they are contiguous).
+  std::vector<int> rp(ctx->E + 1), col((size_t)ctx->nnz + 1), rpl(ctx->E + 1);
+  HGX_HIP(ctx, hipMemcpy(rp.data(), ctx->rp_e.p, sizeof(int) * (ctx->E + 1),
+                         hipMemcpyDeviceToHost));
+  if (ctx->nnz)
+    HGX_HIP(ctx, hipMemcpy(col.data(), ctx->col_e.p, sizeof(int) * ctx->nnz,
+                           hipMemcpyDeviceToHost));
+  std::vector<int> cl;
+  cl.reserve((size_t)ctx->nnz / 2 + 1);
+  rpl[0] = 0;
+  for (int e = 0; e < ctx->E; e++) {
+    auto b = col.begin() + rp[e], en = col.begin() + rp[e + 1];
+    auto lo = std::lower_bound(b, en, row0), hi = std::lower_bound(b, en, row1);
+    cl.insert(cl.end(), lo, hi);
+    rpl[e + 1] = (int)cl.size();
+  }
+  HGX_TRY(hgx_ensure(ctx, ctx->rp_el, sizeof(int) * (ctx->E + 1)));
+  HGX_TRY(hgx_ensure(ctx, ctx->col_el, sizeof(int) * (cl.size() + 1)));
+  HGX_HIP(ctx, hipMemcpy(ctx->rp_el.p, rpl.data(), sizeof(int) * (ctx->E + 1),
+                         hipMemcpyHostToDevice));
+  if (!cl.empty())
+    HGX_HIP(ctx, hipMemcpy(ctx->col_el.p, cl.data(), sizeof(int) * cl.size(),
+                           hipMemcpyHostToDevice));
+  ctx->row0 = row0;
+  ctx->row1 = row1;
+  ctx->ext_partial = (float *)d_partial;
+  ctx->ext_mm = (int *)d_mm;
+  ctx->ext_iters = iters;
+  HGX_TRY(init_mm(ctx, ctx->ext_mm, (int64_t)2 * ctx->ks * iters));
+  if (ks_out) *ks_out = ctx->ks;
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HGX_OK;
+}
+
+extern "C" int hgx_alg_shard_node(hgx_ctx *ctx, int it) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->ext_mm && it >= 0 && it < ctx->ext_iters, HGX_ESTATE,
+            "shard iteration %d out of order", it);
+  const size_t slot = 2 * (size_t)ctx->ks;
+  const int *prev = it ? ctx->ext_mm + slot * (it - 1) : nullptr;
+  int *cur = ctx->ext_mm + slot * it;
+  float *xc = ctx->X[ctx->xcur].as<float>(), *xn = ctx->X[ctx->xcur ^ 1].as<float>();
+  float *yc = ctx->Y[ctx->ycur].as<float>();
+  HGX_TRY(launch_half(ctx, MODE_FULL, ctx->row0, ctx->row1 - ctx->row0,
+                      ctx->rp_n.as<int>(), ctx->col_n.as<int>(), xc, yc, xn,
+                      prev, prev != nullptr, cur, ctx->avg_deg_n));
+  return HGX_OK;
+}
+
+extern "C" int hgx_alg_shard_edge_partial(hgx_ctx *ctx, int it) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->ext_mm && it >= 0 && it < ctx->ext_iters, HGX_ESTATE,
+            "shard iteration %d out of order", it);
+  float *xn = ctx->X[ctx->xcur ^ 1].as<float>();
+  const double avg = (double)std::max<int64_t>(1, ctx->nnz) / ctx->E;
+  HGX_TRY(launch_half(ctx, MODE_PARTIAL, 0, ctx->E, ctx->rp_el.as<int>(),
+                      ctx->col_el.as<int>(), nullptr, xn, ctx->ext_partial,
+                      nullptr, 0, nullptr, avg));
+  return HGX_OK;
+}
+
+extern "C" int hgx_alg_shard_edge_final(hgx_ctx *ctx, int it) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->ext_mm && it >= 0 && it < ctx->ext_iters, HGX_ESTATE,
+            "shard iteration %d out of order", it);
+  const size_t slot = 2 * (size_t)ctx->ks;
+  const int *prev = it ? ctx->ext_mm + slot * (it - 1) : nullptr;
+  int *cur = ctx->ext_mm + slot * it;
+  float *yc = ctx->Y[ctx->ycur].as<float>(), *yn = ctx->Y[ctx->ycur ^ 1].as<float>();
+  hipLaunchKernelGGL(algdist_edge_final,
+                     dim3(grid_for((int64_t)ctx->E * ctx->ks, 256)), dim3(256),
+                     0, ctx->stream, ctx->E, ctx->ks, ctx->k,
+                     ctx->rp_e.as<int>(), yc, ctx->ext_partial, yn, prev, cur);
+  HGX_LAUNCH_CHECK(ctx);
+  ctx->xcur ^= 1;
+  ctx->ycur ^= 1;
+  return HGX_OK;
+}
+
+extern "C" int hgx_alg_shard_end(hgx_ctx *ctx) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->ext_mm, HGX_ESTATE, "hgx_alg_shard_begin not called");
+  const size_t slot = 2 * (size_t)ctx->ks;
+  HGX_TRY(final_affine(ctx, ctx->row0, ctx->row1 - ctx->row0,
+                       ctx->ext_mm + slot * (ctx->ext_iters - 1)));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->ext_mm = nullptr;
+  ctx->ext_partial = nullptr;
+  return HGX_OK;
+}

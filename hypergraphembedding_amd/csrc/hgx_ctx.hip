@@ -1,0 +1,166 @@
+// Context lifetime, errors, incidence upload. See include/hgx.h.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "hgx_internal.h"
+
+int hgx_fail(hgx_ctx *ctx, int code, const char *fmt, ...) {
+  if (ctx) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    ctx->err = buf;
+  }
+  return code;
+}
+
+int hgx_ensure(hgx_ctx *ctx, DevBuf &b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.bytes >= bytes) return HGX_OK;
+  if (b.p) {
+    hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e != hipSuccess) {
+    b.p = nullptr;
+    (void)hipGetLastError();
+    return hgx_fail(ctx, HGX_ENOMEM, "hipMalloc(%zu bytes) failed: %s", bytes,
+                    hipGetErrorString(e));
+  }
+  b.bytes = bytes;
+  return HGX_OK;
+}
+
+void hgx_release(DevBuf &b) {
+  if (b.p) hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+extern "C" int hgx_version(void) { return 1; }
+
+extern "C" int hgx_create(int device, hgx_ctx **out) {
+  if (!out) return HGX_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    return HGX_EHIP;
+  }
+  if (device < 0 || device >= n) return HGX_EINVAL;
+  if (hipSetDevice(device) != hipSuccess) return HGX_EHIP;
+  hgx_ctx *ctx = new hgx_ctx();
+  ctx->device = device;
+  if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) !=
+      hipSuccess) {
+    delete ctx;
+    return HGX_EHIP;
+  }
+  ctx->stream = ctx->own_stream;
+  hipEventCreate(&ctx->ev0);
+  hipEventCreate(&ctx->ev1);
+  *out = ctx;
+  return HGX_OK;
+}
+
+extern "C" int hgx_destroy(hgx_ctx *ctx) {
+  if (!ctx) return HGX_OK;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  DevBuf *bufs[] = {&ctx->rp_n, &ctx->col_n, &ctx->rp_e, &ctx->col_e,
+                    &ctx->X[0], &ctx->X[1], &ctx->Y[0], &ctx->Y[1], &ctx->mm,
+                    &ctx->rp_el, &ctx->col_el,
+                    &ctx->rec_idx, &ctx->rec_tgt, &ctx->ntab, &ctx->etab,
+                    &ctx->nacc, &ctx->eacc, &ctx->s0, &ctx->s1, &ctx->s2,
+                    &ctx->s3, &ctx->s4, &ctx->s5, &ctx->s6, &ctx->s7};
+  for (DevBuf *b : bufs) hgx_release(*b);
+  if (ctx->ev0) hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) hipEventDestroy(ctx->ev1);
+  if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+  return HGX_OK;
+}
+
+extern "C" const char *hgx_last_error(const hgx_ctx *ctx) {
+  return ctx ? ctx->err.c_str() : "null context";
+}
+
+extern "C" int hgx_set_stream(hgx_ctx *ctx, void *hip_stream) {
+  if (!ctx) return HGX_EINVAL;
+  ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+  return HGX_OK;
+}
+
+extern "C" int hgx_synchronize(hgx_ctx *ctx) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HGX_OK;
+}
+
+static int check_csr(hgx_ctx *ctx, const char *name, int32_t R, int32_t C,
+                     int64_t nnz, const int32_t *rp, const int32_t *col) {
+  HGX_CHECK(ctx, rp && (nnz == 0 || col), HGX_EINVAL, "%s: null pointer", name);
+  HGX_CHECK(ctx, rp[0] == 0 && rp[R] == nnz, HGX_EINVAL,
+            "%s: rowptr must start at 0 and end at nnz", name);
+  for (int32_t r = 0; r < R; r++) {
+    HGX_CHECK(ctx, rp[r + 1] >= rp[r], HGX_EINVAL, "%s: rowptr not monotone",
+              name);
+    for (int32_t t = rp[r]; t < rp[r + 1]; t++) {
+      HGX_CHECK(ctx, col[t] >= 0 && col[t] < C, HGX_EINVAL,
+                "%s: column %d out of range [0,%d)", name, col[t], C);
+      HGX_CHECK(ctx, t == rp[r] || col[t] > col[t - 1], HGX_EINVAL,
+                "%s: columns of row %d not strictly increasing", name, r);
+    }
+  }
+  return HGX_OK;
+}
+
+extern "C" int hgx_upload_incidence(hgx_ctx *ctx, int32_t N, int32_t E,
+                                    int64_t nnz, const int32_t *rowptr_n,
+                                    const int32_t *col_n,
+                                    const int32_t *rowptr_e,
+                                    const int32_t *col_e) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, N > 0 && E > 0, HGX_EINVAL, "empty hypergraph (N=%d E=%d)",
+            N, E);
+  HGX_CHECK(ctx, nnz >= 0 && nnz < (int64_t)INT32_MAX, HGX_EUNSUP,
+            "nnz %lld outside int32 CSR range", (long long)nnz);
+  // Host-side validation: the kernels index without bounds checks, so an
+  // out-of-range column must be rejected here, never reach the GPU.
+  HGX_TRY(check_csr(ctx, "node-major", N, E, nnz, rowptr_n, col_n));
+  HGX_TRY(check_csr(ctx, "edge-major", E, N, nnz, rowptr_e, col_e));
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  HGX_TRY(hgx_ensure(ctx, ctx->rp_n, sizeof(int32_t) * (N + 1)));
+  HGX_TRY(hgx_ensure(ctx, ctx->rp_e, sizeof(int32_t) * (E + 1)));
+  HGX_TRY(hgx_ensure(ctx, ctx->col_n, sizeof(int32_t) * (nnz + 1)));
+  HGX_TRY(hgx_ensure(ctx, ctx->col_e, sizeof(int32_t) * (nnz + 1)));
+  HGX_HIP(ctx, hipMemcpyAsync(ctx->rp_n.p, rowptr_n, sizeof(int32_t) * (N + 1),
+                              hipMemcpyHostToDevice, ctx->stream));
+  HGX_HIP(ctx, hipMemcpyAsync(ctx->rp_e.p, rowptr_e, sizeof(int32_t) * (E + 1),
+                              hipMemcpyHostToDevice, ctx->stream));
+  if (nnz) {
+    HGX_HIP(ctx, hipMemcpyAsync(ctx->col_n.p, col_n, sizeof(int32_t) * nnz,
+                                hipMemcpyHostToDevice, ctx->stream));
+    HGX_HIP(ctx, hipMemcpyAsync(ctx->col_e.p, col_e, sizeof(int32_t) * nnz,
+                                hipMemcpyHostToDevice, ctx->stream));
+  }
+  int32_t mn = 0, me = 0;
+  for (int32_t r = 0; r < N; r++) mn = std::max(mn, rowptr_n[r + 1] - rowptr_n[r]);
+  for (int32_t r = 0; r < E; r++) me = std::max(me, rowptr_e[r + 1] - rowptr_e[r]);
+  ctx->N = N;
+  ctx->E = E;
+  ctx->nnz = nnz;
+  ctx->max_deg_n = mn;
+  ctx->max_deg_e = me;
+  ctx->avg_deg_n = (double)nnz / N;
+  ctx->avg_deg_e = (double)nnz / E;
+  ctx->k = 0;  // alg coords belong to the previous incidence
+  ctx->n_rec = 0;
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HGX_OK;
+}

@@ -1,0 +1,124 @@
+// Internal state of libhgx.so (MI355X / gfx950). See include/hgx.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "hgx.h"
+
+// Device buffer owned by a context; grows on demand, never shrinks.
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+struct hgx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;      // stream every launch goes to
+  hipStream_t own_stream = nullptr;  // created by hgx_create
+  std::string err;
+
+  // ---- incidence (compressed, both orientations, sorted columns) ----
+  int32_t N = 0, E = 0;
+  int64_t nnz = 0;
+  DevBuf rp_n, col_n, rp_e, col_e;
+  double avg_deg_n = 0, avg_deg_e = 0;
+  int32_t max_deg_n = 0, max_deg_e = 0;
+
+  // ---- algebraic distance: rows of KS floats = [w, x_0..x_{k-1}, pad] ----
+  int k = 0, ks = 0;
+  DevBuf X[2], Y[2];
+  int xcur = 0, ycur = 0;
+  DevBuf mm;            // per iteration [2][ks] int32 (max, ~min) encodings
+  // sharded (node-row) mode: own node rows [row0,row1), local edge sub-CSR
+  // of those rows, caller-owned exchange buffers (reduced by the caller).
+  int32_t row0 = 0, row1 = 0;
+  DevBuf rp_el, col_el;
+  float *ext_partial = nullptr;  // E x ks
+  int *ext_mm = nullptr;         // iters x 2 x ks
+  int ext_iters = 0;
+  double alg_ms = 0, alg_bytes = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+
+  // ---- records (SamplesToModelInput layout) ----
+  int64_t n_rec = 0;
+  int K = 0;
+  DevBuf rec_idx, rec_tgt;
+
+  // ---- model ----
+  int d = 0, dp = 0;
+  int64_t node_rows = 0, edge_rows = 0;
+  DevBuf ntab, etab, nacc, eacc;
+  double train_ms = 0;
+  int64_t train_records = 0, train_batches = 0;
+
+  // ---- scratch ----
+  DevBuf s0, s1, s2, s3, s4, s5, s6, s7;
+};
+
+int hgx_fail(hgx_ctx *ctx, int code, const char *fmt, ...);
+int hgx_ensure(hgx_ctx *ctx, DevBuf &b, size_t bytes);
+void hgx_release(DevBuf &b);
+
+#define HGX_HIP(ctx, expr)                                                   \
+  do {                                                                       \
+    hipError_t e_ = (expr);                                                  \
+    if (e_ != hipSuccess)                                                    \
+      return hgx_fail((ctx), HGX_EHIP, "%s failed: %s (%s:%d)", #expr,        \
+                      hipGetErrorString(e_), __FILE__, __LINE__);            \
+  } while (0)
+
+#define HGX_CHECK(ctx, cond, code, ...)                                      \
+  do {                                                                       \
+    if (!(cond)) return hgx_fail((ctx), (code), __VA_ARGS__);                \
+  } while (0)
+
+#define HGX_TRY(expr)                                                        \
+  do {                                                                       \
+    int rc_ = (expr);                                                        \
+    if (rc_ != HGX_OK) return rc_;                                           \
+  } while (0)
+
+#define HGX_LAUNCH_CHECK(ctx) HGX_HIP(ctx, hipGetLastError())
+
+// ---- device helpers shared by the kernels ----
+namespace hgx {
+
+// Order-preserving float <-> signed int32 so a per-dim min/max reduces with
+// atomicMax on device and all_reduce(MAX) on int32 across ranks. Max slots
+// hold f2ord(x); min slots hold ~f2ord(x) (bitwise not: order-reversing,
+// no overflow). Empty slot = INT_MIN.
+__device__ __forceinline__ int f2ord(float f) {
+  unsigned u = __float_as_uint(f);
+  unsigned s = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return (int)(s ^ 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(int e) {
+  unsigned s = (unsigned)e ^ 0x80000000u;
+  unsigned u = (s & 0x80000000u) ? (s & 0x7fffffffu) : ~s;
+  return __uint_as_float(u);
+}
+
+// splitmix64 finaliser: counter-based uniform bits for the samplers.
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t rand64(uint64_t seed,
+                                                    uint64_t stream,
+                                                    uint64_t ctr) {
+  return mix64(mix64(seed ^ mix64(stream + 0x632be59bd9b4e019ull)) + ctr);
+}
+// uniform integer in [0, n) (multiply-high on 64 random bits: bias < n/2^64)
+__device__ __forceinline__ uint32_t bounded(uint64_t r, uint32_t n) {
+  return (uint32_t)__umul64hi(r, (uint64_t)n);
+}
+
+}  // namespace hgx

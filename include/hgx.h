@@ -1,0 +1,160 @@
+/*
+ * hgx.h -- C ABI of libhgx.so, the MI355X (gfx950) FOBE/HOBE hot path.
+ *
+ * Plain pointers and sizes only. The caller owns every host buffer; the
+ * library owns all device memory, one HIP stream per context (a context is
+ * thread-compatible: use one per thread) and no global state.
+ *
+ * Every call returns 0 on success or a negative HGX_E* code; the message is
+ * in hgx_last_error(ctx). The Python host package (hypergraphembedding_amd)
+ * maps HGX_EINVAL -> AssertionError (the reference's precondition style,
+ * e.g. embedding.py:83-85, hg2v_sample.py:646-647), HGX_EZERODIV ->
+ * ZeroDivisionError (algebraic_distance.py:49 on an isolated row) and the
+ * rest -> RuntimeError.
+ *
+ * Each entry point names the reference interface it replaces
+ * (JSybrandt/HypergraphEmbedding, hypergraph_embedding/<file>:<line>).
+ */
+#ifndef HGX_H_
+#define HGX_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HGX_OK 0
+#define HGX_EINVAL -1    /* precondition violated (AssertionError)          */
+#define HGX_EHIP -2      /* HIP / RCCL runtime error                        */
+#define HGX_ENOMEM -3    /* device allocation failed                        */
+#define HGX_EZERODIV -4  /* isolated node/edge in algebraic distance        */
+#define HGX_ESTATE -5    /* call out of order (e.g. no incidence uploaded)  */
+#define HGX_EUNSUP -6    /* shape outside what this build supports          */
+
+#define HGX_LOSS_KLD 0   /* BooleanModel: kullback_leibler_divergence       */
+#define HGX_LOSS_MSE 1   /* UnweightedFloatModel: mean_squared_error        */
+#define HGX_ACT_SIGMOID 0
+#define HGX_ACT_RELU 1
+
+typedef struct hgx_ctx hgx_ctx;
+
+/* ---- context ---------------------------------------------------------- */
+int hgx_create(int device, hgx_ctx **out);
+int hgx_destroy(hgx_ctx *ctx);
+const char *hgx_last_error(const hgx_ctx *ctx);
+int hgx_version(void);
+/* Run on an external stream (e.g. torch.cuda.current_stream()); NULL =
+ * the context's own stream. */
+int hgx_set_stream(hgx_ctx *ctx, void *hip_stream);
+int hgx_synchronize(hgx_ctx *ctx);
+
+/* ---- incidence --------------------------------------------------------- *
+ * Replaces ToCsrMatrix / ToEdgeCsrMatrix(CompressRange(hg))
+ * (hypergraph_util.py:96-135, 223-244): the compressed N x E incidence in
+ * both orientations, int32 CSR with sorted columns. */
+int hgx_upload_incidence(hgx_ctx *ctx, int32_t N, int32_t E, int64_t nnz,
+                         const int32_t *rowptr_n, const int32_t *col_n,
+                         const int32_t *rowptr_e, const int32_t *col_e);
+
+/* ---- algebraic distance ----------------------------------------------- *
+ * Replaces EmbedAlgebraicDistance's relaxation loop
+ * (algebraic_distance.py:126-175, helpers 34-123): per iteration the node
+ * half, then the edge half on the NEW node coords, then the joint per-dim
+ * min-max rescale to [0,1]. Coordinates are fp32 on device.
+ *   hgx_alg_dist: upload node_xy (N x k) / edge_xy (E x k), run `iters`
+ *   iterations, download the rescaled result into the same buffers.
+ * The split calls keep the coords resident for benchmarking / HOBE:
+ *   hgx_alg_set -> hgx_alg_run (repeatable) -> hgx_alg_get. */
+int hgx_alg_dist(hgx_ctx *ctx, int k, int iters, float *node_xy,
+                 float *edge_xy);
+int hgx_alg_set(hgx_ctx *ctx, int k, const float *node_xy,
+                const float *edge_xy);
+int hgx_alg_run(hgx_ctx *ctx, int iters);
+int hgx_alg_get(hgx_ctx *ctx, float *node_xy, float *edge_xy);
+/* Device time (ms) of the last hgx_alg_run and its algorithmic bytes
+ * (8*nnz + (8+12k)*(N+E) per iteration). */
+int hgx_alg_last_stats(hgx_ctx *ctx, double *ms, double *bytes);
+
+/* Multi-GPU, node-row sharded. Rank g owns node rows
+ * [row0,row1); every rank holds all edge coords. The CALLER owns the two
+ * exchange buffers (device memory, e.g. torch tensors) and runs the
+ * collectives (torch.distributed "nccl" = RCCL over xGMI) between calls:
+ *   begin(row0,row1, partial[E*KS] f32, mm[iters*2*KS] i32, iters, &KS)
+ *   for it: node(it); edge_partial(it); all_reduce(partial, SUM);
+ *           edge_final(it); all_reduce(mm[it*2*KS : (it+1)*2*KS], MAX)
+ *   end()   -> own node rows + all edge rows rescaled on device
+ * min/max words are order-preserving int32 (max slot f(x), min slot ~f(x)),
+ * so MAX is the only reduction needed. */
+int hgx_alg_shard_begin(hgx_ctx *ctx, int32_t row0, int32_t row1,
+                        void *d_partial, void *d_mm, int iters, int *ks_out);
+int hgx_alg_shard_node(hgx_ctx *ctx, int it);
+int hgx_alg_shard_edge_partial(hgx_ctx *ctx, int it);
+int hgx_alg_shard_edge_final(hgx_ctx *ctx, int it);
+int hgx_alg_shard_end(hgx_ctx *ctx);
+
+/* ---- HOBE probabilities ------------------------------------------------ *
+ * _same_type_dist_calc (hg2v_sample.py:527-543) and DiffTypeDistanceSample
+ * (:588-629) on the device-resident alg coords (after hgx_alg_run or
+ * hgx_alg_set; values are used exactly as given, i.e. already rescaled).
+ * kind: 0 node-node, 1 edge-edge, 2 node-edge. Bit-exact with numpy's
+ * float32 norm (double-accumulated float products, k < 32). */
+int hgx_hobe_probs(hgx_ctx *ctx, int kind, int64_t n, const int32_t *a,
+                   const int32_t *b, float *out);
+
+/* Per-incidence weights (hg2v_weighting.py): which = 0 UniformWeight
+ * (195-198), 1 WeightByNeighborhood(alpha) (137-167), 2 HOBE distance weight
+ * (hg2v_sample.py:540-541). Output is node-major (nnz, CSR order of col_n)
+ * and edge-major (nnz, CSR order of col_e); either may be NULL. */
+int hgx_incidence_weights(hgx_ctx *ctx, int which, double alpha,
+                          float *node_major, float *edge_major);
+
+/* ---- samplers ----------------------------------------------------------- *
+ * Record layout = SamplesToModelInput(records, K, weighted=False)
+ * (hg2v_sample.py:751-797): int32 [ln, le, rn, re, nn_0..K-1, ne_0..K-1]
+ * (ids +1, 0 = absent) and float32 [nn_prob, ee_prob, ne_prob].
+ * Records stay on the device for hgx_train; hgx_records_get copies out.
+ *
+ * BooleanSamples (hg2v_sample.py:125-242). Quotas are the reference's
+ * int(weight * num_samples) (:138-146); the negative quotas may be NULL
+ * (neg_samples == 0). Uniform draws come from a counter-based generator
+ * keyed by `seed` (distribution-identical to the reference, not the same
+ * stream). */
+int hgx_sample_fobe(hgx_ctx *ctx, uint64_t seed, int K,
+                    const int32_t *node_quota, const int32_t *edge_quota,
+                    const int32_t *neg_node_quota,
+                    const int32_t *neg_edge_quota, int64_t *n_records);
+/* AlgebraicDistanceSamples (hg2v_sample.py:632-717) on the device alg
+ * coords: quota S for every row, nn/ee/ne probabilities as above. */
+int hgx_sample_hobe(hgx_ctx *ctx, uint64_t seed, int K, int S,
+                    int64_t *n_records);
+int hgx_records_set(hgx_ctx *ctx, int64_t n, int K, const int32_t *idx,
+                    const float *tgt);
+int hgx_records_info(hgx_ctx *ctx, int64_t *n, int *K);
+int hgx_records_get(hgx_ctx *ctx, int32_t *idx, float *tgt);
+
+/* ---- model + trainer ---------------------------------------------------- *
+ * Replaces BooleanModel / UnweightedFloatModel (hg2v_model.py:51-203) and
+ * the model.fit loop (embedding.py:269-305): two tables of (rows x d) fp32,
+ * row 0 = padding, Keras Adagrad (a += g^2; p -= lr*g/(sqrt(a)+eps),
+ * duplicate rows of a batch summed), loss = sum over the three heads of the
+ * batch mean, EarlyStopping(monitor=loss, min_delta, patience=0).
+ *   init_tables NULL -> uniform(-0.05, 0.05) from `seed` on device. */
+int hgx_model_init(hgx_ctx *ctx, int d, int64_t node_rows, int64_t edge_rows,
+                   uint64_t seed, const float *node_tab, const float *edge_tab);
+int hgx_model_get(hgx_ctx *ctx, float *node_tab, float *edge_tab);
+/* perms: NULL -> a fresh device shuffle per epoch keyed by shuffle_seed,
+ * else max_epochs x n int64 permutations (Keras' np.random.shuffle order).
+ * epoch_loss: max_epochs floats (may be NULL). */
+int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr, float eps,
+              int loss, int act, float min_delta, uint64_t shuffle_seed,
+              const int64_t *perms, float *epoch_loss, int *epochs_run);
+/* Device time (ms) of the last hgx_train spent in the per-batch kernels and
+ * the number of records they processed. */
+int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
+                         int64_t *batches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HGX_H_ */
