@@ -1,0 +1,135 @@
+"""GPU parity: the Keras-semantics Adagrad trainer vs the CPU oracle.
+
+Same record stream (reference-generated golden records), same initial
+tables, same per-epoch batch order (host permutations). The trainer is
+"parity unpinned" against Keras itself (keras/tensorflow are absent), so the
+oracle here is the restatement in oracle/hgref.c (hgref_train).
+
+Tolerance: per-row cosine p50 >= 0.9999 and p1 >= 0.999 after
+training, plus epoch losses within 1e-4 relative; fp32 summation order is
+the only difference, so the observed agreement is far tighter.
+"""
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+  from hypergraphembedding_amd import _hgx
+  c = _hgx.Context(0)
+  yield c
+  c.close()
+
+
+def _row_cos(a, b):
+  a = a.astype(np.float64)
+  b = b.astype(np.float64)
+  num = (a * b).sum(1)
+  den = np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1)
+  ok = den > 0
+  return num[ok] / den[ok]
+
+
+def _run_both(ctx, idx, tgt, K, d, loss, act, batch, epochs, seed=0,
+              min_delta=1e-3):
+  rs = np.random.RandomState(seed)
+  nrows = int(idx[:, [0, 2] + list(range(4, 4 + K))].max()) + 2
+  erows = int(idx[:, [1, 3] + list(range(4 + K, 4 + 2 * K))].max()) + 2
+  nt = rs.uniform(-0.05, 0.05, (nrows, d)).astype(np.float32)
+  et = rs.uniform(-0.05, 0.05, (erows, d)).astype(np.float32)
+  perms = np.stack([rs.permutation(idx.shape[0]) for _ in range(epochs)])
+  ont, oet, olosses, _, _ = O.train(idx, tgt, K, nt, et, loss, act,
+                                    batch=batch, max_epochs=epochs, perms=perms,
+                                    min_delta=min_delta)
+  ctx.records_set(idx, tgt)
+  ctx.model_init(d, nrows, erows, node_tab=nt, edge_tab=et)
+  glosses = ctx.train(batch=batch, max_epochs=epochs, loss=loss, act=act,
+                      perms=perms, min_delta=min_delta)
+  gnt, get_ = ctx.model_get()
+  return (ont, oet, olosses), (gnt, get_, glosses), (nt, et)
+
+
+def _check(o, g, init):
+  ont, oet, ol = o
+  gnt, get_, gl = g
+  assert ol.shape == gl.shape, (ol, gl)
+  assert np.allclose(gl, ol, rtol=1e-4, atol=1e-7), (gl, ol)
+  for a, b, i in ((gnt, ont, init[0]), (get_, oet, init[1])):
+    c = _row_cos(a, b)
+    assert np.percentile(c, 50) >= 0.9999
+    assert np.percentile(c, 1) >= 0.999
+    # the update actually happened
+    assert not np.array_equal(a, i)
+
+
+@pytest.mark.parametrize("d,batch", [(8, 64), (16, 256), (128, 256), (5, 37)])
+def test_train_hobe_records_vs_oracle(ctx, d, batch):
+  z = golden("hobe_small.npz")
+  o, g, init = _run_both(ctx, z["idx"], z["tgt"], int(z["K"]), d, O.LOSS_MSE,
+                         O.ACT_RELU, batch, epochs=3)
+  _check(o, g, init)
+
+
+@pytest.mark.parametrize("d,batch", [(16, 256), (256, 100), (2, 1)])
+def test_train_fobe_records_vs_oracle(ctx, d, batch):
+  z = golden("fobe_small_ns.npz")
+  idx, tgt = z["idx"], z["tgt"]
+  if batch == 1:  # the reference test's batch_size=1 (test_embedding.py:193)
+    idx, tgt = idx[:300], tgt[:300]
+  o, g, init = _run_both(ctx, idx, tgt, int(z["K"]), d, O.LOSS_KLD,
+                         O.ACT_SIGMOID, batch, epochs=2)
+  _check(o, g, init)
+
+
+def test_train_k5_synthetic_with_duplicates(ctx):
+  """K=5 (the default), heavy row reuse inside a batch, last batch ragged."""
+  rs = np.random.RandomState(7)
+  n, K = 3000, 5
+  idx = np.zeros((n, 4 + 2 * K), np.int32)
+  kind = rs.randint(0, 3, n)
+  idx[kind == 0, 0] = rs.randint(1, 30, (kind == 0).sum())
+  idx[kind == 0, 2] = rs.randint(1, 30, (kind == 0).sum())
+  idx[kind == 1, 1] = rs.randint(1, 12, (kind == 1).sum())
+  idx[kind == 1, 3] = rs.randint(1, 12, (kind == 1).sum())
+  m = kind == 2
+  idx[m, 0] = rs.randint(1, 30, m.sum())
+  idx[m, 3] = rs.randint(1, 12, m.sum())
+  idx[m, 4:4 + K] = rs.randint(1, 30, (m.sum(), K))
+  idx[m, 4 + K:] = rs.randint(1, 12, (m.sum(), K))
+  tgt = np.zeros((n, 3), np.float32)
+  tgt[np.arange(n), kind] = rs.uniform(0, 1, n).astype(np.float32)
+  o, g, init = _run_both(ctx, idx, tgt, K, 32, O.LOSS_MSE, O.ACT_RELU, 256,
+                         epochs=2)
+  _check(o, g, init)
+
+
+def test_train_early_stopping_and_device_shuffle(ctx):
+  z = golden("hobe_small.npz")
+  K = int(z["K"])
+  ctx.records_set(z["idx"], z["tgt"])
+  ctx.model_init(16, 200, 100, seed=5)
+  losses = ctx.train(batch=64, max_epochs=10, loss=O.LOSS_MSE, act=O.ACT_RELU,
+                     shuffle_seed=3, min_delta=1e9)
+  # min_delta huge: epoch 1 improves on inf, epoch 2 cannot -> stop (Keras
+  # EarlyStopping with patience=0)
+  assert losses.size == 2
+  losses = ctx.train(batch=64, max_epochs=4, loss=O.LOSS_MSE, act=O.ACT_RELU,
+                     shuffle_seed=4, min_delta=-1.0)
+  assert losses.size == 4
+  ms, rec, bat = ctx.train_stats()
+  assert rec == 4 * z["idx"].shape[0] and ms > 0
+  del K
+
+
+def test_train_rejects_out_of_range_rows(ctx):
+  z = golden("hobe_small.npz")
+  ctx.records_set(z["idx"], z["tgt"])
+  ctx.model_init(8, 3, 3, seed=1)  # far too few rows
+  with pytest.raises(AssertionError):
+    ctx.train(batch=64, max_epochs=1)
