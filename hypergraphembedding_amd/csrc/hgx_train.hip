@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "hgx_internal.h"
@@ -47,7 +48,11 @@ struct TrainArgs {
   int B, R, K, dp;
   float *ntab, *etab, *nacc, *eacc;
   float *gslot, *gzero, *lossbuf;
-  const int *ukey, *uoff, *slots, *ucount;
+  // chunk buffers written by train_prep: batch-ordered records, each
+  // slot's position in its batch's sorted (row, slot) order, unique keys
+  int *bidx;
+  float *btgt;
+  int *inv, *ukey, *uoff, *ucount;
   int *ctr;  // [0] K1 batch, [1] K2 batch, [2] chunk base batch, [3] chunk nb
   int SB, nblk1;
   float lr, eps;
@@ -128,9 +133,9 @@ __global__ __launch_bounds__(kTB) void train_fwd_bwd(TrainArgs a) {
   for (int v = 0; v < VPL; v++) zN[v] = zE[v] = f4(0.f);
   float lrec = 0.f;
   if (rib < nb) {
-    const int rec = a.perm[r0 + rib];
-    const int *ri = a.idx + (int64_t)rec * R;
-    const float *yt = a.tgt + (int64_t)rec * 3;
+    const int *ri = a.bidx + ((size_t)cb * a.B + rib) * R;
+    const float *yt = a.btgt + ((size_t)cb * a.B + rib) * 3;
+    const int *pos = a.inv + (size_t)cb * a.SB + (size_t)rib * R;
     const int ln = ri[0], le = ri[1], rn = ri[2], re = ri[3];
     int nnk[KMAX], nek[KMAX];
 #pragma unroll
@@ -202,7 +207,6 @@ __global__ __launch_bounds__(kTB) void train_fwd_bwd(TrainArgs a) {
     const float dz1 = g1 * act_d(act, z1, y1);
     const float dz2 = g2 * act_d(act, z2, y2);
     const float dP = g3 * Q / (float)K, dQ = g3 * P / (float)K;
-    float* gs = a.gslot + (size_t)rib * R * dp;
     auto emit = [&](int s, int row, bool edge, const float4(&g)[VPL]) {
       if (row == 0) {
 #pragma unroll
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(kTB) void train_fwd_bwd(TrainArgs a) {
           else zN[v] = zN[v] + g[v];
         }
       } else {
-        float4 *p = reinterpret_cast<float4 *>(gs + (size_t)s * dp);
+        float4 *p = reinterpret_cast<float4 *>(a.gslot + (size_t)pos[s] * dp);
 #pragma unroll
         for (int v = 0; v < VPL; v++) p[v * L + lane] = g[v];
       }
@@ -277,7 +281,6 @@ __global__ __launch_bounds__(kTB) void train_update(TrainArgs a) {
   const int U = a.ucount[cb];
   const int *ukey = a.ukey + (size_t)cb * a.SB;
   const int *uoff = a.uoff + (size_t)cb * (a.SB + 1);
-  const int *slots = a.slots + (size_t)cb * a.SB;
   const int grp = threadIdx.x / L, lane = threadIdx.x % L;
   const int dp = a.dp;
   for (int it = blockIdx.x * GPB + grp; it < U + 2; it += gridDim.x * GPB) {
@@ -289,21 +292,33 @@ __global__ __launch_bounds__(kTB) void train_update(TrainArgs a) {
       const int key = ukey[it];
       table = key >> 30;
       row = key & 0x3fffffff;
+      // this row's slot gradients are contiguous (prep sorted them)
       const int j1 = uoff[it + 1];
       for (int j = uoff[it]; j < j1; j++) {
-        const float4 *p = reinterpret_cast<const float4 *>(
-            a.gslot + (size_t)slots[j] * dp);
+        const float4 *p = reinterpret_cast<const float4 *>(a.gslot + (size_t)j * dp);
 #pragma unroll
         for (int v = 0; v < VPL; v++) g[v] = g[v] + p[v * L + lane];
       }
     } else {
       table = it - U;
       row = 0;
-      for (int b = 0; b < a.nblk1; b++) {
-        const float4 *p = reinterpret_cast<const float4 *>(
-            a.gzero + ((size_t)b * 2 + table) * dp);
+      // padding row: one partial per K1 workgroup, 8 loads in flight
+      const float4 *base = reinterpret_cast<const float4 *>(a.gzero + (size_t)table * dp);
+      const size_t bstride = (size_t)2 * dp / 4;
+      int b = 0;
+      for (; b + 8 <= a.nblk1; b += 8) {
 #pragma unroll
-        for (int v = 0; v < VPL; v++) g[v] = g[v] + p[v * L + lane];
+        for (int v = 0; v < VPL; v++) {
+          float4 t[8];
+#pragma unroll
+          for (int q = 0; q < 8; q++) t[q] = base[(b + q) * bstride + v * L + lane];
+#pragma unroll
+          for (int q = 0; q < 8; q++) g[v] = g[v] + t[q];
+        }
+      }
+      for (; b < a.nblk1; b++) {
+#pragma unroll
+        for (int v = 0; v < VPL; v++) g[v] = g[v] + base[b * bstride + v * L + lane];
       }
     }
     float4 *P = reinterpret_cast<float4 *>((table ? a.etab : a.ntab) + (size_t)row * dp);
@@ -362,12 +377,19 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
   const int nb = (int)min((int64_t)a.B, a.n - r0);
   const int R = a.R, K = a.K;
   const int S = nb * R;
+  int *bidx = a.bidx + (size_t)cb * a.B * R;
+  float *btgt = a.btgt + (size_t)cb * a.B * 3;
+  for (int t = threadIdx.x; t < nb * 3; t += kTB) {
+    const int i = t / 3;
+    btgt[t] = a.tgt[(int64_t)a.perm[r0 + i] * 3 + (t - 3 * i)];
+  }
   for (int t = threadIdx.x; t < P; t += kTB) {
     unsigned long long key = ~0ull;
     if (t < S) {
       const int i = t / R, s = t % R;
       const int rec = a.perm[r0 + i];
       const int row = a.idx[(int64_t)rec * R + s];
+      bidx[t] = row;
       if (row != 0) {
         const unsigned k32 = ((unsigned)slot_is_edge(s, K) << 30) | (unsigned)row;
         key = ((unsigned long long)k32 << 32) | (unsigned)t;
@@ -404,13 +426,13 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
   int U = 0, V = 0;
   int u = block_exclusive_scan(cnt, &U, s_ws);
   block_exclusive_scan(valid, &V, s_ws);
-  int *ukey = const_cast<int *>(a.ukey) + (size_t)cb * a.SB;
-  int *uoff = const_cast<int *>(a.uoff) + (size_t)cb * (a.SB + 1);
-  int *slots = const_cast<int *>(a.slots) + (size_t)cb * a.SB;
+  int *ukey = a.ukey + (size_t)cb * a.SB;
+  int *uoff = a.uoff + (size_t)cb * (a.SB + 1);
+  int *inv = a.inv + (size_t)cb * a.SB;
   for (int t = t0; t < t0 + per; t++) {
     const unsigned long long x = s_key[t];
     if (x == ~0ull) break;
-    slots[t] = (int)(x & 0xffffffffu);
+    inv[x & 0xffffffffu] = t;
     if (t == 0 || (unsigned)(s_key[t - 1] >> 32) != (unsigned)(x >> 32)) {
       ukey[u] = (int)(x >> 32);
       uoff[u] = t;
@@ -419,7 +441,7 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
   }
   if (threadIdx.x == 0) {
     uoff[U] = V;
-    const_cast<int *>(a.ucount)[cb] = U;
+    a.ucount[cb] = U;
   }
 }
 
@@ -430,14 +452,28 @@ __global__ void set_ctr(int *ctr, int base, int nbc) {
   ctr[3] = nbc;
 }
 
-// deterministic single-block sum of the chunk's per-block losses
-__global__ void loss_reduce(const float *lossbuf, int64_t m, double *acc) {
+// deterministic two-level sum of the chunk's per-block losses:
+// loss_partial (kLossBlocks blocks) then loss_final (one block)
+constexpr int kLossBlocks = 256;
+__global__ void loss_partial(const float *lossbuf, int64_t m, double *part) {
   __shared__ double s[kTB];
   double v = 0.0;
-  for (int64_t i = threadIdx.x; i < m; i += kTB) v += (double)lossbuf[i];
+  for (int64_t i = blockIdx.x * (int64_t)kTB + threadIdx.x; i < m;
+       i += (int64_t)kLossBlocks * kTB)
+    v += (double)lossbuf[i];
   s[threadIdx.x] = v;
   __syncthreads();
   for (int o = kTB / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = s[0];
+}
+__global__ void loss_final(const double *part, double *acc) {
+  __shared__ double s[kLossBlocks];
+  s[threadIdx.x] = part[threadIdx.x];
+  __syncthreads();
+  for (int o = kLossBlocks / 2; o > 0; o >>= 1) {
     if (threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
     __syncthreads();
   }
@@ -455,16 +491,27 @@ __global__ void shuffle_keys(uint64_t seed, int epoch, int64_t n,
 
 __global__ void max_index(const int *idx, int64_t n, int R, int K, int *out) {
   int mn = 0, me = 0, neg = 0;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-       i < n * R; i += (int64_t)gridDim.x * blockDim.x) {
-    const int s = (int)(i % R), v = idx[i];
-    neg |= v < 0;
-    if (slot_is_edge(s, K)) me = max(me, v);
-    else mn = max(mn, v);
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const int *p = idx + r * R;
+    for (int s = 0; s < R; s++) {
+      const int v = p[s];
+      neg |= v < 0;
+      if (slot_is_edge(s, K)) me = max(me, v);
+      else mn = max(mn, v);
+    }
   }
-  atomicMax(&out[0], mn);
-  atomicMax(&out[1], me);
-  atomicOr(&out[2], neg);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mn = max(mn, __shfl_xor(mn, off));
+    me = max(me, __shfl_xor(me, off));
+    neg |= __shfl_xor(neg, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&out[0], mn);
+    atomicMax(&out[1], me);
+    atomicOr(&out[2], neg);
+  }
 }
 
 __global__ void init_uniform(float *tab, int64_t rows, int d, int dp,
@@ -703,7 +750,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   // indices must fit the tables (kernels do not bounds-check)
   HGX_TRY(hgx_ensure(ctx, ctx->s0, 16));
   HGX_HIP(ctx, hipMemsetAsync(ctx->s0.p, 0, 16, ctx->stream));
-  hipLaunchKernelGGL(max_index, dim3(grid_for(n * R, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(max_index, dim3(grid_for(n, 256)), dim3(256), 0,
                      ctx->stream, ctx->rec_idx.as<int>(), n, R, K,
                      ctx->s0.as<int>());
   HGX_LAUNCH_CHECK(ctx);
@@ -724,10 +771,10 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   const int RPB = kTB / L;
   const int nblk1 = (batch + RPB - 1) / RPB;
   const int GPB2 = kTB / L;
-  const int grid2 = std::max(1, std::min(1024, (SB + 2 + GPB2 - 1) / GPB2));
+  const int grid2 = std::max(1, std::min(256, (SB + 2 + GPB2 - 1) / GPB2));
   const int64_t nbatches = (n + batch - 1) / batch;
   // chunk of batches whose unique-row lists are prepared together (<=~1 GB)
-  const int64_t per_batch = (int64_t)SB * 3 + 2;
+  const int64_t per_batch = (int64_t)SB * 4 + 3 * batch + 2;
   const int CB = (int)std::max<int64_t>(
       1, std::min<int64_t>(nbatches, (int64_t)(256ll << 20) / per_batch));
 
@@ -736,8 +783,8 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   HGX_TRY(hgx_ensure(ctx, ctx->s2, sizeof(float) * (size_t)SB * dp));    // gslot
   HGX_TRY(hgx_ensure(ctx, ctx->s3, sizeof(float) * (size_t)nblk1 * 2 * dp));
   HGX_TRY(hgx_ensure(ctx, ctx->s4, sizeof(float) * (size_t)CB * nblk1 + 16));
-  HGX_TRY(hgx_ensure(ctx, ctx->s5, sizeof(int) * ((size_t)CB * (3 * (size_t)SB + 2) + 8)));
-  HGX_TRY(hgx_ensure(ctx, ctx->s6, 64));                                // ctr + loss acc
+  HGX_TRY(hgx_ensure(ctx, ctx->s5, sizeof(int) * ((size_t)CB * per_batch + 8)));
+  HGX_TRY(hgx_ensure(ctx, ctx->s6, 64 + sizeof(double) * kLossBlocks));  // ctr, loss
   int *perm = ctx->s1.as<int>();
   int *prep = ctx->s5.as<int>();
   TrainArgs a;
@@ -756,12 +803,15 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   a.gslot = ctx->s2.as<float>();
   a.gzero = ctx->s3.as<float>();
   a.lossbuf = ctx->s4.as<float>();
-  a.ukey = prep;
-  a.slots = prep + (size_t)CB * SB;
-  a.uoff = prep + (size_t)CB * SB * 2;
-  a.ucount = prep + (size_t)CB * (3 * (size_t)SB + 1);
+  a.bidx = prep;                                         // CB*SB
+  a.inv = prep + (size_t)CB * SB;                        // CB*SB
+  a.ukey = prep + (size_t)CB * SB * 2;                   // CB*SB
+  a.uoff = prep + (size_t)CB * SB * 3;                   // CB*(SB+1)
+  a.btgt = reinterpret_cast<float *>(prep + (size_t)CB * (4 * (size_t)SB + 1));  // CB*B*3
+  a.ucount = prep + (size_t)CB * (4 * (size_t)SB + 1 + 3 * (size_t)batch);      // CB
   a.ctr = ctx->s6.as<int>();
   double *dloss = reinterpret_cast<double *>(ctx->s6.as<char>() + 32);
+  double *dpart = reinterpret_cast<double *>(ctx->s6.as<char>() + 64);
   a.SB = SB;
   a.nblk1 = nblk1;
   a.lr = lr;
@@ -784,21 +834,27 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     vals_in = reinterpret_cast<int *>(keys_out + n);
   }
 
-  // graph: kGraphBatches x [K1, K2]
+  // graph: kGraphBatches x [K1, K2]. HGX_NO_GRAPH=1 launches the same
+  // kernels directly (profilers that mishandle graph replay).
   const int GB = (int)std::min<int64_t>(kGraphBatches, CB);
+  const char *nog = getenv("HGX_NO_GRAPH");
+  const bool use_graph = !(nog && nog[0] == '1');
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;
-  HGX_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
-  for (int b = 0; b < GB; b++) {
-    hipLaunchKernelGGL(k1, dim3(nblk1), dim3(kTB), 0, ctx->stream, a);
-    hipLaunchKernelGGL(k2, dim3(grid2), dim3(kTB), 0, ctx->stream, a);
-  }
-  hipError_t ce = hipStreamEndCapture(ctx->stream, &graph);
-  if (ce != hipSuccess) return hgx_fail(ctx, HGX_EHIP, "graph capture failed: %s", hipGetErrorString(ce));
-  ce = hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0);
-  if (ce != hipSuccess) {
-    hipGraphDestroy(graph);
-    return hgx_fail(ctx, HGX_EHIP, "graph instantiate failed: %s", hipGetErrorString(ce));
+  if (use_graph) {
+    HGX_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
+    for (int b = 0; b < GB; b++) {
+      hipLaunchKernelGGL(k1, dim3(nblk1), dim3(kTB), 0, ctx->stream, a);
+      hipLaunchKernelGGL(k2, dim3(grid2), dim3(kTB), 0, ctx->stream, a);
+    }
+    hipError_t ce = hipStreamEndCapture(ctx->stream, &graph);
+    if (ce != hipSuccess)
+      return hgx_fail(ctx, HGX_EHIP, "graph capture failed: %s", hipGetErrorString(ce));
+    ce = hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0);
+    if (ce != hipSuccess) {
+      hipGraphDestroy(graph);
+      return hgx_fail(ctx, HGX_EHIP, "graph instantiate failed: %s", hipGetErrorString(ce));
+    }
   }
 
   std::vector<int> hperm;
@@ -844,15 +900,24 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
       hipLaunchKernelGGL(train_prep, dim3(nbc), dim3(kTB),
                          (size_t)P * sizeof(unsigned long long), ctx->stream, a,
                          base, nbc, P);
-      for (int g = 0; g < nbc; g += GB) {
-        if (hipGraphLaunch(gexec, ctx->stream) != hipSuccess) {
-          rc = hgx_fail(ctx, HGX_EHIP, "graph launch failed");
-          break;
+      if (use_graph) {
+        for (int g = 0; g < nbc; g += GB) {
+          if (hipGraphLaunch(gexec, ctx->stream) != hipSuccess) {
+            rc = hgx_fail(ctx, HGX_EHIP, "graph launch failed");
+            break;
+          }
+        }
+      } else {
+        for (int g = 0; g < nbc; g++) {
+          hipLaunchKernelGGL(k1, dim3(nblk1), dim3(kTB), 0, ctx->stream, a);
+          hipLaunchKernelGGL(k2, dim3(grid2), dim3(kTB), 0, ctx->stream, a);
         }
       }
       if (rc) break;
-      hipLaunchKernelGGL(loss_reduce, dim3(1), dim3(kTB), 0, ctx->stream,
-                         a.lossbuf, (int64_t)nbc * nblk1, dloss);
+      hipLaunchKernelGGL(loss_partial, dim3(kLossBlocks), dim3(kTB), 0,
+                         ctx->stream, a.lossbuf, (int64_t)nbc * nblk1, dpart);
+      hipLaunchKernelGGL(loss_final, dim3(1), dim3(kLossBlocks), 0,
+                         ctx->stream, dpart, dloss);
     }
     if (rc) break;
     double lsum = 0.0;
@@ -876,8 +941,8 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   hipEventSynchronize(ctx->ev1);
   float ms = 0.f;
   hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
-  hipGraphExecDestroy(gexec);
-  hipGraphDestroy(graph);
+  if (gexec) hipGraphExecDestroy(gexec);
+  if (graph) hipGraphDestroy(graph);
   if (rc) return rc;
   HGX_LAUNCH_CHECK(ctx);
   ctx->train_ms = ms;
