@@ -126,6 +126,36 @@ __global__ void incidence_weight_kernel(int which, double alpha, int R,
   }
 }
 
+// HOBE targets for records [b, e) of one kind (ids in the records are +1)
+__global__ void fill_probs_kernel(int kind, int64_t b, int64_t e, int R,
+                                  const int *__restrict__ idx,
+                                  float *__restrict__ tgt,
+                                  const int *__restrict__ rp_n,
+                                  const int *__restrict__ col_n,
+                                  const int *__restrict__ rp_e,
+                                  const int *__restrict__ col_e,
+                                  const float *__restrict__ X,
+                                  const float *__restrict__ Y, int KS, int k) {
+  for (int64_t q = b + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < e;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int *ri = idx + q * R;
+    float p;
+    if (kind == 0) {
+      p = same_type_prob(rp_n, col_n, ri[0] - 1, ri[2] - 1, X, Y, KS, k);
+    } else if (kind == 1) {
+      p = same_type_prob(rp_e, col_e, ri[1] - 1, ri[3] - 1, Y, X, KS, k);
+    } else {
+      const int v = ri[0] - 1, ed = ri[3] - 1;
+      p = 0.f;
+      for (int t = rp_n[v]; t < rp_n[v + 1]; t++) {
+        const float pe = same_type_prob(rp_e, col_e, ed, col_n[t], Y, X, KS, k);
+        if (pe > p) p = pe;
+      }
+    }
+    tgt[q * 3 + kind] = p;
+  }
+}
+
 int grid_for(int64_t work, int per_block) {
   int64_t g = (work + per_block - 1) / per_block;
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, 4096));
@@ -221,5 +251,19 @@ extern "C" int hgx_incidence_weights(hgx_ctx *ctx, int which, double alpha,
                                 hipMemcpyDeviceToHost, ctx->stream));
     HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   }
+  return HGX_OK;
+}
+
+// Used by hgx_sample_hobe: fill the probability target of records [b, e).
+int hgx_hobe_fill_probs(hgx_ctx *ctx, int kind, int64_t b, int64_t e) {
+  if (e <= b) return HGX_OK;
+  hipLaunchKernelGGL(fill_probs_kernel, dim3(grid_for(e - b, 256)), dim3(256),
+                     0, ctx->stream, kind, b, e, 4 + 2 * ctx->K,
+                     ctx->rec_idx.as<int>(), ctx->rec_tgt.as<float>(),
+                     ctx->rp_n.as<int>(), ctx->col_n.as<int>(),
+                     ctx->rp_e.as<int>(), ctx->col_e.as<int>(),
+                     ctx->X[ctx->xcur].as<float>(),
+                     ctx->Y[ctx->ycur].as<float>(), ctx->ks, ctx->k);
+  HGX_LAUNCH_CHECK(ctx);
   return HGX_OK;
 }
