@@ -25,6 +25,7 @@
 // 2*KS min/max words (MAX).
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -37,7 +38,15 @@ using hgx::ord2f;
 namespace {
 
 constexpr int kBlock = 256;
+// min/max words are spread over kRep replicas (workgroup b adds to replica
+// b % kRep): 2048 workgroups on one word serialise at the memory-side
+// atomic unit (~90 us per sweep); 32 per word do not. Readers fold the
+// replicas once per workgroup into LDS.
+constexpr int kRep = 64;
 enum { MODE_FULL = 0, MODE_PARTIAL = 1 };
+// diagnostic ablation bits (HGX_ALG_ABLATE, timing experiments only):
+// 1 = skip the min/max flush, 2 = skip the source gathers
+__constant__ int g_ablate = 0;
 
 __device__ __forceinline__ float4 f4fma(float w, float4 v, float4 a) {
   return make_float4(fmaf(w, v.x, a.x), fmaf(w, v.y, a.y), fmaf(w, v.z, a.z),
@@ -53,29 +62,52 @@ __device__ __forceinline__ void f4set(float4 &v, int c, float x) {
   else v.w = x;
 }
 
-// min and delta of the previous iteration's rescale for slot i (identity
-// when there is none).
-__device__ __forceinline__ void affine_of(const int *mm_prev, int KS, int i,
-                                          float &m, float &dl) {
-  if (mm_prev) {
-    m = ord2f(~mm_prev[KS + i]);
-    dl = ord2f(mm_prev[i]) - m;
-  } else {
-    m = 0.f;
-    dl = 1.f;
-  }
-}
-
-template <int KS>
-__device__ __forceinline__ void load_affine(const int *mm_prev, int k,
-                                            float *s_m, float *s_d) {
+// Fold the kRep replicas of the previous iteration's min/max (layout
+// [2*KS][kRep]) into s_m (min) and s_d (max - min) for slots 0..KS-1;
+// identity when there is no previous iteration. Whole block, ends with a
+// barrier.
+// s_d = max - min, or 1 / (max - min) when `inverse` (narrow kernels).
+__device__ void load_affine(const int *mm_prev, int KS, int k, float *s_m,
+                            float *s_d, bool inverse = false) {
   const int tid = threadIdx.x;
-  if (tid < KS) {
-    float m = 0.f, dl = 1.f;
-    if (tid >= 1 && tid <= k) affine_of(mm_prev, KS, tid, m, dl);
-    s_m[tid] = m;
-    s_d[tid] = dl;
+  const int lane = tid & 63, wave = tid >> 6;
+  static_assert(kRep == 64, "one wave folds one slot");
+  constexpr int W = kBlock / 64;
+  constexpr int B = 8;  // slots per wave per batch: all loads issued first
+  for (int i0 = wave; i0 < KS; i0 += W * B) {
+    int mx[B], mn[B];
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+      const int i = i0 + W * b;
+      const bool live = mm_prev && i >= 1 && i <= k && i < KS;
+      mx[b] = live ? mm_prev[(size_t)i * kRep + lane] : 0;
+      mn[b] = live ? mm_prev[(size_t)(KS + i) * kRep + lane] : 0;
+    }
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        mx[b] = max(mx[b], __shfl_xor(mx[b], off));
+        mn[b] = max(mn[b], __shfl_xor(mn[b], off));
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int b = 0; b < B; b++) {
+        const int i = i0 + W * b;
+        if (i < KS) {
+          float m = 0.f, dl = 1.f;
+          if (mm_prev && i >= 1 && i <= k) {
+            m = ord2f(~mn[b]);
+            dl = ord2f(mx[b]) - m;
+          }
+          s_m[i] = m;
+          s_d[i] = inverse ? 1.0f / dl : dl;
+        }
+      }
+    }
   }
+  __syncthreads();
 }
 
 // Block-wide min/max of per-thread partials -> 2k atomics per workgroup.
@@ -109,8 +141,9 @@ __device__ __forceinline__ void flush_minmax(const float (&lmn)[KS],
       b = fmaxf(b, s_red[1][w][tid]);
     }
     if (b >= a) {
-      atomicMax(&mm_cur[tid], f2ord(b));
-      atomicMax(&mm_cur[KS + tid], ~f2ord(a));
+      const int r = blockIdx.x % kRep;
+      atomicMax(&mm_cur[(size_t)tid * kRep + r], f2ord(b));
+      atomicMax(&mm_cur[(size_t)(KS + tid) * kRep + r], ~f2ord(a));
     }
   }
 }
@@ -121,7 +154,7 @@ __device__ __forceinline__ void flush_minmax(const float (&lmn)[KS],
 // xor-shuffle reduction over the G lanes; lane 0 of the group writes.
 //   MODE_FULL:    out[r] = [1/len, (s(self) + s?(sum w*src / sum w)) / 2]
 //   MODE_PARTIAL: out[r] = [sum w, sum w*src]    (no self, no min/max)
-template <int KS, int G, int MODE>
+template <int KS, int G, int MODE, int M>
 __global__ __launch_bounds__(kBlock) void algdist_half_narrow(
     int row0, int R, const int *__restrict__ rp, const int *__restrict__ col,
     const float *__restrict__ self_in, const float *__restrict__ src,
@@ -129,8 +162,7 @@ __global__ __launch_bounds__(kBlock) void algdist_half_narrow(
     int *__restrict__ mm_cur, int k) {
   constexpr int NV = KS / 4;
   __shared__ float s_m[KS], s_d[KS];
-  load_affine<KS>(mm_prev, k, s_m, s_d);
-  __syncthreads();
+  load_affine(mm_prev, KS, k, s_m, s_d, true);
   const int tid = threadIdx.x;
   const int lg = tid % G;
   constexpr int GPB = kBlock / G;
@@ -145,68 +177,77 @@ __global__ __launch_bounds__(kBlock) void algdist_half_narrow(
   for (int rr = blockIdx.x * GPB + tid / G; rr < R; rr += ngroups) {
     const int r = row0 + rr;
     const int beg = rp[r], end = rp[r + 1];
+    // own row early (MODE_FULL): its latency hides under the gathers
+    // lane lg owns output vectors j = lg, lg + G, ...
+    float4 self[NV];
+    if (MODE == MODE_FULL) {
+      const float4 *sp = reinterpret_cast<const float4 *>(self_in) + (size_t)r * NV;
+#pragma unroll
+      for (int j = 0; j < NV; j++)
+        if (j % G == lg) self[j] = sp[j];
+    }
     float4 acc[NV];
 #pragma unroll
     for (int j = 0; j < NV; j++) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
     float wsum = 0.f;
-    int t = beg + lg;
-    for (; t + G < end; t += 2 * G) {
-      const int c0 = col[t], c1 = col[t + G];
-      float4 v0[NV], v1[NV];
+    for (int base = beg + lg; base < end; base += G * M) {
+      int c[M];
 #pragma unroll
-      for (int j = 0; j < NV; j++) v0[j] = src4[(size_t)c0 * NV + j];
+      for (int m = 0; m < M; m++) {
+        const int t = base + G * m;
+        c[m] = t < end ? ((g_ablate & 2) ? -2 : col[t]) : -1;
+      }
+      float4 v[M][NV];
 #pragma unroll
-      for (int j = 0; j < NV; j++) v1[j] = src4[(size_t)c1 * NV + j];
-      const float w0 = v0[0].x, w1 = v1[0].x;
-      wsum += w0;
-      wsum += w1;
+      for (int m = 0; m < M; m++) {
+        if (c[m] >= 0) {
 #pragma unroll
-      for (int j = 0; j < NV; j++) acc[j] = f4fma(w1, v1[j], f4fma(w0, v0[j], acc[j]));
-    }
-    if (t < end) {
-      const int c0 = col[t];
-      float4 v0[NV];
+          for (int j = 0; j < NV; j++) v[m][j] = src4[(size_t)c[m] * NV + j];
+        }
+      }
 #pragma unroll
-      for (int j = 0; j < NV; j++) v0[j] = src4[(size_t)c0 * NV + j];
-      const float w0 = v0[0].x;
-      wsum += w0;
+      for (int m = 0; m < M; m++) {
+        if (c[m] >= 0) {
+          const float w = v[m][0].x;
+          wsum += w;
 #pragma unroll
-      for (int j = 0; j < NV; j++) acc[j] = f4fma(w0, v0[j], acc[j]);
-    }
-#pragma unroll
-    for (int off = G / 2; off > 0; off >>= 1) {
-      wsum += __shfl_xor(wsum, off);
-#pragma unroll
-      for (int j = 0; j < NV; j++) {
-        acc[j].x += __shfl_xor(acc[j].x, off);
-        acc[j].y += __shfl_xor(acc[j].y, off);
-        acc[j].z += __shfl_xor(acc[j].z, off);
-        acc[j].w += __shfl_xor(acc[j].w, off);
+          for (int j = 0; j < NV; j++) acc[j] = f4fma(w, v[m][j], acc[j]);
+        }
       }
     }
-    if (lg == 0) {
+    wsum = hgx::group_allreduce_sum<G>(wsum);
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+      acc[j].x = hgx::group_allreduce_sum<G>(acc[j].x);
+      acc[j].y = hgx::group_allreduce_sum<G>(acc[j].y);
+      acc[j].z = hgx::group_allreduce_sum<G>(acc[j].z);
+      acc[j].w = hgx::group_allreduce_sum<G>(acc[j].w);
+    }
+    {
       float4 *op = reinterpret_cast<float4 *>(out) + (size_t)r * NV;
       if (MODE == MODE_PARTIAL) {
         acc[0].x = wsum;
 #pragma unroll
-        for (int j = 0; j < NV; j++) op[j] = acc[j];
+        for (int j = 0; j < NV; j++)
+          if (j % G == lg) op[j] = acc[j];
       } else {
-        const float4 *sp = reinterpret_cast<const float4 *>(self_in) + (size_t)r * NV;
-        const float own_w = 1.0f / (float)(end - beg);
+        // one reciprocal per row; per-dim 1/(max-min) comes from LDS
+        const float inv_w = 1.0f / wsum;
 #pragma unroll
         for (int j = 0; j < NV; j++) {
-          const float4 s = sp[j];
+          if (j % G != lg) continue;
+          const float4 s = self[j];
           float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
           for (int c = 0; c < 4; c++) {
             const int i = 4 * j + c;
             float v;
             if (i == 0) {
-              v = own_w;
+              v = 1.0f / (float)(end - beg);
             } else if (i <= k) {
-              const float sv = (f4get(s, c) - s_m[i]) / s_d[i];
-              float mv = f4get(acc[j], c) / wsum;
-              if (src_affine) mv = (mv - s_m[i]) / s_d[i];
+              const float sv = (f4get(s, c) - s_m[i]) * s_d[i];
+              float mv = f4get(acc[j], c) * inv_w;
+              if (src_affine) mv = (mv - s_m[i]) * s_d[i];
               v = (sv + mv) * 0.5f;
               lmn[i] = fminf(lmn[i], v);
               lmx[i] = fmaxf(lmx[i], v);
@@ -220,7 +261,161 @@ __global__ __launch_bounds__(kBlock) void algdist_half_narrow(
       }
     }
   }
-  if (MODE == MODE_FULL) flush_minmax<KS>(lmn, lmx, k, mm_cur);
+  if (MODE == MODE_FULL && !(g_ablate & 1)) flush_minmax<KS>(lmn, lmx, k, mm_cur);
+}
+
+// Incidence-parallel half-sweep for narrow rows (KS <= 20). Rows are cut
+// into row-blocks (<= kBlkRows whole rows, <= kBlkNnz incidences; a longer
+// row is a block by itself). One wave owns a block: its lanes take
+// consecutive incidences (coalesced col loads, kFlatU windows of gathers in
+// flight per lane), fold w*src into per-row LDS accumulators, then one lane
+// per row finishes: MODE_FULL writes [1/len, (s(self) + s?(mean)) / 2] and
+// tracks min/max; MODE_PARTIAL writes [sum w, sum w*src].
+constexpr int kFlatU = 4;
+constexpr int kBlkRows = 64;   // keep in sync with hgx_make_row_blocks
+constexpr int kBlkNnz = 256;
+
+template <int KS, int MODE>
+__global__ __launch_bounds__(kBlock) void algdist_half_flat(
+    int nblk, const int *__restrict__ blk, const int *__restrict__ rp,
+    const int *__restrict__ col, const float *__restrict__ self_in,
+    const float *__restrict__ src, float *__restrict__ out,
+    const int *__restrict__ mm_prev, int src_affine, int *__restrict__ mm_cur,
+    int k) {
+  constexpr int NV = KS / 4;
+  constexpr int W = kBlock / 64;
+  constexpr int AS = KS + 1;  // odd stride: conflict-free per-row reads
+  __shared__ float s_acc[W][kBlkRows * AS];
+  __shared__ int s_rp[W][kBlkRows + 1];
+  __shared__ float s_m[KS], s_d[KS];
+  load_affine(mm_prev, KS, k, s_m, s_d, true);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float lmn[KS], lmx[KS];
+#pragma unroll
+  for (int i = 0; i < KS; i++) {
+    lmn[i] = INFINITY;
+    lmx[i] = -INFINITY;
+  }
+  const float4 *src4 = reinterpret_cast<const float4 *>(src);
+  float *acc = s_acc[wv];
+  int *srp = s_rp[wv];
+  for (int b = blockIdx.x * W + wv; b < nblk; b += gridDim.x * W) {
+    const int rA = blk[b], nr = blk[b + 1] - rA;
+    for (int i = lane; i <= nr; i += 64) srp[i] = rp[rA + i];
+    for (int i = lane; i < nr * AS; i += 64) acc[i] = 0.f;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int tA = srp[0], tB = srp[nr];
+    for (int base = tA; base < tB; base += 64 * kFlatU) {  // wave-uniform
+      const int t0 = base + lane;
+      int c[kFlatU];
+#pragma unroll
+      for (int u = 0; u < kFlatU; u++) {
+        const int t = t0 + 64 * u;
+        c[u] = t < tB ? ((g_ablate & 2) ? -2 : col[t]) : -1;
+      }
+      float4 v[kFlatU][NV];
+#pragma unroll
+      for (int u = 0; u < kFlatU; u++)
+        if (c[u] >= 0) {
+#pragma unroll
+          for (int j = 0; j < NV; j++) v[u][j] = src4[(size_t)c[u] * NV + j];
+        }
+#pragma unroll
+      for (int u = 0; u < kFlatU; u++) {
+        const int t = t0 + 64 * u;
+        // local row of incidence t: last i with srp[i] <= t (-1: no incidence)
+        int rl = -1;
+        if (c[u] >= 0) {
+          int lo = 0, hi = nr - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (srp[mid] <= t) lo = mid;
+            else hi = mid - 1;
+          }
+          rl = lo;
+        }
+        // segmented inclusive scan over the wave: a row's incidences are
+        // consecutive lanes, so its sum lands in the row's last lane
+        float val[KS];
+        const float w = c[u] >= 0 ? v[u][0].x : 0.f;
+        val[0] = w;
+#pragma unroll
+        for (int j = 0; j < NV; j++)
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const int i = 4 * j + q;
+            if (i >= 1) val[i] = (c[u] >= 0 && i <= k) ? w * f4get(v[u][j], q) : 0.f;
+          }
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int pr = __shfl_up(rl, d);
+          const bool add = lane >= d && pr == rl;
+#pragma unroll
+          for (int i = 0; i < KS; i++) {
+            const float o = __shfl_up(val[i], d);
+            if (add) val[i] += o;
+          }
+        }
+        const int nx = __shfl_down(rl, 1);
+        if (rl >= 0 && (lane == 63 || nx != rl)) {
+          float *ar = acc + rl * AS;
+#pragma unroll
+          for (int i = 0; i < KS; i++)
+            if (i <= k) ar[i] += val[i];
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int l = lane; l < nr; l += 64) {
+      const int r = rA + l;
+      const float *ar = acc + l * AS;
+      float4 *op = reinterpret_cast<float4 *>(out) + (size_t)r * NV;
+      if (MODE == MODE_PARTIAL) {
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+          float4 o;
+#pragma unroll
+          for (int q = 0; q < 4; q++) f4set(o, q, ar[4 * j + q]);
+          op[j] = o;
+        }
+      } else {
+        const float4 *sp = reinterpret_cast<const float4 *>(self_in) + (size_t)r * NV;
+        const float inv_w = 1.0f / ar[0];
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+          const float4 sv4 = sp[j];
+          float4 o;
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const int i = 4 * j + q;
+            float v;
+            if (i == 0) {
+              v = 1.0f / (float)(srp[l + 1] - srp[l]);
+            } else if (i <= k) {
+              const float sv = (f4get(sv4, q) - s_m[i]) * s_d[i];
+              float mv = ar[i] * inv_w;
+              if (src_affine) mv = (mv - s_m[i]) * s_d[i];
+              v = (sv + mv) * 0.5f;
+              lmn[i] = fminf(lmn[i], v);
+              lmx[i] = fmaxf(lmx[i], v);
+            } else {
+              v = 0.f;
+            }
+            f4set(o, q, v);
+          }
+          op[j] = o;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (MODE == MODE_FULL && !(g_ablate & 1)) flush_minmax<KS>(lmn, lmx, k, mm_cur);
 }
 
 // Wide rows (k > 19): one wave per destination row, the row's float4
@@ -233,6 +428,8 @@ __global__ __launch_bounds__(kBlock) void algdist_half_wide(
     const int *__restrict__ mm_prev, int src_affine, int *__restrict__ mm_cur,
     int k) {
   const int NV = KS / 4;
+  __shared__ float s_m[2048], s_d[2048];
+  load_affine(mm_prev, KS, k, s_m, s_d);
   const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   const int nw = gridDim.x * (kBlock / 64);
@@ -251,15 +448,28 @@ __global__ __launch_bounds__(kBlock) void algdist_half_wide(
 #pragma unroll
     for (int q = 0; q < MAXV; q++) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     float wsum = 0.f;
-    for (int t = beg; t < end; t++) {
-      const int c = col[t];
-      const float w = src[(size_t)c * KS];
-      wsum += w;
+    constexpr int U = 8;  // incidences in flight per wave
+    for (int t0 = beg; t0 < end; t0 += U) {
+      int c[U];
+      float w[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) c[u] = t0 + u < end ? col[t0 + u] : -1;
+#pragma unroll
+      for (int u = 0; u < U; u++) w[u] = c[u] >= 0 ? src[(size_t)c[u] * KS] : 0.f;
 #pragma unroll
       for (int q = 0; q < MAXV; q++) {
         const int j = lane + 64 * q;
-        if (j < NV) acc[q] = f4fma(w, src4[(size_t)c * NV + j], acc[q]);
+        if (j < NV) {
+          float4 v[U];
+#pragma unroll
+          for (int u = 0; u < U; u++)
+            v[u] = c[u] >= 0 ? src4[(size_t)c[u] * NV + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int u = 0; u < U; u++) acc[q] = f4fma(w[u], v[u], acc[q]);
+        }
       }
+#pragma unroll
+      for (int u = 0; u < U; u++) wsum += w[u];
     }
     const float own_w = 1.0f / (float)(end - beg);
 #pragma unroll
@@ -279,8 +489,7 @@ __global__ __launch_bounds__(kBlock) void algdist_half_wide(
           if (i == 0) {
             v = own_w;
           } else if (i <= k) {
-            float m, dl;
-            affine_of(mm_prev, KS, i, m, dl);
+            const float m = s_m[i], dl = s_d[i];
             const float sv = (f4get(s, c) - m) / dl;
             float mv = f4get(acc[q], c) / wsum;
             if (src_affine) mv = (mv - m) / dl;
@@ -303,8 +512,9 @@ __global__ __launch_bounds__(kBlock) void algdist_half_wide(
     for (int c = 0; c < 4; c++) {
       const int i = 4 * j + c;
       if (i >= 1 && i <= k && lmx[4 * q + c] >= lmn[4 * q + c]) {
-        atomicMax(&mm_cur[i], f2ord(lmx[4 * q + c]));
-        atomicMax(&mm_cur[KS + i], ~f2ord(lmn[4 * q + c]));
+        const int r = (int)((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) % kRep);
+        atomicMax(&mm_cur[(size_t)i * kRep + r], f2ord(lmx[4 * q + c]));
+        atomicMax(&mm_cur[(size_t)(KS + i) * kRep + r], ~f2ord(lmn[4 * q + c]));
       }
     }
   }
@@ -318,8 +528,9 @@ __global__ __launch_bounds__(kBlock) void algdist_edge_final(
     float *__restrict__ out, const int *__restrict__ mm_prev,
     int *__restrict__ mm_cur) {
   __shared__ int s_mm[4096];  // 2 * KS, KS <= 2048
+  __shared__ float s_m[2048], s_d[2048];
   for (int i = threadIdx.x; i < 2 * KS; i += blockDim.x) s_mm[i] = INT_MIN;
-  __syncthreads();
+  load_affine(mm_prev, KS, k, s_m, s_d);
   const int64_t total = (int64_t)E * KS;
   for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < total;
        q += (int64_t)gridDim.x * blockDim.x) {
@@ -328,9 +539,7 @@ __global__ __launch_bounds__(kBlock) void algdist_edge_final(
     if (i == 0) {
       v = 1.0f / (float)(rp_e[e + 1] - rp_e[e]);
     } else if (i <= k) {
-      float m, dl;
-      affine_of(mm_prev, KS, i, m, dl);
-      const float sv = (self_in[q] - m) / dl;
+      const float sv = (self_in[q] - s_m[i]) / s_d[i];
       const float mv = part[q] / part[(int64_t)e * KS];
       v = (sv + mv) * 0.5f;
       atomicMax(&s_mm[i], f2ord(v));
@@ -341,7 +550,8 @@ __global__ __launch_bounds__(kBlock) void algdist_edge_final(
   __syncthreads();
   for (int i = threadIdx.x; i < 2 * KS; i += blockDim.x) {
     const int s = i % KS;
-    if (s >= 1 && s <= k && s_mm[i] != INT_MIN) atomicMax(&mm_cur[i], s_mm[i]);
+    if (s >= 1 && s <= k && s_mm[i] != INT_MIN)
+      atomicMax(&mm_cur[(size_t)i * kRep + blockIdx.x % kRep], s_mm[i]);
   }
 }
 
@@ -361,19 +571,17 @@ __global__ void pack_rows(int R, int k, int KS, const int *__restrict__ rp,
 }
 
 // In place on rows [row0, row0+R): apply the affine of mm to slots 1..k.
-__global__ void apply_affine(int row0, int R, int k, int KS,
-                             float *__restrict__ rows,
-                             const int *__restrict__ mm) {
+__global__ __launch_bounds__(kBlock) void apply_affine(
+    int row0, int R, int k, int KS, float *__restrict__ rows,
+    const int *__restrict__ mm) {
+  __shared__ float s_m[2048], s_d[2048];
+  load_affine(mm, KS, k, s_m, s_d);
   const int64_t total = (int64_t)R * KS;
   float *base = rows + (int64_t)row0 * KS;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int s = (int)(i % KS);
-    if (s >= 1 && s <= k) {
-      float m, dl;
-      affine_of(mm, KS, s, m, dl);
-      base[i] = (base[i] - m) / dl;
-    }
+    if (s >= 1 && s <= k) base[i] = (base[i] - s_m[s]) / s_d[s];
   }
 }
 
@@ -402,31 +610,80 @@ __global__ void fill_int(int *p, int64_t n, int v) {
     p[i] = v;
 }
 
-int grid_for(int64_t work, int per_block) {
+int grid_for(int64_t work, int per_block, int cap = 2048) {
   int64_t g = (work + per_block - 1) / per_block;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(g, 2048));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+// One resident round of workgroups: each amortises its prologue (the
+// min/max replica fold) and its flush over many rows.
+template <class F>
+int resident_grid(F fn) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, 0) !=
+          hipSuccess || per_cu <= 0)
+    per_cu = 2;
+  return cus * per_cu;
 }
 
 int pick_g(double avg) {
+  static const int lpi = [] {  // incidences per lane targeted
+    const char *e = getenv("HGX_ALG_LPI");
+    return e ? atoi(e) : 4;
+  }();
   int g = 1;
-  while (g < 64 && g * 4 < avg) g *= 2;
+  while (g < 64 && g * lpi < avg) g *= 2;
   return g;
 }
 
 using HalfFn = void (*)(int, int, const int *, const int *, const float *,
                         const float *, float *, const int *, int, int *, int);
+using FlatFn = void (*)(int, const int *, const int *, const int *,
+                        const float *, const float *, float *, const int *, int,
+                        int *, int);
+
+template <int MODE>
+FlatFn flat_fn(int ks) {
+  switch (ks) {
+    case 4: return algdist_half_flat<4, MODE>;
+    case 8: return algdist_half_flat<8, MODE>;
+    case 12: return algdist_half_flat<12, MODE>;
+    case 16: return algdist_half_flat<16, MODE>;
+    case 20: return algdist_half_flat<20, MODE>;
+    default: return nullptr;
+  }
+}
+
+// M = incidences in flight per lane
+template <int KS, int MODE, int M>
+HalfFn narrow_for_gm(int g) {
+  switch (g) {
+    case 1: return algdist_half_narrow<KS, 1, MODE, M>;
+    case 2: return algdist_half_narrow<KS, 2, MODE, M>;
+    case 4: return algdist_half_narrow<KS, 4, MODE, M>;
+    case 8: return algdist_half_narrow<KS, 8, MODE, M>;
+    case 16: return algdist_half_narrow<KS, 16, MODE, M>;
+    case 32: return algdist_half_narrow<KS, 32, MODE, M>;
+    default: return algdist_half_narrow<KS, 64, MODE, M>;
+  }
+}
 
 template <int KS, int MODE>
 HalfFn narrow_for_g(int g) {
-  switch (g) {
-    case 1: return algdist_half_narrow<KS, 1, MODE>;
-    case 2: return algdist_half_narrow<KS, 2, MODE>;
-    case 4: return algdist_half_narrow<KS, 4, MODE>;
-    case 8: return algdist_half_narrow<KS, 8, MODE>;
-    case 16: return algdist_half_narrow<KS, 16, MODE>;
-    case 32: return algdist_half_narrow<KS, 32, MODE>;
-    default: return algdist_half_narrow<KS, 64, MODE>;
-  }
+  static const int m = [] {
+    const char *e = getenv("HGX_ALG_M");
+    return e ? atoi(e) : 2;
+  }();
+  return m >= 4 ? narrow_for_gm<KS, MODE, 4>(g)
+                : m == 1 ? narrow_for_gm<KS, MODE, 1>(g)
+                         : narrow_for_gm<KS, MODE, 2>(g);
 }
 
 template <int MODE>
@@ -444,20 +701,31 @@ HalfFn narrow_fn(int ks, int g) {
 int launch_half(hgx_ctx *ctx, int mode, int row0, int R, const int *rp,
                 const int *col, const float *self_in, const float *src,
                 float *out, const int *mm_prev, int src_affine, int *mm_cur,
-                double avg) {
+                double avg, const int *blk, int nblk) {
   const int k = ctx->k, KS = ctx->ks;
   if (R <= 0) return HGX_OK;
-  if (KS <= 20) {
+  static const bool flat_env = [] {
+    const char *e = getenv("HGX_ALG_FLAT");
+    return e && e[0] == '1';
+  }();
+  if (KS <= 20 && flat_env) {
+    FlatFn fn = mode == MODE_FULL ? flat_fn<MODE_FULL>(KS) : flat_fn<MODE_PARTIAL>(KS);
+    hipLaunchKernelGGL(fn, dim3(grid_for(nblk, kBlock / 64, resident_grid(fn))),
+                       dim3(kBlock), 0, ctx->stream, nblk, blk, rp, col,
+                       self_in, src, out, mm_prev, src_affine, mm_cur, k);
+  } else if (KS <= 20) {
     const int g = pick_g(avg);
     HalfFn fn = mode == MODE_FULL ? narrow_fn<MODE_FULL>(KS, g)
                                   : narrow_fn<MODE_PARTIAL>(KS, g);
-    hipLaunchKernelGGL(fn, dim3(grid_for(R, kBlock / g)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(fn, dim3(grid_for(R, kBlock / g, resident_grid(fn))),
+                       dim3(kBlock), 0,
                        ctx->stream, row0, R, rp, col, self_in, src, out,
                        mm_prev, src_affine, mm_cur, k);
   } else {
     auto fn = mode == MODE_FULL ? algdist_half_wide<MODE_FULL>
                                 : algdist_half_wide<MODE_PARTIAL>;
-    hipLaunchKernelGGL(fn, dim3(grid_for(R, kBlock / 64)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(fn, dim3(grid_for(R, kBlock / 64, resident_grid(fn))),
+                       dim3(kBlock), 0,
                        ctx->stream, row0, R, KS, rp, col, self_in, src, out,
                        mm_prev, src_affine, mm_cur, k);
   }
@@ -515,7 +783,14 @@ extern "C" int hgx_alg_set(hgx_ctx *ctx, int k, const float *node_xy,
   HGX_CHECK(ctx, node_xy && edge_xy, HGX_EINVAL, "null coordinate buffer");
   HGX_HIP(ctx, hipSetDevice(ctx->device));
   HGX_TRY(check_nonempty(ctx));
-  const int KS = ((k + 1) + 3) / 4 * 4;
+  int KS = ((k + 1) + 3) / 4 * 4;
+  {
+    // rows of 12 floats straddle 64-byte sectors; HGX_ALG_KS forces a wider
+    // row stride (diagnostic / tuning)
+    const char *e = getenv("HGX_ALG_KS");
+    const int want = e ? atoi(e) : 0;
+    if (want > KS && want % 4 == 0 && want <= 20) KS = want;
+  }
   ctx->k = k;
   ctx->ks = KS;
   for (int b = 0; b < 2; b++) {
@@ -550,8 +825,13 @@ extern "C" int hgx_alg_run(hgx_ctx *ctx, int iters) {
   HGX_CHECK(ctx, iters >= 0, HGX_EINVAL, "iterations must be >= 0");
   HGX_HIP(ctx, hipSetDevice(ctx->device));
   if (iters == 0) return HGX_OK;
+  {
+    const char *ab = getenv("HGX_ALG_ABLATE");
+    int v = ab ? atoi(ab) : 0;
+    HGX_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_ablate), &v, sizeof(int)));
+  }
   const int KS = ctx->ks;
-  const size_t slot = 2 * (size_t)KS;
+  const size_t slot = 2 * (size_t)KS * kRep;
   HGX_TRY(hgx_ensure(ctx, ctx->mm, sizeof(int) * slot * iters));
   int *mm = ctx->mm.as<int>();
   HGX_TRY(init_mm(ctx, mm, (int64_t)slot * iters));
@@ -564,11 +844,11 @@ extern "C" int hgx_alg_run(hgx_ctx *ctx, int iters) {
     // node half: self x (scaled), gathered y (scaled)
     HGX_TRY(launch_half(ctx, MODE_FULL, 0, ctx->N, ctx->rp_n.as<int>(),
                         ctx->col_n.as<int>(), xc, yc, xn, prev, prev != nullptr,
-                        cur, ctx->avg_deg_n));
+                        cur, ctx->avg_deg_n, ctx->blk_n.as<int>(), ctx->nblk_n));
     // edge half: self y (scaled), gathered NEW x (raw)
     HGX_TRY(launch_half(ctx, MODE_FULL, 0, ctx->E, ctx->rp_e.as<int>(),
                         ctx->col_e.as<int>(), yc, xn, yn, prev, 0, cur,
-                        ctx->avg_deg_e));
+                        ctx->avg_deg_e, ctx->blk_e.as<int>(), ctx->nblk_e));
     ctx->xcur ^= 1;
     ctx->ycur ^= 1;
   }
@@ -666,12 +946,21 @@ extern "C" int hgx_alg_shard_begin(hgx_ctx *ctx, int32_t row0, int32_t row1,
   if (!cl.empty())
     HGX_HIP(ctx, hipMemcpy(ctx->col_el.p, cl.data(), sizeof(int) * cl.size(),
                            hipMemcpyHostToDevice));
+  {
+    std::vector<int> rpn(ctx->N + 1);
+    HGX_HIP(ctx, hipMemcpy(rpn.data(), ctx->rp_n.p, sizeof(int) * (ctx->N + 1),
+                           hipMemcpyDeviceToHost));
+    HGX_TRY(hgx_make_row_blocks(ctx, rpn.data(), row0, row1, ctx->blk_sn,
+                                ctx->nblk_sn));
+    HGX_TRY(hgx_make_row_blocks(ctx, rpl.data(), 0, ctx->E, ctx->blk_el,
+                                ctx->nblk_el));
+  }
   ctx->row0 = row0;
   ctx->row1 = row1;
   ctx->ext_partial = (float *)d_partial;
   ctx->ext_mm = (int *)d_mm;
   ctx->ext_iters = iters;
-  HGX_TRY(init_mm(ctx, ctx->ext_mm, (int64_t)2 * ctx->ks * iters));
+  HGX_TRY(init_mm(ctx, ctx->ext_mm, (int64_t)2 * ctx->ks * kRep * iters));
   if (ks_out) *ks_out = ctx->ks;
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return HGX_OK;
@@ -681,14 +970,15 @@ extern "C" int hgx_alg_shard_node(hgx_ctx *ctx, int it) {
   if (!ctx) return HGX_EINVAL;
   HGX_CHECK(ctx, ctx->ext_mm && it >= 0 && it < ctx->ext_iters, HGX_ESTATE,
             "shard iteration %d out of order", it);
-  const size_t slot = 2 * (size_t)ctx->ks;
+  const size_t slot = 2 * (size_t)ctx->ks * kRep;
   const int *prev = it ? ctx->ext_mm + slot * (it - 1) : nullptr;
   int *cur = ctx->ext_mm + slot * it;
   float *xc = ctx->X[ctx->xcur].as<float>(), *xn = ctx->X[ctx->xcur ^ 1].as<float>();
   float *yc = ctx->Y[ctx->ycur].as<float>();
   HGX_TRY(launch_half(ctx, MODE_FULL, ctx->row0, ctx->row1 - ctx->row0,
                       ctx->rp_n.as<int>(), ctx->col_n.as<int>(), xc, yc, xn,
-                      prev, prev != nullptr, cur, ctx->avg_deg_n));
+                      prev, prev != nullptr, cur, ctx->avg_deg_n,
+                      ctx->blk_sn.as<int>(), ctx->nblk_sn));
   return HGX_OK;
 }
 
@@ -700,7 +990,8 @@ extern "C" int hgx_alg_shard_edge_partial(hgx_ctx *ctx, int it) {
   const double avg = (double)std::max<int64_t>(1, ctx->nnz) / ctx->E;
   HGX_TRY(launch_half(ctx, MODE_PARTIAL, 0, ctx->E, ctx->rp_el.as<int>(),
                       ctx->col_el.as<int>(), nullptr, xn, ctx->ext_partial,
-                      nullptr, 0, nullptr, avg));
+                      nullptr, 0, nullptr, avg, ctx->blk_el.as<int>(),
+                      ctx->nblk_el));
   return HGX_OK;
 }
 
@@ -708,7 +999,7 @@ extern "C" int hgx_alg_shard_edge_final(hgx_ctx *ctx, int it) {
   if (!ctx) return HGX_EINVAL;
   HGX_CHECK(ctx, ctx->ext_mm && it >= 0 && it < ctx->ext_iters, HGX_ESTATE,
             "shard iteration %d out of order", it);
-  const size_t slot = 2 * (size_t)ctx->ks;
+  const size_t slot = 2 * (size_t)ctx->ks * kRep;
   const int *prev = it ? ctx->ext_mm + slot * (it - 1) : nullptr;
   int *cur = ctx->ext_mm + slot * it;
   float *yc = ctx->Y[ctx->ycur].as<float>(), *yn = ctx->Y[ctx->ycur ^ 1].as<float>();
@@ -725,7 +1016,7 @@ extern "C" int hgx_alg_shard_edge_final(hgx_ctx *ctx, int it) {
 extern "C" int hgx_alg_shard_end(hgx_ctx *ctx) {
   if (!ctx) return HGX_EINVAL;
   HGX_CHECK(ctx, ctx->ext_mm, HGX_ESTATE, "hgx_alg_shard_begin not called");
-  const size_t slot = 2 * (size_t)ctx->ks;
+  const size_t slot = 2 * (size_t)ctx->ks * kRep;
   HGX_TRY(final_affine(ctx, ctx->row0, ctx->row1 - ctx->row0,
                        ctx->ext_mm + slot * (ctx->ext_iters - 1)));
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -74,7 +74,8 @@ extern "C" int hgx_destroy(hgx_ctx *ctx) {
   hipStreamSynchronize(ctx->stream);
   DevBuf *bufs[] = {&ctx->rp_n, &ctx->col_n, &ctx->rp_e, &ctx->col_e,
                     &ctx->X[0], &ctx->X[1], &ctx->Y[0], &ctx->Y[1], &ctx->mm,
-                    &ctx->rp_el, &ctx->col_el,
+                    &ctx->rp_el, &ctx->col_el, &ctx->blk_n, &ctx->blk_e,
+                    &ctx->blk_sn, &ctx->blk_el,
                     &ctx->rec_idx, &ctx->rec_tgt, &ctx->ntab, &ctx->etab,
                     &ctx->nacc, &ctx->eacc, &ctx->s0, &ctx->s1, &ctx->s2,
                     &ctx->s3, &ctx->s4, &ctx->s5, &ctx->s6, &ctx->s7};
@@ -149,6 +150,8 @@ extern "C" int hgx_upload_incidence(hgx_ctx *ctx, int32_t N, int32_t E,
     HGX_HIP(ctx, hipMemcpyAsync(ctx->col_e.p, col_e, sizeof(int32_t) * nnz,
                                 hipMemcpyHostToDevice, ctx->stream));
   }
+  HGX_TRY(hgx_make_row_blocks(ctx, rowptr_n, 0, N, ctx->blk_n, ctx->nblk_n));
+  HGX_TRY(hgx_make_row_blocks(ctx, rowptr_e, 0, E, ctx->blk_e, ctx->nblk_e));
   int32_t mn = 0, me = 0;
   for (int32_t r = 0; r < N; r++) mn = std::max(mn, rowptr_n[r + 1] - rowptr_n[r]);
   for (int32_t r = 0; r < E; r++) me = std::max(me, rowptr_e[r + 1] - rowptr_e[r]);
@@ -162,5 +165,32 @@ extern "C" int hgx_upload_incidence(hgx_ctx *ctx, int32_t N, int32_t E,
   ctx->k = 0;  // alg coords belong to the previous incidence
   ctx->n_rec = 0;
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HGX_OK;
+}
+
+int hgx_make_row_blocks(hgx_ctx *ctx, const int32_t *rp, int32_t r0, int32_t r1,
+                        DevBuf &blk, int &nblk) {
+  constexpr int kRows = 64, kNnz = 256;  // must match hgx_algdist.hip
+  std::vector<int32_t> b;
+  b.reserve((size_t)(r1 - r0) / 8 + 2);
+  b.push_back(r0);
+  int rows = 0;
+  int64_t nz = 0;
+  for (int32_t r = r0; r < r1; r++) {
+    const int64_t len = rp[r + 1] - rp[r];
+    if (rows > 0 && (rows + 1 > kRows || nz + len > kNnz)) {
+      b.push_back(r);
+      rows = 0;
+      nz = 0;
+    }
+    rows++;
+    nz += len;
+  }
+  if (r1 > r0) b.push_back(r1);
+  nblk = (int)b.size() - 1;
+  if (nblk < 0) nblk = 0;
+  HGX_TRY(hgx_ensure(ctx, blk, sizeof(int32_t) * b.size()));
+  HGX_HIP(ctx, hipMemcpy(blk.p, b.data(), sizeof(int32_t) * b.size(),
+                         hipMemcpyHostToDevice));
   return HGX_OK;
 }

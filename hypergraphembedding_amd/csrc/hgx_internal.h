@@ -27,6 +27,10 @@ struct hgx_ctx {
   int32_t N = 0, E = 0;
   int64_t nnz = 0;
   DevBuf rp_n, col_n, rp_e, col_e;
+  // alg-dist row-blocks (<= 64 whole rows, <= 256 incidences each; a longer
+  // row is a block of its own): row starts, nblk + 1 entries
+  DevBuf blk_n, blk_e;
+  int nblk_n = 0, nblk_e = 0;
   double avg_deg_n = 0, avg_deg_e = 0;
   int32_t max_deg_n = 0, max_deg_e = 0;
 
@@ -38,7 +42,8 @@ struct hgx_ctx {
   // sharded (node-row) mode: own node rows [row0,row1), local edge sub-CSR
   // of those rows, caller-owned exchange buffers (reduced by the caller).
   int32_t row0 = 0, row1 = 0;
-  DevBuf rp_el, col_el;
+  DevBuf rp_el, col_el, blk_sn, blk_el;
+  int nblk_sn = 0, nblk_el = 0;
   float *ext_partial = nullptr;  // E x ks
   int *ext_mm = nullptr;         // iters x 2 x ks
   int ext_iters = 0;
@@ -62,6 +67,9 @@ struct hgx_ctx {
 };
 
 int hgx_fail(hgx_ctx *ctx, int code, const char *fmt, ...);
+// alg-dist row-block partition of rows [r0, r1) of a CSR (host side)
+int hgx_make_row_blocks(hgx_ctx *ctx, const int32_t *rp, int32_t r0, int32_t r1,
+                        DevBuf &blk, int &nblk);
 int hgx_ensure(hgx_ctx *ctx, DevBuf &b, size_t bytes);
 void hgx_release(DevBuf &b);
 
@@ -119,6 +127,28 @@ __host__ __device__ __forceinline__ uint64_t rand64(uint64_t seed,
 // uniform integer in [0, n) (multiply-high on 64 random bits: bias < n/2^64)
 __device__ __forceinline__ uint32_t bounded(uint64_t r, uint32_t n) {
   return (uint32_t)__umul64hi(r, (uint64_t)n);
+}
+
+// Sum over aligned groups of G lanes (G a power of two <= 64); every lane of
+// the group gets the sum. Steps inside a 16-lane DPP row are single VALU ops
+// (quad_perm xor1 / xor2, row_half_mirror, row_mirror pair lanes whose
+// partial sums are disjoint); only the 16- and 32-lane steps go through
+// ds_bpermute.
+template <int ctrl>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), ctrl,
+                                         0xF, 0xF, false));
+}
+template <int G>
+__device__ __forceinline__ float group_allreduce_sum(float x) {
+  if (G >= 2) x += dpp_f<0xB1>(x);   // quad_perm [1,0,3,2]
+  if (G >= 4) x += dpp_f<0x4E>(x);   // quad_perm [2,3,0,1]
+  if (G >= 8) x += dpp_f<0x141>(x);  // row_half_mirror
+  if (G >= 16) x += dpp_f<0x140>(x); // row_mirror
+  if (G >= 32) x += __shfl_xor(x, 16);
+  if (G >= 64) x += __shfl_xor(x, 32);
+  return x;
 }
 
 }  // namespace hgx

@@ -99,9 +99,7 @@ __device__ __forceinline__ float dot4(float4 a, float4 b) {
 
 template <int L>
 __device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int off = L / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
+  return hgx::group_allreduce_sum<L>(v);
 }
 
 template <int L, int VPL>

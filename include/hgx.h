@@ -80,12 +80,13 @@ int hgx_alg_last_stats(hgx_ctx *ctx, double *ms, double *bytes);
  * [row0,row1); every rank holds all edge coords. The CALLER owns the two
  * exchange buffers (device memory, e.g. torch tensors) and runs the
  * collectives (torch.distributed "nccl" = RCCL over xGMI) between calls:
- *   begin(row0,row1, partial[E*KS] f32, mm[iters*2*KS] i32, iters, &KS)
+ *   begin(row0,row1, partial[E*KS] f32, mm[iters*M] i32, iters, &KS)
  *   for it: node(it); edge_partial(it); all_reduce(partial, SUM);
- *           edge_final(it); all_reduce(mm[it*2*KS : (it+1)*2*KS], MAX)
+ *           edge_final(it); all_reduce(mm[it*M : (it+1)*M], MAX)
  *   end()   -> own node rows + all edge rows rescaled on device
- * min/max words are order-preserving int32 (max slot f(x), min slot ~f(x)),
- * so MAX is the only reduction needed. */
+ * with M = 2 * KS * HGX_MM_REPLICAS. min/max words are order-preserving
+ * int32 (max slot f(x), min slot ~f(x)), so MAX is the only reduction. */
+#define HGX_MM_REPLICAS 64
 int hgx_alg_shard_begin(hgx_ctx *ctx, int32_t row0, int32_t row1,
                         void *d_partial, void *d_mm, int iters, int *ks_out);
 int hgx_alg_shard_node(hgx_ctx *ctx, int it);
