@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""Benchmark: HOBE (HG2V_ALG_DIST) dim=128 on the synthetic random 100k/50k
+hypergraph (BASELINE.json configs[2]).
+
+One step = one training epoch (forward + backward + Keras Adagrad over every
+HOBE record, batch 256, fresh device shuffle) with the records, tables and
+incidence already resident in HBM. Reported beside it, from the same run:
+the algebraic-distance relaxation (k=10, 20 iterations) in algorithmic GB/s,
+HOBE sampling time, the roofline object of the dominant kernel (the per-batch
+train_fwd_bwd + train_update pair) and the CPU baseline (the oracle's
+single-threaded trainer, oracle/hgref.c, on a bounded slice of the same
+records).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Multi-GPU: alg-dist is node-row sharded with RCCL all-reduces
+(algebraic_distance.alg_dist_sharded); training runs as independent replicas
+(synchronous batch-256 Adagrad does not partition), so `value`
+is weak-scaled: total records trained by all ranks / max wall time.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = ("training samples/sec + alg-dist SpMV GB/s, HOBE dim=128 at "
+          "1/2/4/8 MI355X")
+
+
+def parse():
+  p = argparse.ArgumentParser()
+  p.add_argument("--gpus", type=int, default=1)
+  p.add_argument("--steps", type=int, default=3)
+  p.add_argument("--warmup", type=int, default=1)
+  p.add_argument("--dim", type=int, default=128)
+  p.add_argument("--num-samples", type=int, default=200)
+  p.add_argument("--num-neighbors", type=int, default=5)
+  p.add_argument("--batch", type=int, default=256)
+  p.add_argument("--alg-iters", type=int, default=20)
+  p.add_argument("--cpu-records", type=int, default=2_000_000,
+                 help="records of the bounded CPU-baseline slice")
+  p.add_argument("--no-cpu", action="store_true")
+  return p.parse_args()
+
+
+def main():
+  args = parse()
+  world = int(os.environ.get("WORLD_SIZE", "1"))
+  rank = int(os.environ.get("RANK", "0"))
+  local = int(os.environ.get("LOCAL_RANK", "0"))
+  dist = None
+  if world > 1:
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+  def barrier():
+    if dist is not None:
+      dist.barrier()
+
+  def sync():
+    # all device work of this process runs on the context's stream
+    if dist is not None:
+      import torch
+      torch.cuda.synchronize()
+    if ctx is not None:
+      ctx.synchronize()
+
+  ctx = None
+
+  from hypergraphembedding_amd import _hgx
+  from hypergraphembedding_amd.synthetic import random_hypergraph
+  from hypergraphembedding_amd.algebraic_distance import alg_dist_sharded
+
+  t = time.time()
+  inc = random_hypergraph(seed=0)
+  gen_s = time.time() - t
+  ctx = _hgx.Context(local)
+  ctx.upload(inc)
+  k = 10
+  rs = np.random.RandomState(0)
+  x0 = rs.random_sample((inc.N, k))
+  y0 = rs.random_sample((inc.E, k))
+  bytes_iter = 8.0 * inc.nnz + (8.0 + 12.0 * k) * (inc.N + inc.E)
+
+  # ---- algebraic distance (SpMV relaxation) ----
+  if world > 1:
+    alg_dist_sharded(ctx, inc, x0, y0, args.alg_iters)  # warm
+    runs = [alg_dist_sharded(ctx, inc, x0, y0, args.alg_iters)[2]
+            for _ in range(3)]
+    alg_ms = float(np.median(runs))
+    import torch
+    tt = torch.tensor([alg_ms], device="cuda")
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    alg_ms = float(tt.item())
+  else:
+    ctx.alg_set(x0, y0)
+    ctx.alg_run(args.alg_iters)  # warm
+    runs = []
+    for _ in range(3):
+      ctx.alg_set(x0, y0)
+      ctx.alg_run(args.alg_iters)
+      runs.append(ctx.alg_stats()[0])
+    alg_ms = float(np.median(runs))
+  alg_gbps = bytes_iter * args.alg_iters / (alg_ms * 1e-3) / 1e9
+
+  # ---- HOBE records (alg coords resident on the device) ----
+  ctx.upload(inc)
+  ctx.alg_set(x0, y0)
+  ctx.alg_run(args.alg_iters)
+  t = time.time()
+  n = ctx.sample_hobe(1000 + rank, args.num_neighbors, args.num_samples)
+  sample_s = time.time() - t
+
+  # ---- training ----
+  ctx.model_init(args.dim, inc.N + 1, inc.E + 1, seed=7 + rank)
+  for w in range(args.warmup):
+    ctx.train(batch=args.batch, max_epochs=1, loss=_hgx.LOSS_MSE,
+              act=_hgx.ACT_RELU, min_delta=-1e30, shuffle_seed=100 + w)
+  barrier()
+  sync()
+  t0 = time.perf_counter()
+  dev_ms = 0.0
+  batches = 0
+  for s in range(args.steps):
+    ctx.train(batch=args.batch, max_epochs=1, loss=_hgx.LOSS_MSE,
+              act=_hgx.ACT_RELU, min_delta=-1e30, shuffle_seed=200 + s)
+    ms, rec, bat = ctx.train_stats()
+    dev_ms += ms
+    batches += bat
+  barrier()
+  sync()
+  elapsed = time.perf_counter() - t0
+  if dist is not None:
+    import torch
+    tt = torch.tensor([elapsed], device="cuda")
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    elapsed = float(tt.item())
+  records = n * args.steps * world
+  value = records / elapsed
+
+  # ---- roofline of the dominant kernel: one batch step (K1 + K2) ----
+  b_rec = 224.0 * args.dim + 68.0  # SURVEY §8d algorithmic bytes / record
+  per_batch_ms = dev_ms / max(batches, 1)
+  batch_bytes = b_rec * (n * args.steps / max(batches, 1))
+  achieved = batch_bytes / (per_batch_ms * 1e-3) / 1e9
+  traffic = None
+  pmc = os.path.join(ROOT, "profiles", "r01_pmc_train.json")
+  if os.path.exists(pmc):
+    with open(pmc) as f:
+      traffic = json.load(f).get("hbm_bytes_per_batch")
+  roofline = {"bound": "hbm", "achieved": round(achieved, 1),
+              "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+              "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+              "kernel": "train_fwd_bwd+train_update (one batch step)",
+              "per_launch_us": round(per_batch_ms * 1e3, 2),
+              "algorithmic_bytes_per_launch": round(batch_bytes)}
+
+  # ---- CPU baseline: oracle trainer on a bounded slice (rank 0, N=1) ----
+  cpu = None
+  if rank == 0 and world == 1 and not args.no_cpu:
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    idx, tgt = ctx.records_get()
+    m = min(args.cpu_records, idx.shape[0])
+    sel = np.random.RandomState(0).permutation(idx.shape[0])[:m]
+    cidx, ctgt = np.ascontiguousarray(idx[sel]), np.ascontiguousarray(tgt[sel])
+    del idx, tgt
+    init = np.random.RandomState(1)
+    nt = init.uniform(-0.05, 0.05, (inc.N + 1, args.dim)).astype(np.float32)
+    et = init.uniform(-0.05, 0.05, (inc.E + 1, args.dim)).astype(np.float32)
+    t = time.perf_counter()
+    O.train(cidx, ctgt, args.num_neighbors, nt, et, O.LOSS_MSE, O.ACT_RELU,
+            batch=args.batch, max_epochs=1, min_delta=-1e30)
+    cpu_s = time.perf_counter() - t
+    cpu = {"value": round(m / cpu_s, 1), "unit": "records/s", "cores": 1,
+           "kind": "port",
+           "sample": f"{m} HOBE records (random slice of this run's stream), "
+                     f"1 epoch, d={args.dim}, batch {args.batch}, "
+                     f"oracle/hgref.c hgref_train single-threaded, "
+                     f"{cpu_s:.1f} s"}
+
+  if rank == 0:
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "records/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: random hypergraph 100k nodes / 50k edges, node "
+                "degree 1+Poisson(19), seed 0; HOBE records sampled on device",
+        "config": {
+            "workload": "C3 HG2V_ALG_DIST (HOBE) dim=128, random 100k/50k, "
+                        "1 step = 1 training epoch",
+            "nodes": inc.N, "edges": inc.E, "nnz": inc.nnz,
+            "records_per_epoch": n, "batch": args.batch, "dim": args.dim,
+            "num_neighbors": args.num_neighbors,
+            "num_samples": args.num_samples,
+            "parallelism": ("replicas (training), node-row sharded + RCCL "
+                            "all-reduce (alg-dist)" if world > 1 else
+                            "single GPU"),
+        },
+        "algdist": {"k": k, "iters": args.alg_iters,
+                    "ms_per_iter": round(alg_ms / args.alg_iters, 4),
+                    "gbps": round(alg_gbps, 1),
+                    "bytes_per_iter": bytes_iter,
+                    "frac_of_hbm_peak": round(alg_gbps / HBM_PEAK_GBPS, 4),
+                    "sharded": world > 1},
+        "hobe_sampling_s": round(sample_s, 3),
+        "graph_gen_s": round(gen_s, 2),
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+  if dist is not None:
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+  main()

@@ -1,0 +1,46 @@
+"""MI355X-native FOBE / HOBE hypergraph embedding.
+
+Drop-in for the FOBE (HG2V_BOOLEAN) / HOBE (HG2V_ALG_DIST) hot path of
+JSybrandt/HypergraphEmbedding: same registry keys, signatures and
+``hypergraph.proto`` messages as the reference package ``__init__``
+(hypergraph_embedding/__init__.py:8-42), with the work done by hand-written
+gfx950 HIP kernels behind the C ABI of libhgx.so (include/hgx.h).
+
+Importing the package does not touch the GPU; the first embedding call
+creates the device context and raises if libhgx.so or a device is missing.
+"""
+
+from .proto import (EvaluationMetrics, ExperimentalResult, Hypergraph,
+                    HypergraphEmbedding)
+from .hypergraph_util import (AddNodeToEdge, CompressRange,
+                              CreateRandomHyperGraph, FromSparseMatrix,
+                              Incidence, IsEmpty, Relabel, RemoveEdge,
+                              RemoveNode, RemoveNodeFromEdge, ToCscMatrix,
+                              ToCsrMatrix, ToEdgeCsrMatrix)
+from .algebraic_distance import EmbedAlgebraicDistance
+from .hg2v_sample import (AlgebraicDistanceSamples, BooleanSamples,
+                          SamplesToModelInput, SimilarityRecord)
+from .hg2v_weighting import UniformWeight, WeightByNeighborhood
+from .hg2v_model import (BooleanModel, KerasModelToEmbedding,
+                         UnweightedFloatModel)
+from .embedding import (COMBINATION_OPTIONS, DEBUG_SUMMARY_OPTIONS,
+                        EMBEDDING_OPTIONS, CombineEmbeddings, Embed,
+                        EmbedHg2vAlgDist, EmbedHg2vBoolean)
+
+__all__ = [
+    # proto
+    "Hypergraph", "HypergraphEmbedding", "EvaluationMetrics",
+    "ExperimentalResult",
+    # embedding
+    "Embed", "EMBEDDING_OPTIONS", "DEBUG_SUMMARY_OPTIONS",
+    "COMBINATION_OPTIONS", "CombineEmbeddings", "EmbedHg2vBoolean",
+    "EmbedHg2vAlgDist", "EmbedAlgebraicDistance",
+    # hot-path pieces
+    "BooleanSamples", "AlgebraicDistanceSamples", "SamplesToModelInput",
+    "SimilarityRecord", "UniformWeight", "WeightByNeighborhood",
+    "BooleanModel", "UnweightedFloatModel", "KerasModelToEmbedding",
+    # hypergraph util
+    "AddNodeToEdge", "RemoveNodeFromEdge", "RemoveNode", "RemoveEdge",
+    "CreateRandomHyperGraph", "FromSparseMatrix", "IsEmpty", "ToCsrMatrix",
+    "ToEdgeCsrMatrix", "ToCscMatrix", "Relabel", "CompressRange", "Incidence",
+]

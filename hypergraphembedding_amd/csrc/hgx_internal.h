@@ -59,7 +59,7 @@ struct hgx_ctx {
   int d = 0, dp = 0;
   int64_t node_rows = 0, edge_rows = 0;
   DevBuf ntab, etab, nacc, eacc;
-  double train_ms = 0;
+  double train_ms = 0, train_epoch_ms = 0;
   int64_t train_records = 0, train_batches = 0;
 
   // ---- scratch ----

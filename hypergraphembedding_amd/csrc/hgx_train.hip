@@ -856,6 +856,17 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   }
 
   std::vector<int> hperm;
+  // device time of the per-batch kernels only (K1+K2 replays), per chunk
+  std::vector<hipEvent_t> bev;
+  double batch_ms = 0.0;
+  auto flush_events = [&]() {
+    for (size_t i = 0; i + 1 < bev.size(); i += 2) {
+      float m = 0.f;
+      if (hipEventElapsedTime(&m, bev[i], bev[i + 1]) == hipSuccess) batch_ms += m;
+    }
+    for (hipEvent_t e : bev) hipEventDestroy(e);
+    bev.clear();
+  };
   double best = INFINITY;
   int ep = 0;
   int rc = HGX_OK;
@@ -898,6 +909,12 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
       hipLaunchKernelGGL(train_prep, dim3(nbc), dim3(kTB),
                          (size_t)P * sizeof(unsigned long long), ctx->stream, a,
                          base, nbc, P);
+      hipEvent_t e0, e1;
+      hipEventCreate(&e0);
+      hipEventCreate(&e1);
+      bev.push_back(e0);
+      bev.push_back(e1);
+      hipEventRecord(e0, ctx->stream);
       if (use_graph) {
         for (int g = 0; g < nbc; g += GB) {
           if (hipGraphLaunch(gexec, ctx->stream) != hipSuccess) {
@@ -911,6 +928,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
           hipLaunchKernelGGL(k2, dim3(grid2), dim3(kTB), 0, ctx->stream, a);
         }
       }
+      hipEventRecord(e1, ctx->stream);
       if (rc) break;
       hipLaunchKernelGGL(loss_partial, dim3(kLossBlocks), dim3(kTB), 0,
                          ctx->stream, a.lossbuf, (int64_t)nbc * nblk1, dpart);
@@ -926,6 +944,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
                     hipGetErrorString(hipGetLastError()));
       break;
     }
+    flush_events();
     const double cur = lsum / (double)n;
     if (epoch_loss) epoch_loss[ep] = (float)cur;
     if (cur < best - (double)min_delta) {
@@ -937,13 +956,15 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   }
   hipEventRecord(ctx->ev1, ctx->stream);
   hipEventSynchronize(ctx->ev1);
+  flush_events();
   float ms = 0.f;
   hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
   if (gexec) hipGraphExecDestroy(gexec);
   if (graph) hipGraphDestroy(graph);
   if (rc) return rc;
   HGX_LAUNCH_CHECK(ctx);
-  ctx->train_ms = ms;
+  ctx->train_ms = batch_ms;
+  ctx->train_epoch_ms = ms;
   ctx->train_records = (int64_t)ep * n;
   ctx->train_batches = (int64_t)ep * nbatches;
   if (epochs_run) *epochs_run = ep;

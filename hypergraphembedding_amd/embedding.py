@@ -1,0 +1,212 @@
+"""Embedding entry points (reference: hypergraph_embedding/embedding.py).
+
+Registry and signatures kept for the FOBE/HOBE path: ``Embed(args, hg)``
+(81-107), ``EMBEDDING_OPTIONS`` (423-444) with "ALG_DIST",
+"HG2V_BOOLEAN", "HG2V_ALG_DIST", "HG2V_BOOLEAN_NS", ``EmbedHg2vBoolean``
+(308-329), ``EmbedHg2vAlgDist`` (389-416), ``CombineEmbeddings`` (51-78).
+
+``_hypergraph2vec_skeleton`` (269-305) runs entirely on one device context:
+incidence upload -> sampler -> records stay in HBM -> tables initialised on
+device -> Keras-semantics fit -> rows idx+1 copied into the proto.
+The reference's other methods (SVD, NMF, node2vec, auto-encoder, Jaccard
+samplers) are outside this hot path: their keys raise like the reference's
+``method_not_supported`` (419-420).
+"""
+
+import logging
+
+import numpy as np
+
+from . import _hgx
+from .algebraic_distance import EmbedAlgebraicDistance, coords_to_embedding
+from .hg2v_model import Hg2vModel
+from .hg2v_sample import sample_fobe, sample_hobe
+from .hypergraph_util import Incidence
+from .proto import HypergraphEmbedding
+from .runtime import get_context
+
+log = logging.getLogger()
+
+COMBINATION_OPTIONS = [
+    "N_E_SUPERVISED",  # default @ 0 (reference); Keras MLP combiner, not here
+    "N_E_SEMI_SUPERVISED",
+    "CONCATENATE",
+]
+
+
+def CombineEmbeddingsViaConcatenation(hypergraph, embeddings):
+  """combine_embeddings_util.py:27-41."""
+  emb = HypergraphEmbedding()
+  emb.dim = sum(e.dim for e in embeddings)
+  for node_idx in hypergraph.node:
+    vec = []
+    for e in embeddings:
+      vec.extend(e.node[node_idx].values)
+    emb.node[node_idx].values.extend(np.asarray(vec, np.float32).tolist())
+  for edge_idx in hypergraph.edge:
+    vec = []
+    for e in embeddings:
+      vec.extend(e.edge[edge_idx].values)
+    emb.edge[edge_idx].values.extend(np.asarray(vec, np.float32).tolist())
+  return emb
+
+
+def CombineEmbeddings(args, hypergraph, embeddings, disable_pbar=False):
+  """embedding.py:51-78. CONCATENATE is supported; the Keras MLP combiners
+  (N_E_SUPERVISED / N_E_SEMI_SUPERVISED) are the next component (SURVEY
+  §8f) and raise NotImplementedError here."""
+  del disable_pbar
+  assert len(embeddings) >= 1
+  if len(embeddings) == 1:
+    return embeddings[0]
+  strategy = args.embedding_combination_strategy
+  if strategy == "CONCATENATE":
+    comb = CombineEmbeddingsViaConcatenation(hypergraph, embeddings)
+    args.embedding_dimension = comb.dim
+  elif strategy in ("N_E_SUPERVISED", "N_E_SEMI_SUPERVISED"):
+    raise NotImplementedError(
+        f"combination strategy {strategy} (Keras MLP combiner) is outside "
+        "the FOBE/HOBE hot path; use CONCATENATE")
+  else:
+    raise ValueError("Args contains an illegal embedding-combination-strategy")
+  comb.method_name = "_".join(args.embedding_method)
+  return comb
+
+
+def Embed(args, hypergraph, shortcut_embeddings=None):
+  """embedding.py:81-107."""
+  assert min(len(hypergraph.node), len(hypergraph.edge)) > \
+      args.embedding_dimension
+  assert len(args.embedding_method) >= 1
+  embeddings = []
+  for method in args.embedding_method:
+    if shortcut_embeddings is not None and method in shortcut_embeddings:
+      embeddings.append(shortcut_embeddings[method])
+      continue
+    log.info("Embedding using method %s with %i dim", method,
+             args.embedding_dimension)
+    if getattr(args, "embedding_debug_summary", None):
+      embeddings.append(EMBEDDING_OPTIONS[method](
+          hypergraph, args.embedding_dimension,
+          debug_summary_path=args.embedding_debug_summary))
+    else:
+      embeddings.append(EMBEDDING_OPTIONS[method](hypergraph,
+                                                  args.embedding_dimension))
+  embedding = CombineEmbeddings(args, hypergraph, embeddings)
+  log.info("Embedding contains %i node and %i edge vectors",
+           len(embedding.node), len(embedding.edge))
+  return embedding
+
+
+def _plot_distributions(path, records):
+  """PlotDistributions (hg2v_sample.py:805-853): histograms of the three
+  target kinds of the record stream."""
+  import matplotlib
+  matplotlib.use("Agg")
+  import matplotlib.pyplot as plt
+  idx, tgt = records.arrays()
+  nn = (idx[:, 0] > 0) & (idx[:, 2] > 0)
+  ee = (idx[:, 1] > 0) & (idx[:, 3] > 0)
+  ne = ~(nn | ee)
+  fig, axes = plt.subplots(3, 1, figsize=(8.5, 11))
+  for ax, sel, col, title in ((axes[0], nn, 0, "Node-Node"),
+                              (axes[1], ee, 1, "Edge-Edge"),
+                              (axes[2], ne, 2, "Node-Edge")):
+    ax.set_title(f"{title} Probability Distribution")
+    ax.hist(tgt[sel, col])
+    ax.set_yscale("log")
+  fig.tight_layout()
+  fig.savefig(str(path))
+
+
+def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
+                             loss, act, fit_batch_size, fit_epochs,
+                             debug_summary_path, disable_pbar, ctx=None):
+  """embedding.py:269-305, device-resident end to end."""
+  del disable_pbar
+  ctx = ctx or get_context()
+  inc = Incidence.from_hypergraph(hypergraph)  # CompressRange + CSR
+  records = sampler_fn(inc, ctx)
+  if debug_summary_path is not None:
+    _plot_distributions(debug_summary_path, records)
+  model = Hg2vModel(inc.N + 1, inc.E + 1, dimension, num_neighbors, loss, act,
+                    ctx=ctx)  # rows = max compressed idx + 2
+  model.fit(batch_size=fit_batch_size, epochs=fit_epochs)
+  node_w, edge_w = model.get_weights()
+  return coords_to_embedding(inc, node_w[1:], edge_w[1:], dimension, "")
+
+
+def EmbedHg2vBoolean(hypergraph, dimension, num_neighbors=5, num_samples=200,
+                     batch_size=256, epochs=10, neg_samples=0,
+                     debug_summary_path=None, disable_pbar=False):
+  """FOBE: BooleanSamples + BooleanModel (embedding.py:308-329)."""
+  sampler_fn = lambda inc, ctx: sample_fobe(inc, num_neighbors, num_samples,
+                                            neg_samples, ctx=ctx)
+  emb = _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors,
+                                 sampler_fn, _hgx.LOSS_KLD, _hgx.ACT_SIGMOID,
+                                 batch_size, epochs, debug_summary_path,
+                                 disable_pbar)
+  emb.method_name = "HG2V_BOOLEAN"
+  return emb
+
+
+def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
+                     num_samples=200, batch_size=256, epochs=10,
+                     debug_summary_path=None, disable_pbar=False):
+  """HOBE: alg-dist (k=10, 20 iterations) + AlgebraicDistanceSamples +
+  UnweightedFloatModel (embedding.py:389-416). `alpha` is accepted and, as
+  in the reference, not used (_alpha_scale is called with alpha=0)."""
+  del alpha
+
+  def sampler_fn(inc, ctx):
+    x0 = np.random.random((inc.N, 10))  # algebraic_distance.py:140-141
+    y0 = np.random.random((inc.E, 10))
+    ctx.upload(inc)
+    ctx.alg_set(x0, y0)
+    ctx.alg_run(20)  # coords stay resident for the HOBE probabilities
+    return sample_hobe(inc, num_neighbors, num_samples, ctx=ctx)
+
+  emb = _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors,
+                                 sampler_fn, _hgx.LOSS_MSE, _hgx.ACT_RELU,
+                                 batch_size, epochs, debug_summary_path,
+                                 disable_pbar)
+  emb.method_name = "HG2V_ALG_DIST"
+  return emb
+
+
+def method_not_supported(hypergraph, dim, **kwargs):
+  raise RuntimeError(
+      "Method not supported. Try making the embedding on your own.")
+
+
+EMBEDDING_OPTIONS = {
+    "ALG_DIST": EmbedAlgebraicDistance,
+    "HG2V_BOOLEAN": EmbedHg2vBoolean,
+    "HG2V_ALG_DIST": EmbedHg2vAlgDist,
+    "HG2V_BOOLEAN_NS": lambda h, d, **kw: EmbedHg2vBoolean(h, d, neg_samples=500,
+                                                           **kw),
+    # outside the FOBE/HOBE hot path (SURVEY §2 "OUT OF SCOPE")
+    "SVD": method_not_supported,
+    "RANDOM": method_not_supported,
+    "NMF": method_not_supported,
+    "AUTO_ENCODER": method_not_supported,
+    "N2V3_BIPARTIDE": method_not_supported,
+    "N2V3_CLIQUE": method_not_supported,
+    "N2V5_BIPARTIDE": method_not_supported,
+    "N2V5_CLIQUE": method_not_supported,
+    "N2V7_BIPARTIDE": method_not_supported,
+    "N2V7_CLIQUE": method_not_supported,
+    "HG2V_ADJ_JAC": method_not_supported,
+    "HG2V_NEIGH_JAC": method_not_supported,
+    "metapath2vec++": method_not_supported,
+    "deepwalk": method_not_supported,
+    "LINE": method_not_supported,
+    "BiNE": method_not_supported,
+}
+
+DEBUG_SUMMARY_OPTIONS = {"HG2V_BOOLEAN", "HG2V_ALG_DIST"}
+
+__all__ = ["Embed", "EMBEDDING_OPTIONS", "DEBUG_SUMMARY_OPTIONS",
+           "COMBINATION_OPTIONS", "CombineEmbeddings", "EmbedHg2vBoolean",
+           "EmbedHg2vAlgDist", "EmbedAlgebraicDistance",
+           "CombineEmbeddingsViaConcatenation", "method_not_supported"]

@@ -1,0 +1,78 @@
+"""FOBE/HOBE models (reference: hypergraph_embedding/hg2v_model.py).
+
+The reference builds a Keras graph (two Embedding tables of (max_idx + 2) x d,
+uniform(-0.05, 0.05) init, three heads, Adagrad). Here a model is a pair of
+tables resident on the device plus its loss/activation; training is libhgx
+``hgx_train`` (Keras 2.x Adagrad semantics, see csrc/hgx_train.hip).
+
+BooleanModel      -> sigmoid heads, kullback_leibler_divergence (51-125)
+UnweightedFloatModel -> relu heads, mean_squared_error (129-203)
+KerasModelToEmbedding -> rows idx + 1 keyed by the original ids (31-48)
+"""
+
+from . import _hgx
+from .proto import HypergraphEmbedding
+from .runtime import get_context, numpy_seed
+
+
+class Hg2vModel:
+  """Two embedding tables on a device context (row 0 = padding)."""
+
+  def __init__(self, node_rows, edge_rows, dimension, num_neighbors, loss, act,
+               ctx=None, seed=None):
+    self.ctx = ctx or get_context()
+    self.dimension = dimension
+    self.num_neighbors = num_neighbors
+    self.loss = loss
+    self.act = act
+    self.ctx.model_init(dimension, node_rows, edge_rows,
+                        numpy_seed() if seed is None else seed)
+
+  def fit(self, batch_size=256, epochs=10, min_delta=1e-3, lr=0.01, eps=1e-7,
+          shuffle_seed=None, perms=None):
+    """Keras fit(shuffle=True) + EarlyStopping(monitor='loss', min_delta,
+    patience=0) over the records resident on the context."""
+    return self.ctx.train(batch=batch_size, max_epochs=epochs, lr=lr, eps=eps,
+                          loss=self.loss, act=self.act, min_delta=min_delta,
+                          shuffle_seed=numpy_seed() if shuffle_seed is None
+                          else shuffle_seed, perms=perms)
+
+  def get_weights(self):
+    return self.ctx.model_get()
+
+
+def _rows(hypergraph):
+  max_node = max(i for i in hypergraph.node)
+  max_edge = max(i for i in hypergraph.edge)
+  return max_node + 2, max_edge + 2
+
+
+def BooleanModel(hypergraph, dimension, num_neighbors):
+  n, e = _rows(hypergraph)
+  return Hg2vModel(n, e, dimension, num_neighbors, _hgx.LOSS_KLD,
+                   _hgx.ACT_SIGMOID)
+
+
+def UnweightedFloatModel(hypergraph, dimension, num_neighbors):
+  n, e = _rows(hypergraph)
+  return Hg2vModel(n, e, dimension, num_neighbors, _hgx.LOSS_MSE,
+                   _hgx.ACT_RELU)
+
+
+def KerasModelToEmbedding(hypergraph, model, node_map, edge_map,
+                          node_layer_name="node_embedding",
+                          edge_layer_name="edge_embedding"):
+  """Rows idx + 1 of the trained tables, keyed by node_map / edge_map."""
+  del node_layer_name, edge_layer_name
+  node_w, edge_w = model.get_weights()
+  emb = HypergraphEmbedding()
+  emb.dim = int(node_w.shape[1])
+  for node_idx in hypergraph.node:
+    emb.node[node_map[node_idx]].values.extend(node_w[node_idx + 1].tolist())
+  for edge_idx in hypergraph.edge:
+    emb.edge[edge_map[edge_idx]].values.extend(edge_w[edge_idx + 1].tolist())
+  return emb
+
+
+__all__ = ["Hg2vModel", "BooleanModel", "UnweightedFloatModel",
+           "KerasModelToEmbedding"]

@@ -1,0 +1,210 @@
+"""FOBE / HOBE samplers (reference: hypergraph_embedding/hg2v_sample.py).
+
+Same names and record semantics as the reference; the sampling runs on the
+GPU (libhgx ``hgx_sample_fobe`` / ``hgx_sample_hobe``), records stay in HBM
+in SamplesToModelInput layout for the trainer. The list-returning functions
+(``BooleanSamples``, ``AlgebraicDistanceSamples``) materialise
+``SimilarityRecord`` tuples only for API compatibility; the embedding
+pipeline (embedding.py) never leaves the device.
+
+Distribution parity: per row the reference draws min(q, |row|) distinct
+columns uniformly (np.random.choice(replace=False), :77-85) and K
+neighbours with replacement (:49-51). The device draws the same
+distribution from a counter-based generator keyed by a seed taken from
+numpy's global RNG, so np.random.seed(s) still makes runs reproducible.
+"""
+
+from collections import namedtuple
+
+import numpy as np
+
+from . import _hgx
+from .hypergraph_util import Incidence
+from .runtime import get_context, numpy_seed
+
+SimilarityRecord = namedtuple(
+    "SimilarityRecord",
+    ("left_node_idx", "left_edge_idx", "right_node_idx", "right_edge_idx",
+     "left_weight", "right_weight", "neighbor_node_indices",
+     "neighbor_node_weights", "neighbor_edge_indices", "neighbor_edge_weights",
+     "node_node_prob", "edge_edge_prob", "node_edge_prob"))
+SimilarityRecord.__new__.__defaults__ = (None,) * len(SimilarityRecord._fields)
+
+
+def _quotas(weights, num_samples):
+  # int(weight * num_samples) with the float32 proto weight (:138-146)
+  return np.array([int(float(w) * num_samples) for w in weights], np.int32)
+
+
+class DeviceRecords:
+  """Handle to the record stream resident on a context (n x (4+2K) int32
+  ids, +1 shifted, and n x 3 float32 targets)."""
+
+  def __init__(self, ctx, inc, n, K):
+    self.ctx, self.inc, self.n, self.K = ctx, inc, n, K
+
+  def arrays(self):
+    return self.ctx.records_get()
+
+  def to_similarity_records(self):
+    idx, tgt = self.arrays()
+    return records_from_arrays(idx, tgt, self.K)
+
+
+def records_from_arrays(idx, tgt, K):
+  """Inverse of SamplesToModelInput(weighted=False) for our own streams."""
+  out = []
+  for r, t in zip(idx.tolist(), tgt.tolist()):
+    ln, le, rn, re = (x - 1 if x > 0 else None for x in r[:4])
+    nn = [x - 1 for x in r[4:4 + K]] if ln is not None and re is not None and rn is None else None
+    ne = [x - 1 for x in r[4 + K:]] if nn is not None else None
+    out.append(SimilarityRecord(
+        left_node_idx=ln, left_edge_idx=le, right_node_idx=rn,
+        right_edge_idx=re, neighbor_node_indices=nn, neighbor_edge_indices=ne,
+        node_node_prob=t[0] if ln is not None and rn is not None else None,
+        edge_edge_prob=t[1] if le is not None and re is not None else None,
+        node_edge_prob=t[2] if nn is not None else None))
+  return out
+
+
+def sample_fobe(inc, num_neighbors, num_samples, neg_samples=0, ctx=None,
+                seed=None):
+  """BooleanSamples on the device; returns DeviceRecords."""
+  assert num_neighbors >= 1
+  ctx = ctx or get_context()
+  ctx.upload(inc)
+  nq = _quotas(inc.node_weight, num_samples)
+  eq = _quotas(inc.edge_weight, num_samples)
+  nnq = neq = None
+  if neg_samples > 0:
+    nnq = _quotas(inc.node_weight, neg_samples)
+    neq = _quotas(inc.edge_weight, neg_samples)
+  n = ctx.sample_fobe(numpy_seed() if seed is None else seed, num_neighbors,
+                      nq, eq, nnq, neq)
+  return DeviceRecords(ctx, inc, n, num_neighbors)
+
+
+def sample_hobe(inc, num_neighbors, num_samples, ctx=None, seed=None,
+                alg_coords=None):
+  """AlgebraicDistanceSamples on the device (alg coords must be resident on
+  ctx, e.g. from algebraic_distance.AlgebraicDistance, or given)."""
+  assert num_neighbors >= 0
+  assert num_samples >= 0
+  ctx = ctx or get_context()
+  if alg_coords is not None:
+    ctx.upload(inc)
+    ctx.alg_set(*alg_coords)
+  n = ctx.sample_hobe(numpy_seed() if seed is None else seed, num_neighbors,
+                      num_samples)
+  return DeviceRecords(ctx, inc, n, num_neighbors)
+
+
+def BooleanSamples(hypergraph, num_neighbors, num_samples, neg_samples=0,
+                   disable_pbar=False):
+  """hg2v_sample.py:125-242 (expects a compressed hypergraph, as the
+  skeleton passes; ids are the compressed ones)."""
+  del disable_pbar
+  inc = Incidence.from_hypergraph(hypergraph)
+  return sample_fobe(inc, num_neighbors, num_samples,
+                     neg_samples).to_similarity_records()
+
+
+def AlgebraicDistanceSamples(hypergraph, algebraic_embedding, num_neighbors,
+                             num_samples, run_in_parallel=True,
+                             disable_pbar=False):
+  """hg2v_sample.py:632-717: probabilities from the (float32) alg coords of
+  `algebraic_embedding`, keyed like the compressed hypergraph."""
+  del run_in_parallel, disable_pbar
+  inc = Incidence.from_hypergraph(hypergraph)
+  x = np.array([algebraic_embedding.node[int(i)].values for i in inc.node_ids],
+               np.float32)
+  y = np.array([algebraic_embedding.edge[int(i)].values for i in inc.edge_ids],
+               np.float32)
+  return sample_hobe(inc, num_neighbors, num_samples,
+                     alg_coords=(x, y)).to_similarity_records()
+
+
+def _same_type_dist_calc(indices, inc, alg_x, alg_y, is_edge, ctx=None):
+  """hg2v_sample.py:527-543 for one pair (device computed, bit-exact)."""
+  ctx = ctx or get_context()
+  ctx.upload(inc)
+  ctx.alg_set(alg_x, alg_y)
+  kind = _hgx.HOBE_EE if is_edge else _hgx.HOBE_NN
+  return float(ctx.hobe_probs(kind, [indices[0]], [indices[1]])[0])
+
+
+################################################################################
+# Samples to model input (hg2v_sample.py:725-797), host side                   #
+################################################################################
+
+
+def _inc_or_zero(x):
+  return 0 if x is None else x + 1
+
+
+def _val_or_zero(x):
+  return 0 if x is None else x
+
+
+def _pad_or_val(arr, idx):
+  if arr is None or idx >= len(arr):
+    return 0
+  return arr[idx]
+
+
+def _pad_or_inc(arr, idx):
+  if arr is None or idx >= len(arr):
+    return 0
+  return arr[idx] + 1
+
+
+def SamplesToModelInput(similarity_records, num_neighbors, weighted=True):
+  """Records -> (features, targets) lists, exactly as hg2v_sample.py:751-797."""
+  K = num_neighbors
+  ln, le, rn, re, lw, rw = [], [], [], [], [], []
+  nn = [[] for _ in range(K)]
+  nnw = [[] for _ in range(K)]
+  ne = [[] for _ in range(K)]
+  new = [[] for _ in range(K)]
+  p_nn, p_ee, p_ne = [], [], []
+  for r in similarity_records:
+    ln.append(_inc_or_zero(r.left_node_idx))
+    rn.append(_inc_or_zero(r.right_node_idx))
+    le.append(_inc_or_zero(r.left_edge_idx))
+    re.append(_inc_or_zero(r.right_edge_idx))
+    lw.append(_val_or_zero(r.left_weight))
+    rw.append(_val_or_zero(r.right_weight))
+    for i in range(K):
+      nn[i].append(_pad_or_inc(r.neighbor_node_indices, i))
+      ne[i].append(_pad_or_inc(r.neighbor_edge_indices, i))
+      if weighted:
+        nnw[i].append(_pad_or_val(r.neighbor_node_weights, i))
+        new[i].append(_pad_or_val(r.neighbor_edge_weights, i))
+    p_nn.append(_val_or_zero(r.node_node_prob))
+    p_ee.append(_val_or_zero(r.edge_edge_prob))
+    p_ne.append(_val_or_zero(r.node_edge_prob))
+  features = [ln, le, rn, re]
+  if weighted:
+    features += [lw, rw]
+  features += nn
+  if weighted:
+    features += nnw
+  features += ne
+  if weighted:
+    features += new
+  return features, [p_nn, p_ee, p_ne]
+
+
+def ModelInputToArrays(features, targets):
+  """(features, targets) of SamplesToModelInput(weighted=False) -> the
+  (n, 4+2K) int32 / (n, 3) float32 arrays hgx_records_set takes."""
+  idx = np.ascontiguousarray(np.array(features, dtype=np.int64).T,
+                             dtype=np.int32)
+  tgt = np.ascontiguousarray(np.array(targets, dtype=np.float64).T,
+                             dtype=np.float32)
+  return idx, tgt
+
+
+__all__ = ["SimilarityRecord", "BooleanSamples", "AlgebraicDistanceSamples",
+           "SamplesToModelInput", "ModelInputToArrays", "DeviceRecords",
+           "sample_fobe", "sample_hobe", "records_from_arrays"]

@@ -150,8 +150,10 @@ int hgx_model_get(hgx_ctx *ctx, float *node_tab, float *edge_tab);
 int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr, float eps,
               int loss, int act, float min_delta, uint64_t shuffle_seed,
               const int64_t *perms, float *epoch_loss, int *epochs_run);
-/* Device time (ms) of the last hgx_train spent in the per-batch kernels and
- * the number of records they processed. */
+/* Device time (ms) of the last hgx_train spent in the per-batch kernels
+ * (the K1+K2 replays, HIP events on the context stream; excludes the
+ * per-epoch shuffle and batch preparation) and the records / batches they
+ * processed. */
 int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
                          int64_t *batches);
 
