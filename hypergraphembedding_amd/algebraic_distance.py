@@ -73,13 +73,22 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None):
   """Node-row-sharded relaxation; the caller's process group does the
   exchange. Every rank must call it with the same inputs. Returns the node
   rows this rank owns (row0, row1, x_own) and all edge coords, already
-  rescaled, plus the device time in ms of the iteration loop."""
+  rescaled, plus the time in ms of the iteration loop.
+
+  `ctx` is a libhgx Context (exchange buffers on its GPU, RCCL) or any
+  object with the same alg_shard_* protocol; with device=cpu the exchange
+  buffers are host tensors and the collectives run over gloo (the CPU tests
+  drive this function with a numpy restatement of the shard kernels).
+  """
+  import time
+  import contextlib
   import torch
   import torch.distributed as dist
   world = dist.get_world_size(group)
   rank = dist.get_rank(group)
   r0, r1 = shard_rows(inc.rp_n, world, rank)
   dev = torch.device("cuda", ctx.device) if device is None else device
+  on_gpu = dev.type == "cuda"
   ctx.upload(inc)
   ctx.alg_set(x0, y0)
   k = x0.shape[1]
@@ -87,19 +96,23 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None):
   M = 2 * ks * 64  # HGX_MM_REPLICAS
   part = torch.zeros(inc.E * ks, dtype=torch.float32, device=dev)
   mm = torch.zeros(iterations * M, dtype=torch.int32, device=dev)
-  # kernels and collectives share one (non-default) torch stream: stream
-  # order is the only synchronisation needed between the phases
-  stream = torch.cuda.Stream(dev)
-  torch.cuda.synchronize(dev)
-  ctx.set_stream(stream.cuda_stream)
+  stream = None
+  if on_gpu:
+    # kernels and collectives share one (non-default) torch stream: stream
+    # order is the only synchronisation needed between the phases
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    ctx.set_stream(stream.cuda_stream)
   try:
     ks_lib = ctx.alg_shard_begin(r0, r1, part.data_ptr(), mm.data_ptr(),
                                  iterations)
     assert ks_lib == ks
-    start = torch.cuda.Event(enable_timing=True)
-    end = torch.cuda.Event(enable_timing=True)
-    with torch.cuda.stream(stream):
+    if on_gpu:
+      start = torch.cuda.Event(enable_timing=True)
+      end = torch.cuda.Event(enable_timing=True)
       start.record(stream)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream) if on_gpu else contextlib.nullcontext():
       for it in range(iterations):
         ctx.alg_shard_node(it)
         ctx.alg_shard_edge_partial(it)
@@ -107,12 +120,15 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None):
         ctx.alg_shard_edge_final(it)
         dist.all_reduce(mm[it * M:(it + 1) * M], op=dist.ReduceOp.MAX,
                         group=group)
-      end.record(stream)
+      if on_gpu:
+        end.record(stream)
     ctx.alg_shard_end()
-    torch.cuda.synchronize(dev)
+    if on_gpu:
+      torch.cuda.synchronize(dev)
   finally:
-    ctx.set_stream(None)
-  ms = start.elapsed_time(end)
+    if on_gpu:
+      ctx.set_stream(None)
+  ms = start.elapsed_time(end) if on_gpu else (time.perf_counter() - t0) * 1e3
   x, y = ctx.alg_get()
   return (r0, r1, x[r0:r1].copy()), y, ms
 

@@ -3,7 +3,8 @@
 UniformWeight (195-198) and WeightByNeighborhood (137-167) are computed on
 the device (libhgx ``hgx_incidence_weights``, bit-exact with the reference's
 double math rounded to float32 by DictToSparseRow) and returned as the same
-scipy CSR pair (node2weight N x E, edge2weight E x N). The small dict helpers
+scipy CSR pair as the reference (node2weight nodes x edges, edge2weight
+edges x nodes, indexed by the hypergraph's own ids). The small dict helpers
 (ZeroOneScaleValues 301-317, OneMinusValues 325-326, AlphaScaleValues
 329-333, DictToSparseRow 336-341) are host-side, as in the reference.
 """
@@ -17,10 +18,18 @@ from .runtime import get_context
 
 
 def _to_csr(inc, node_major, edge_major):
-  n2w = scipy.sparse.csr_matrix((node_major, inc.col_n, inc.rp_n),
-                                shape=(inc.N, inc.E), dtype=np.float32)
-  e2w = scipy.sparse.csr_matrix((edge_major, inc.col_e, inc.rp_e),
-                                shape=(inc.E, inc.N), dtype=np.float32)
+  """Weights keyed by the hypergraph's own ids, shaped like the reference's
+  ToCsrMatrix / ToEdgeCsrMatrix ((max id + 1) rows and columns)."""
+  nrow = int(inc.node_ids.max()) + 1 if inc.N else 0
+  ncol = int(inc.edge_ids.max()) + 1 if inc.E else 0
+  rows = np.repeat(inc.node_ids, np.diff(inc.rp_n))
+  cols = inc.edge_ids[inc.col_n]
+  n2w = scipy.sparse.csr_matrix((node_major, (rows, cols)), shape=(nrow, ncol),
+                                dtype=np.float32)
+  rows = np.repeat(inc.edge_ids, np.diff(inc.rp_e))
+  cols = inc.node_ids[inc.col_e]
+  e2w = scipy.sparse.csr_matrix((edge_major, (rows, cols)), shape=(ncol, nrow),
+                                dtype=np.float32)
   return n2w, e2w
 
 

@@ -1,0 +1,116 @@
+"""Test double: a numpy restatement of libhgx's alg_shard_* protocol
+(csrc/hgx_algdist.hip hgx_alg_shard_begin/node/edge_partial/edge_final/end)
+so the real multi-rank driver (algebraic_distance.alg_dist_sharded) can be
+exercised with gloo on CPU. Test infrastructure only.
+
+Buffers are the caller's CPU tensors (passed as data pointers, as the C ABI
+passes device pointers):
+  partial  float32 E x KS   [sum w, sum w * x_new]  over this rank's node rows
+  mm       int32 iters x 2 x KS x 64   order-preserving words, MAX-reduced:
+           max slot i holds f2ord(v), min slot KS+i holds ~f2ord(v)
+Coordinates are kept unscaled between iterations and the previous
+iteration's min/max are applied on read, as the kernels do.
+"""
+
+import ctypes
+
+import numpy as np
+
+REP = 64
+INT_MIN = np.int32(-2**31)
+
+
+def f2ord(v):
+  u = np.asarray(v, np.float32).view(np.uint32)
+  s = np.where(u & 0x80000000, ~u, u | 0x80000000).astype(np.uint32)
+  return (s ^ np.uint32(0x80000000)).view(np.int32)
+
+
+def ord2f(e):
+  s = np.asarray(e, np.int32).view(np.uint32) ^ np.uint32(0x80000000)
+  u = np.where(s & 0x80000000, s & 0x7fffffff, ~s).astype(np.uint32)
+  return u.view(np.float32)
+
+
+def _view(ptr, n, ctype, dtype):
+  return np.ctypeslib.as_array((ctype * n).from_address(ptr)).view(dtype)
+
+
+class ShardEmu:
+  device = None
+
+  def upload(self, inc):
+    self.inc = inc
+
+  def alg_set(self, x, y):
+    self.k = x.shape[1]
+    self.ks = ((self.k + 1) + 3) // 4 * 4
+    self.X = np.asarray(x, np.float32).copy()
+    self.Y = np.asarray(y, np.float32).copy()
+
+  def alg_shard_begin(self, row0, row1, d_partial, d_mm, iters):
+    inc = self.inc
+    self.row0, self.row1, self.iters = row0, row1, iters
+    self.part = _view(d_partial, inc.E * self.ks, ctypes.c_float,
+                      np.float32).reshape(inc.E, self.ks)
+    self.mm = _view(d_mm, iters * 2 * self.ks * REP, ctypes.c_int32,
+                    np.int32).reshape(iters, 2 * self.ks, REP)
+    self.mm[:] = INT_MIN
+    self.deg_n = np.diff(inc.rp_n).astype(np.float32)
+    self.deg_e = np.diff(inc.rp_e).astype(np.float32)
+    return self.ks
+
+  def _affine(self, it):
+    """(min, 1/(max-min)) per dim from slot it-1 (identity for it == 0)."""
+    if it == 0:
+      return np.zeros(self.k, np.float32), np.ones(self.k, np.float32)
+    w = self.mm[it - 1].max(axis=1)
+    hi = ord2f(w[1:self.k + 1])
+    lo = ord2f(~w[self.ks + 1:self.ks + self.k + 1])
+    return lo, (np.float32(1) / (hi - lo)).astype(np.float32)
+
+  def _fold(self, it, v):
+    slot = self.mm[it]
+    hi = f2ord(v.max(axis=0))
+    lo = ~f2ord(v.min(axis=0))
+    slot[1:self.k + 1, 0] = np.maximum(slot[1:self.k + 1, 0], hi)
+    slot[self.ks + 1:self.ks + self.k + 1, 0] = np.maximum(
+        slot[self.ks + 1:self.ks + self.k + 1, 0], lo)
+
+  def alg_shard_node(self, it):
+    inc, (m, d) = self.inc, self._affine(it)
+    ys = (self.Y.astype(np.float64) - m) * d
+    xn = self.X.copy()
+    for r in range(self.row0, self.row1):
+      c = inc.col_n[inc.rp_n[r]:inc.rp_n[r + 1]]
+      w = 1.0 / self.deg_e[c].astype(np.float64)
+      mean = (w[:, None] * ys[c]).sum(0) / w.sum()
+      xn[r] = (((self.X[r] - m) * d + mean) * 0.5).astype(np.float32)
+    if self.row1 > self.row0:
+      self._fold(it, xn[self.row0:self.row1])
+    self.Xn = xn
+
+  def alg_shard_edge_partial(self, it):
+    inc = self.inc
+    self.part[:] = 0
+    for e in range(inc.E):
+      c = inc.col_e[inc.rp_e[e]:inc.rp_e[e + 1]]
+      c = c[(c >= self.row0) & (c < self.row1)]
+      w = 1.0 / self.deg_n[c].astype(np.float64)
+      self.part[e, 0] = w.sum()
+      self.part[e, 1:self.k + 1] = (w[:, None] * self.Xn[c]).sum(0)
+
+  def alg_shard_edge_final(self, it):
+    m, d = self._affine(it)
+    mean = self.part[:, 1:self.k + 1] / self.part[:, :1]
+    yn = (((self.Y - m) * d + mean) * 0.5).astype(np.float32)
+    self._fold(it, yn)
+    self.X, self.Y = self.Xn, yn
+
+  def alg_shard_end(self):
+    m, d = self._affine(self.iters)
+    self.X = ((self.X - m) * d).astype(np.float32)
+    self.Y = ((self.Y - m) * d).astype(np.float32)
+
+  def alg_get(self):
+    return self.X, self.Y

@@ -1,0 +1,94 @@
+"""Multi-rank alg-dist driver on CPU: world_size 2 and 3 over gloo.
+
+The driver (algebraic_distance.alg_dist_sharded) is the one bench.py runs
+over RCCL; here each rank's kernels are the numpy restatement in
+shard_emu.py, so the test covers the decomposition (row shards, SUM of the
+edge partials, MAX of the order-preserving min/max words) against the
+reference's float64 golden vectors.
+"""
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import golden, golden_incidence
+from hypergraphembedding_amd.algebraic_distance import shard_rows
+
+
+def _free_port():
+  s = socket.socket()
+  s.bind(("127.0.0.1", 0))
+  p = s.getsockname()[1]
+  s.close()
+  return p
+
+
+def _worker(rank, world, port, out_path, iters):
+  import torch
+  import torch.distributed as dist
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  sys.path[:0] = [root, os.path.join(root, "oracle"),
+                  os.path.join(root, "tests")]
+  import oracle as O
+  from conftest import golden_incidence as gi
+  from shard_emu import ShardEmu
+  from hypergraphembedding_amd.algebraic_distance import alg_dist_sharded
+  os.environ["MASTER_ADDR"] = "127.0.0.1"
+  os.environ["MASTER_PORT"] = str(port)
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  inc = gi("csr_tiny.npz")
+  r = O.Rng(0)
+  x0, y0 = r.random((inc.N, 10)), r.random((inc.E, 10))
+  (r0, r1, xo), y, _ = alg_dist_sharded(ShardEmu(), inc, x0, y0, iters,
+                                        device=torch.device("cpu"))
+  np.savez(out_path + f".{rank}.npz", r0=r0, r1=r1, x=xo, y=y)
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_driver_gloo(tmp_path, world):
+  import torch.multiprocessing as mp
+  iters = 20
+  out = str(tmp_path / "shard")
+  mp.start_processes(_worker, args=(world, _free_port(), out, iters),
+                     nprocs=world, join=True, start_method="spawn")
+  inc = golden_incidence("csr_tiny.npz")
+  z = golden("algdist_tiny.npz")
+  x = np.full((inc.N, 10), np.nan, np.float32)
+  ys = []
+  for r in range(world):
+    d = np.load(out + f".{r}.npz")
+    x[int(d["r0"]):int(d["r1"])] = d["x"]
+    ys.append(d["y"])
+  assert not np.isnan(x).any()  # the shards tile the node rows
+  for y in ys[1:]:
+    assert np.array_equal(y, ys[0])  # edge coords replicated identically
+  assert np.abs(x - z["x_20"]).max() <= 1e-4
+  assert np.abs(ys[0] - z["y_20"]).max() <= 1e-4
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8, 64])
+def test_shard_rows_tile_and_balance(world, small_inc):
+  rp = small_inc.rp_n
+  spans = [shard_rows(rp, world, r) for r in range(world)]
+  assert spans[0][0] == 0 and spans[-1][1] == small_inc.N
+  for (a, b), (c, d) in zip(spans, spans[1:]):
+    assert b == c and a <= b
+  loads = [int(rp[b] - rp[a]) for a, b in spans]
+  assert sum(loads) == small_inc.nnz
+  max_deg = int(np.diff(rp).max())
+  assert max(loads) <= small_inc.nnz / world + max_deg + 1
+
+
+def test_order_words_roundtrip():
+  from shard_emu import f2ord, ord2f
+  v = np.array([-np.inf, -3.5, -1e-30, -0.0, 0.0, 1e-30, 0.25, 7.0, np.inf],
+               np.float32)
+  w = f2ord(v)
+  assert np.all(np.diff(w.astype(np.int64)) >= 0)  # order preserving
+  assert np.array_equal(ord2f(w), v)
+  assert np.all(np.diff((~w).astype(np.int64)) <= 0)  # ~ reverses order
