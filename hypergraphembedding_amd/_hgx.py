@@ -78,11 +78,13 @@ def lib():
   """Load libhgx.so (raises if it was not built)."""
   global _lib
   if _lib is None:
-    if not os.path.exists(LIB_PATH):
+    # HGX_LIB_PATH: load another build of the same ABI (A/B timing)
+    path = os.environ.get("HGX_LIB_PATH") or LIB_PATH
+    if not os.path.exists(path):
       raise ImportError(
-          f"{LIB_PATH} missing: run hypergraphembedding_amd.build.build() "
+          f"{path} missing: run hypergraphembedding_amd.build.build() "
           "(there is no CPU fallback)")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
       fn = getattr(L, name)
       fn.restype = res

@@ -23,9 +23,12 @@
 // The unique-row lists come from train_prep, run for a whole chunk of
 // batches in parallel (one workgroup per batch: LDS bitonic sort of the
 // batch's (row, slot) keys). K1/K2 for a run of batches are captured once
-// in a hipGraph and replayed; the batch index lives in device counters
-// (K1 reads ctr[0] and publishes ctr[1]; K2 reads ctr[1] and advances
-// ctr[0]), so the graph needs no per-batch arguments.
+// in hipGraphs of 64 batches each, the chunk-local batch index baked into
+// every node's arguments (no device counters, no dependent index load).
+// Preparation runs once per chunk of up to 1024 batches, on the same stream:
+// overlapping it with training on a second stream measured slower (the
+// per-batch kernels are latency-bound and lose more to the interference
+// than the preparation costs).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -38,7 +41,33 @@
 namespace {
 
 constexpr int kTB = 256;
-constexpr int kGraphBatches = 64;
+constexpr int kGraphBatches = 64;  // batches per chunk buffer and per graph
+
+// diagnostic ablation bits (HGX_TRAIN_ABLATE, timing experiments only;
+// results are wrong when set): 1 empty K1, 2 empty K2, 4 K1 gathers hit
+// row 0, 8 K1 skips gradient stores, 16 K2 skips slot sums, 32 K2 skips
+// the table read-modify-write.
+__constant__ int g_tab = 0;
+
+// diagnostic phase trace (HGX_TRAIN_TRACE=<file>, timing experiments only):
+// wave 0 of every workgroup stamps s_memrealtime (100 MHz) at phase ends
+// for the first g_trace_nb batches; slots [batch][kernel][block < 1024][8].
+__constant__ unsigned long long *g_trace = nullptr;
+__constant__ int g_trace_nb = 0;
+#define HGX_STAMP(var)                                              \
+  do {                                                              \
+    if (g_trace) {                                                  \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   \
+      var = __builtin_amdgcn_s_memrealtime();                       \
+    }                                                               \
+  } while (0)
+__device__ __forceinline__ void trace_put(int gb, int kern, int nst,
+                                          const unsigned long long *t) {
+  if (g_trace && threadIdx.x == 0 && gb < g_trace_nb && blockIdx.x < 1024) {
+    unsigned long long *q = g_trace + (((size_t)gb * 2 + kern) * 1024 + blockIdx.x) * 8;
+    for (int i = 0; i < nst; i++) q[i] = t[i];
+  }
+}
 
 struct TrainArgs {
   const int *idx;
@@ -53,7 +82,7 @@ struct TrainArgs {
   int *bidx;
   float *btgt;
   int *inv, *ukey, *uoff, *ucount;
-  int *ctr;  // [0] K1 batch, [1] K2 batch, [2] chunk base batch, [3] chunk nb
+  int2 *bmeta;  // per chunk-local batch: {records (0 = no batch), global batch}
   int SB, nblk1;
   float lr, eps;
   int loss, act;
@@ -110,36 +139,48 @@ __device__ __forceinline__ void load_row(const float *tab, int row, int dp,
   for (int v = 0; v < VPL; v++) out[v] = p[v * L + lane];
 }
 
-template <int L, int VPL, int KMAX>
-__global__ __launch_bounds__(kTB) void train_fwd_bwd(TrainArgs a) {
-  constexpr int RPB = kTB / L;
+// MODE: 0 = activation and loss read from the arguments; 1 = FOBE (sigmoid,
+// KLD); 2 = HOBE (relu, MSE). KEXACT: K == KMAX at compile time. The
+// specialised forms drop the per-record branches, exp and log of the other
+// head types: each wave runs its record chain alone on its SIMD, so its
+// instruction count is its latency.
+template <int L, int VPL, int KMAX, bool KEXACT, int MODE, int TB>
+__global__ __launch_bounds__(TB) void train_fwd_bwd(TrainArgs a, int cb) {
+  constexpr int RPB = TB / L;
   __shared__ float4 s_z[2][RPB][L * VPL];
   __shared__ float s_loss[RPB];
-  const int cb = a.ctr[0];
-  // publish before the tail check: a tail K2 must see cb >= nb and exit
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[1] = cb;
-  if (cb >= a.ctr[3]) return;
-  const int64_t gb = (int64_t)a.ctr[2] + cb;
-  const int64_t r0 = gb * a.B;
-  const int nb = (int)min((int64_t)a.B, a.n - r0);
-  const float inv_b = 1.0f / (float)nb;
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (g_trace) ts[0] = __builtin_amdgcn_s_memrealtime();
   const int grp = threadIdx.x / L, lane = threadIdx.x % L;
   const int rib = blockIdx.x * RPB + grp;
-  const int K = a.K, R = a.R, dp = a.dp;
+  const int K = KEXACT ? KMAX : a.K, R = KEXACT ? 4 + 2 * KMAX : a.R;
+  const int dp = a.dp;
+  // everything below depends only on (cb, rib): the batch metadata and the
+  // record's ids / slot positions load together (buffers are padded)
+  const int2 bm = a.bmeta[cb];
+  const int *ri = a.bidx + ((size_t)cb * a.B + rib) * R;
+  const float *yt = a.btgt + ((size_t)cb * a.B + rib) * 3;
+  const int *pos = a.inv + (size_t)cb * a.SB + (size_t)rib * R;
+  int ln = ri[0], le = ri[1], rn = ri[2], re = ri[3];
+  int nnk[KMAX], nek[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; k++) {
+    nnk[k] = k < K ? ri[4 + k] : 0;
+    nek[k] = k < K ? ri[4 + K + k] : 0;
+  }
+  const int nb = bm.x;
+  HGX_STAMP(ts[1]);
+  if (nb == 0 || (g_tab & 1)) return;
+  const float inv_b = 1.0f / (float)nb;
   float4 zN[VPL], zE[VPL];
 #pragma unroll
   for (int v = 0; v < VPL; v++) zN[v] = zE[v] = f4(0.f);
   float lrec = 0.f;
   if (rib < nb) {
-    const int *ri = a.bidx + ((size_t)cb * a.B + rib) * R;
-    const float *yt = a.btgt + ((size_t)cb * a.B + rib) * 3;
-    const int *pos = a.inv + (size_t)cb * a.SB + (size_t)rib * R;
-    const int ln = ri[0], le = ri[1], rn = ri[2], re = ri[3];
-    int nnk[KMAX], nek[KMAX];
+    if (g_tab & 4) {
+      ln = le = rn = re = 0;
 #pragma unroll
-    for (int k = 0; k < KMAX; k++) {
-      nnk[k] = k < K ? ri[4 + k] : 0;
-      nek[k] = k < K ? ri[4 + K + k] : 0;
+      for (int k = 0; k < KMAX; k++) nnk[k] = nek[k] = 0;
     }
     float4 Nl[VPL], Nr[VPL], El[VPL], Er[VPL], Nk[KMAX][VPL], Ek[KMAX][VPL];
     load_row<L, VPL>(a.ntab, ln, dp, lane, Nl);
@@ -153,6 +194,7 @@ __global__ __launch_bounds__(kTB) void train_fwd_bwd(TrainArgs a) {
         load_row<L, VPL>(a.etab, nek[k], dp, lane, Ek[k]);
       }
     }
+    HGX_STAMP(ts[2]);
     float z1 = 0.f, z2 = 0.f, za[KMAX], zb[KMAX];
 #pragma unroll
     for (int v = 0; v < VPL; v++) {
@@ -179,7 +221,8 @@ __global__ __launch_bounds__(kTB) void train_fwd_bwd(TrainArgs a) {
         zb[k] = group_sum<L>(zb[k]);
       }
     }
-    const int act = a.act;
+    const int act = MODE == 1 ? 0 : MODE == 2 ? 1 : a.act;
+    const int lossk = MODE == 1 ? 0 : MODE == 2 ? 1 : a.loss;
     const float y1 = act_f(act, z1), y2 = act_f(act, z2);
     float sa[KMAX], sb[KMAX], P = 0.f, Q = 0.f;
 #pragma unroll
@@ -195,10 +238,11 @@ __global__ __launch_bounds__(kTB) void train_fwd_bwd(TrainArgs a) {
     Q = Q / (float)K;
     const float y3 = P * Q;
     float l1, l2, l3, g1, g2, g3;
-    head_loss(a.loss, y1, yt[0], l1, g1);
-    head_loss(a.loss, y2, yt[1], l2, g2);
-    head_loss(a.loss, y3, yt[2], l3, g3);
+    head_loss(lossk, y1, yt[0], l1, g1);
+    head_loss(lossk, y2, yt[1], l2, g2);
+    head_loss(lossk, y3, yt[2], l3, g3);
     lrec = l1 + l2 + l3;
+    HGX_STAMP(ts[3]);
     g1 *= inv_b;
     g2 *= inv_b;
     g3 *= inv_b;
@@ -212,7 +256,7 @@ __global__ __launch_bounds__(kTB) void train_fwd_bwd(TrainArgs a) {
           if (edge) zE[v] = zE[v] + g[v];
           else zN[v] = zN[v] + g[v];
         }
-      } else {
+      } else if (!(g_tab & 8)) {
         float4 *p = reinterpret_cast<float4 *>(a.gslot + (size_t)pos[s] * dp);
 #pragma unroll
         for (int v = 0; v < VPL; v++) p[v * L + lane] = g[v];
@@ -249,6 +293,7 @@ __global__ __launch_bounds__(kTB) void train_fwd_bwd(TrainArgs a) {
 #pragma unroll
     for (int v = 0; v < VPL; v++) tmp[v] = fma4(dz2, Er[v], f4(0.f));
     emit(1, le, true, tmp);
+    HGX_STAMP(ts[4]);
   }
   // padding-row partials and loss: reduce over the record groups
 #pragma unroll
@@ -258,7 +303,7 @@ __global__ __launch_bounds__(kTB) void train_fwd_bwd(TrainArgs a) {
   }
   if (lane == 0) s_loss[grp] = lrec;
   __syncthreads();
-  for (int t = threadIdx.x; t < 2 * L * VPL; t += kTB) {
+  for (int t = threadIdx.x; t < 2 * L * VPL; t += TB) {
     const int tab = t / (L * VPL), j = t % (L * VPL);
     float4 s = f4(0.f);
     for (int g = 0; g < RPB; g++) s = s + s_z[tab][g][j];
@@ -267,79 +312,124 @@ __global__ __launch_bounds__(kTB) void train_fwd_bwd(TrainArgs a) {
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int g = 0; g < RPB; g++) s += s_loss[g];
-    a.lossbuf[(size_t)cb * a.nblk1 + blockIdx.x] = s;
+    a.lossbuf[(size_t)bm.y * a.nblk1 + blockIdx.x] = s;
+  }
+  HGX_STAMP(ts[5]);
+  trace_put(bm.y, 0, 6, ts);
+}
+
+// Adagrad on one float4 of a row (Keras 2.x formulas, round-to-nearest ops
+// so the device matches the oracle's rounding)
+__device__ __forceinline__ void adagrad4(float4 &p, float4 &ac, float4 g,
+                                         float lr, float eps) {
+  float *pp = &p.x, *aa = &ac.x;
+  const float *gv = &g.x;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const float na = __fadd_rn(aa[c], __fmul_rn(gv[c], gv[c]));
+    aa[c] = na;
+    pp[c] = __fsub_rn(pp[c], __fdiv_rn(__fmul_rn(lr, gv[c]),
+                                       __fadd_rn(sqrtf(na), eps)));
   }
 }
 
+// K2. Workgroups [0, gridDim-2): one L-lane group per unique touched row.
+// The last two workgroups: the padding row 0 of the node / edge table, its
+// gradient = the sum of the nblk1 per-K1-workgroup partials, loaded by all
+// 256 threads at once and tree-summed in LDS (fixed order: deterministic).
 template <int L, int VPL>
-__global__ __launch_bounds__(kTB) void train_update(TrainArgs a) {
+__global__ __launch_bounds__(kTB) void train_update(TrainArgs a, int cb) {
   constexpr int GPB = kTB / L;
-  const int cb = a.ctr[1];
-  if (cb >= a.ctr[3]) return;
-  const int U = a.ucount[cb];
-  const int *ukey = a.ukey + (size_t)cb * a.SB;
-  const int *uoff = a.uoff + (size_t)cb * (a.SB + 1);
-  const int grp = threadIdx.x / L, lane = threadIdx.x % L;
-  const int dp = a.dp;
-  for (int it = blockIdx.x * GPB + grp; it < U + 2; it += gridDim.x * GPB) {
-    float4 g[VPL];
-#pragma unroll
-    for (int v = 0; v < VPL; v++) g[v] = f4(0.f);
-    int table, row;
-    if (it < U) {
-      const int key = ukey[it];
-      table = key >> 30;
-      row = key & 0x3fffffff;
-      // this row's slot gradients are contiguous (prep sorted them)
-      const int j1 = uoff[it + 1];
-      for (int j = uoff[it]; j < j1; j++) {
-        const float4 *p = reinterpret_cast<const float4 *>(a.gslot + (size_t)j * dp);
-#pragma unroll
-        for (int v = 0; v < VPL; v++) g[v] = g[v] + p[v * L + lane];
-      }
-    } else {
-      table = it - U;
-      row = 0;
-      // padding row: one partial per K1 workgroup, 8 loads in flight
-      const float4 *base = reinterpret_cast<const float4 *>(a.gzero + (size_t)table * dp);
-      const size_t bstride = (size_t)2 * dp / 4;
-      int b = 0;
-      for (; b + 8 <= a.nblk1; b += 8) {
-#pragma unroll
-        for (int v = 0; v < VPL; v++) {
-          float4 t[8];
-#pragma unroll
-          for (int q = 0; q < 8; q++) t[q] = base[(b + q) * bstride + v * L + lane];
-#pragma unroll
-          for (int q = 0; q < 8; q++) g[v] = g[v] + t[q];
-        }
-      }
-      for (; b < a.nblk1; b++) {
-#pragma unroll
-        for (int v = 0; v < VPL; v++) g[v] = g[v] + base[b * bstride + v * L + lane];
-      }
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (g_trace) ts[0] = __builtin_amdgcn_s_memrealtime();
+  const int dp = a.dp, SB = a.SB;
+  const int2 bm = a.bmeta[cb];
+  if (blockIdx.x >= gridDim.x - 2) {
+    __shared__ float4 s_part[kTB];
+    const int table = blockIdx.x - (gridDim.x - 2);
+    const int NC = dp / 4;                  // float4 columns, <= 256
+    const int TPC = kTB / NC;               // threads per column (>= 1)
+    const int col = threadIdx.x % NC, sub = threadIdx.x / NC;
+    float4 *P = reinterpret_cast<float4 *>(table ? a.etab : a.ntab);
+    float4 *A = reinterpret_cast<float4 *>(table ? a.eacc : a.nacc);
+    const bool own = sub == 0;
+    float4 pv = f4(0.f), av = f4(0.f);
+    if (own && threadIdx.x < NC * TPC) {
+      pv = P[col];
+      av = A[col];
     }
-    float4 *P = reinterpret_cast<float4 *>((table ? a.etab : a.ntab) + (size_t)row * dp);
-    float4 *A = reinterpret_cast<float4 *>((table ? a.eacc : a.nacc) + (size_t)row * dp);
+    HGX_STAMP(ts[1]);
+    if (bm.x == 0 || (g_tab & 2)) return;
+    float4 g = f4(0.f);
+    if (sub < TPC && !(g_tab & 16)) {
+      const float4 *base = reinterpret_cast<const float4 *>(a.gzero) +
+                           (size_t)table * NC + col;
+      const size_t bstride = (size_t)2 * NC;
+      for (int b = sub; b < a.nblk1; b += TPC) g = g + base[b * bstride];
+    }
+    s_part[threadIdx.x] = g;
+    __syncthreads();
+    for (int w = TPC / 2; w > 0; w >>= 1) {  // TPC is a power of two
+      if (sub < w) s_part[threadIdx.x] = s_part[threadIdx.x] + s_part[threadIdx.x + w * NC];
+      __syncthreads();
+    }
+    HGX_STAMP(ts[2]);
+    if (own && !(g_tab & 32)) {
+      adagrad4(pv, av, s_part[col], a.lr, a.eps);
+      P[col] = pv;
+      A[col] = av;
+    }
+    HGX_STAMP(ts[3]);
+    trace_put(bm.y, 1, 4, ts);
+    return;
+  }
+  const int grp = threadIdx.x / L, lane = threadIdx.x % L;
+  const int it = blockIdx.x * GPB + grp;
+  // the task's key and slot range load beside the batch metadata
+  const int *ukey = a.ukey + (size_t)cb * SB;
+  const int *uoff = a.uoff + (size_t)cb * (SB + 1);
+  const int itc = min(it, SB - 1);
+  const int key = ukey[itc], j0 = uoff[itc], j1 = uoff[min(it + 1, SB)];
+  const int U = a.ucount[cb];
+  HGX_STAMP(ts[1]);
+  if (bm.x == 0 || (g_tab & 2) || it >= U) {
+    ts[2] = ts[3] = ts[1];
+    trace_put(bm.y, 1, 4, ts);
+    return;
+  }
+  const int table = key >> 30, row = key & 0x3fffffff;
+  float4 *P = reinterpret_cast<float4 *>((table ? a.etab : a.ntab) + (size_t)row * dp);
+  float4 *A = reinterpret_cast<float4 *>((table ? a.eacc : a.nacc) + (size_t)row * dp);
+  // table row and accumulator first: their latency hides under the sums
+  float4 pv[VPL], av[VPL];
+  if (!(g_tab & 32)) {
 #pragma unroll
     for (int v = 0; v < VPL; v++) {
-      const int j = v * L + lane;
-      float4 p = P[j], ac = A[j];
-      const float4 gg = g[v];
-      float *pp = &p.x, *aa = &ac.x;
-      const float *gv = &gg.x;
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const float na = __fadd_rn(aa[c], __fmul_rn(gv[c], gv[c]));
-        aa[c] = na;
-        pp[c] = __fsub_rn(pp[c], __fdiv_rn(__fmul_rn(a.lr, gv[c]),
-                                           __fadd_rn(sqrtf(na), a.eps)));
-      }
-      P[j] = p;
-      A[j] = ac;
+      pv[v] = P[v * L + lane];
+      av[v] = A[v * L + lane];
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr[0] = cb + 1;
+  float4 g[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; v++) g[v] = f4(0.f);
+  if (!(g_tab & 16)) {
+    // this row's slot gradients are contiguous (prep sorted them)
+    for (int j = j0; j < j1; j++) {
+      const float4 *p = reinterpret_cast<const float4 *>(a.gslot + (size_t)j * dp);
+#pragma unroll
+      for (int v = 0; v < VPL; v++) g[v] = g[v] + p[v * L + lane];
+    }
+  }
+  HGX_STAMP(ts[2]);
+  if (g_tab & 32) return;
+#pragma unroll
+  for (int v = 0; v < VPL; v++) {
+    adagrad4(pv[v], av[v], g[v], a.lr, a.eps);
+    P[v * L + lane] = pv[v];
+    A[v * L + lane] = av[v];
+  }
+  HGX_STAMP(ts[3]);
+  trace_put(bm.y, 1, 4, ts);
 }
 
 // Block-wide exclusive scan of one int per thread.
@@ -370,9 +460,13 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
   extern __shared__ __attribute__((aligned(16))) unsigned long long s_key[];
   __shared__ int s_ws[kTB / 64];
   const int cb = blockIdx.x;
-  if (cb >= nbc) return;
+  if (cb >= nbc) {  // graph nodes past the last batch find no work
+    if (threadIdx.x == 0) a.bmeta[cb] = make_int2(0, 0);
+    return;
+  }
   const int64_t r0 = (base + cb) * a.B;
   const int nb = (int)min((int64_t)a.B, a.n - r0);
+  if (threadIdx.x == 0) a.bmeta[cb] = make_int2(nb, (int)(base + cb));
   const int R = a.R, K = a.K;
   const int S = nb * R;
   int *bidx = a.bidx + (size_t)cb * a.B * R;
@@ -441,13 +535,6 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
     uoff[U] = V;
     a.ucount[cb] = U;
   }
-}
-
-__global__ void set_ctr(int *ctr, int base, int nbc) {
-  ctr[0] = 0;
-  ctr[1] = 0;
-  ctr[2] = base;
-  ctr[3] = nbc;
 }
 
 // deterministic two-level sum of the chunk's per-block losses:
@@ -560,20 +647,29 @@ void geometry(int d, int &L, int &VPL) {
   if (VPL == 3) VPL = 4;
 }
 
-using KFn = void (*)(TrainArgs);
+using KFn = void (*)(TrainArgs, int);
 
-template <int L, int VPL>
-KFn fwd_for_k(int K) {
-  if (K <= 2) return train_fwd_bwd<L, VPL, 2>;
-  if (K <= 5) return train_fwd_bwd<L, VPL, 5>;
-  if (K <= 8) return train_fwd_bwd<L, VPL, 8>;
-  return train_fwd_bwd<L, VPL, 16>;
+int env_int(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return v && v[0] ? atoi(v) : dflt;
 }
 
-bool pick_kernels(int L, int VPL, int K, KFn &k1, KFn &k2) {
+template <int L, int VPL>
+KFn fwd_for(int K, int loss, int act) {
+  if (K == 5 && loss == 0 && act == 0) return train_fwd_bwd<L, VPL, 5, true, 1, kTB>;
+  if (K == 5 && loss == 1 && act == 1) return train_fwd_bwd<L, VPL, 5, true, 2, kTB>;
+  if (K <= 2) return train_fwd_bwd<L, VPL, 2, false, 0, kTB>;
+  if (K <= 5) return train_fwd_bwd<L, VPL, 5, false, 0, kTB>;
+  if (K <= 8) return train_fwd_bwd<L, VPL, 8, false, 0, kTB>;
+  return train_fwd_bwd<L, VPL, 16, false, 0, kTB>;
+}
+
+bool pick_kernels(int L, int VPL, int K, int loss, int act, KFn &k1, KFn &k2) {
 #define HGX_CASE(LL, VV)                                                     \
   if (L == LL && VPL == VV) {                                                \
-    k1 = fwd_for_k<LL, VV>(K);                                               \
+    k1 = env_int("HGX_TRAIN_GENERIC", 0) == 1                                \
+             ? train_fwd_bwd<LL, VV, 16, false, 0, kTB>                      \
+             : fwd_for<LL, VV>(K, loss, act);                                \
     k2 = train_update<LL, VV>;                                               \
     return true;                                                             \
   }
@@ -583,6 +679,7 @@ bool pick_kernels(int L, int VPL, int K, KFn &k1, KFn &k2) {
 #undef HGX_CASE
   return false;
 }
+
 
 }  // namespace
 
@@ -763,28 +860,67 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
 
   int L, VPL;
   geometry(ctx->d, L, VPL);
+  const int tb1 = kTB;
   KFn k1 = nullptr, k2 = nullptr;
-  HGX_CHECK(ctx, pick_kernels(L, VPL, K, k1, k2), HGX_EUNSUP,
+  HGX_CHECK(ctx, pick_kernels(L, VPL, K, loss, act, k1, k2), HGX_EUNSUP,
             "no kernel for d=%d", ctx->d);
-  const int RPB = kTB / L;
+  {
+    const int ab = env_int("HGX_TRAIN_ABLATE", 0);
+    HGX_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_tab), &ab, sizeof(int)));
+  }
+  const char *trace_path = getenv("HGX_TRAIN_TRACE");
+  const int trace_nb = 256;
+  struct TraceBuf {
+    void *p = nullptr;
+    ~TraceBuf() {
+      if (p) {
+        unsigned long long *z = nullptr;
+        hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &z, sizeof(z));
+        hipFree(p);
+      }
+    }
+  } tb;
+  const size_t trace_bytes = sizeof(unsigned long long) * trace_nb * 2 * 1024 * 8;
+  {
+    unsigned long long *tp = nullptr;
+    int tn = 0;
+    if (trace_path && trace_path[0]) {
+      HGX_HIP(ctx, hipMalloc(&tb.p, trace_bytes));
+      HGX_HIP(ctx, hipMemset(tb.p, 0, trace_bytes));
+      tp = (unsigned long long *)tb.p;
+      tn = trace_nb;
+    }
+    HGX_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &tp, sizeof(tp)));
+    HGX_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_trace_nb), &tn, sizeof(tn)));
+  }
+  const int RPB = tb1 / L;
   const int nblk1 = (batch + RPB - 1) / RPB;
   const int GPB2 = kTB / L;
-  const int grid2 = std::max(1, std::min(256, (SB + 2 + GPB2 - 1) / GPB2));
+  // one unique-row task per group, plus the two padding-row workgroups
+  const int grid2 = (SB + GPB2 - 1) / GPB2 + 2;
   const int64_t nbatches = (n + batch - 1) / batch;
-  // chunk of batches whose unique-row lists are prepared together (<=~1 GB)
-  const int64_t per_batch = (int64_t)SB * 4 + 3 * batch + 2;
-  const int CB = (int)std::max<int64_t>(
-      1, std::min<int64_t>(nbatches, (int64_t)(256ll << 20) / per_batch));
+  const int GB = kGraphBatches;
+  // prep chunk: CB batches (a multiple of GB) prepared by one launch, then
+  // trained by CB / GB graph replays (graph g holds chunk-local batches
+  // [g*GB, (g+1)*GB), their indices baked into the node arguments)
+  const int CB = (int)std::min<int64_t>(1024, (nbatches + GB - 1) / GB * GB);
+  const int NG = CB / GB;
+  const int64_t nchunks = (nbatches + CB - 1) / CB;
 
-  // buffers
+  // record copies padded so K1's unconditional id loads stay in bounds
+  const size_t bidx_n = (size_t)CB * batch * R + (size_t)RPB * R * 2 + 64;
+  const size_t btgt_n = (size_t)CB * batch * 3 + (size_t)RPB * 3 * 2 + 64;
+  const size_t inv_n = (size_t)CB * SB + (size_t)RPB * R * 2 + 64;
+  const size_t prep_ints = bidx_n + btgt_n + inv_n + (size_t)CB * SB +
+                           (size_t)CB * (SB + 1) + CB + 2 * CB + 64;
   HGX_TRY(hgx_ensure(ctx, ctx->s1, sizeof(int) * (n + 1)));              // perm
   HGX_TRY(hgx_ensure(ctx, ctx->s2, sizeof(float) * (size_t)SB * dp));    // gslot
   HGX_TRY(hgx_ensure(ctx, ctx->s3, sizeof(float) * (size_t)nblk1 * 2 * dp));
-  HGX_TRY(hgx_ensure(ctx, ctx->s4, sizeof(float) * (size_t)CB * nblk1 + 16));
-  HGX_TRY(hgx_ensure(ctx, ctx->s5, sizeof(int) * ((size_t)CB * per_batch + 8)));
-  HGX_TRY(hgx_ensure(ctx, ctx->s6, 64 + sizeof(double) * kLossBlocks));  // ctr, loss
+  HGX_TRY(hgx_ensure(ctx, ctx->s4, sizeof(float) * (size_t)nbatches * nblk1 + 16));
+  HGX_TRY(hgx_ensure(ctx, ctx->s5, sizeof(int) * prep_ints));
+  HGX_TRY(hgx_ensure(ctx, ctx->s6, 64 + sizeof(double) * kLossBlocks));  // loss
   int *perm = ctx->s1.as<int>();
-  int *prep = ctx->s5.as<int>();
+  HGX_HIP(ctx, hipMemsetAsync(ctx->s5.p, 0, sizeof(int) * prep_ints, ctx->stream));
   TrainArgs a;
   a.idx = ctx->rec_idx.as<int>();
   a.tgt = ctx->rec_tgt.as<float>();
@@ -801,29 +937,39 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   a.gslot = ctx->s2.as<float>();
   a.gzero = ctx->s3.as<float>();
   a.lossbuf = ctx->s4.as<float>();
-  a.bidx = prep;                                         // CB*SB
-  a.inv = prep + (size_t)CB * SB;                        // CB*SB
-  a.ukey = prep + (size_t)CB * SB * 2;                   // CB*SB
-  a.uoff = prep + (size_t)CB * SB * 3;                   // CB*(SB+1)
-  a.btgt = reinterpret_cast<float *>(prep + (size_t)CB * (4 * (size_t)SB + 1));  // CB*B*3
-  a.ucount = prep + (size_t)CB * (4 * (size_t)SB + 1 + 3 * (size_t)batch);      // CB
-  a.ctr = ctx->s6.as<int>();
-  double *dloss = reinterpret_cast<double *>(ctx->s6.as<char>() + 32);
-  double *dpart = reinterpret_cast<double *>(ctx->s6.as<char>() + 64);
   a.SB = SB;
   a.nblk1 = nblk1;
   a.lr = lr;
   a.eps = eps;
   a.loss = loss;
   a.act = act;
+  {
+    int *q = ctx->s5.as<int>();
+    a.bidx = q;
+    q += bidx_n;
+    a.btgt = reinterpret_cast<float *>(q);
+    q += btgt_n;
+    a.inv = q;
+    q += inv_n;
+    a.ukey = q;
+    q += (size_t)CB * SB;
+    a.uoff = q;
+    q += (size_t)CB * (SB + 1);
+    a.ucount = q;
+    q += CB;
+    q += ((uintptr_t)q / sizeof(int)) % 2;  // 8-B align
+    a.bmeta = reinterpret_cast<int2 *>(q);
+  }
+  double *dloss = reinterpret_cast<double *>(ctx->s6.as<char>() + 32);
+  double *dpart = reinterpret_cast<double *>(ctx->s6.as<char>() + 64);
 
   // shuffle scratch (device shuffle only)
   size_t sort_tmp = 0, sort_off = 0;
   unsigned long long *keys_in = nullptr, *keys_out = nullptr;
   int *vals_in = nullptr;
   if (!perms) {
-    hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, keys_in, keys_out,
-                                       vals_in, perm, (int)n);
+    HGX_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, keys_in,
+                                                    keys_out, vals_in, perm, (int)n));
     sort_off = (sizeof(unsigned long long) * 2 * n + sizeof(int) * n + 255) / 256 * 256;
     HGX_TRY(hgx_ensure(ctx, ctx->s7, sort_off + sort_tmp + 256));
     char *base = ctx->s7.as<char>();
@@ -832,41 +978,51 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     vals_in = reinterpret_cast<int *>(keys_out + n);
   }
 
-  // graph: kGraphBatches x [K1, K2]. HGX_NO_GRAPH=1 launches the same
-  // kernels directly (profilers that mishandle graph replay).
-  const int GB = (int)std::min<int64_t>(kGraphBatches, CB);
-  const char *nog = getenv("HGX_NO_GRAPH");
-  const bool use_graph = !(nog && nog[0] == '1');
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t gexec = nullptr;
+  // graphs and events, released on every exit path
+  struct Res {
+    std::vector<hipGraph_t> graph;
+    std::vector<hipGraphExec_t> gexec;
+    std::vector<hipEvent_t> ev;
+    ~Res() {
+      for (auto g : gexec) (void)hipGraphExecDestroy(g);
+      for (auto g : graph) (void)hipGraphDestroy(g);
+      for (auto e : ev) (void)hipEventDestroy(e);
+    }
+  } res;
+  // HGX_NO_GRAPH=1 launches the same kernels directly (profilers that
+  // mishandle graph replay)
+  const bool use_graph = env_int("HGX_NO_GRAPH", 0) != 1;
+  auto launch_run = [&](int cb0, int nrun) {
+    for (int b = cb0; b < cb0 + nrun; b++) {
+      hipLaunchKernelGGL(k1, dim3(nblk1), dim3(tb1), 0, ctx->stream, a, b);
+      hipLaunchKernelGGL(k2, dim3(grid2), dim3(kTB), 0, ctx->stream, a, b);
+    }
+  };
   if (use_graph) {
-    HGX_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
-    for (int b = 0; b < GB; b++) {
-      hipLaunchKernelGGL(k1, dim3(nblk1), dim3(kTB), 0, ctx->stream, a);
-      hipLaunchKernelGGL(k2, dim3(grid2), dim3(kTB), 0, ctx->stream, a);
+    for (int g = 0; g < NG; g++) {
+      hipGraph_t gr = nullptr;
+      hipGraphExec_t ge = nullptr;
+      HGX_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
+      launch_run(g * GB, GB);
+      hipError_t ce = hipStreamEndCapture(ctx->stream, &gr);
+      if (ce != hipSuccess)
+        return hgx_fail(ctx, HGX_EHIP, "graph capture failed: %s", hipGetErrorString(ce));
+      res.graph.push_back(gr);
+      ce = hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
+      if (ce != hipSuccess)
+        return hgx_fail(ctx, HGX_EHIP, "graph instantiate failed: %s", hipGetErrorString(ce));
+      res.gexec.push_back(ge);
     }
-    hipError_t ce = hipStreamEndCapture(ctx->stream, &graph);
-    if (ce != hipSuccess)
-      return hgx_fail(ctx, HGX_EHIP, "graph capture failed: %s", hipGetErrorString(ce));
-    ce = hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0);
-    if (ce != hipSuccess) {
-      hipGraphDestroy(graph);
-      return hgx_fail(ctx, HGX_EHIP, "graph instantiate failed: %s", hipGetErrorString(ce));
-    }
+  }
+  // one event pair per prep chunk: device time of the batch kernels only
+  std::vector<hipEvent_t> bev(2 * nchunks);
+  for (auto &e : bev) {
+    HGX_HIP(ctx, hipEventCreate(&e));
+    res.ev.push_back(e);
   }
 
   std::vector<int> hperm;
-  // device time of the per-batch kernels only (K1+K2 replays), per chunk
-  std::vector<hipEvent_t> bev;
   double batch_ms = 0.0;
-  auto flush_events = [&]() {
-    for (size_t i = 0; i + 1 < bev.size(); i += 2) {
-      float m = 0.f;
-      if (hipEventElapsedTime(&m, bev[i], bev[i + 1]) == hipSuccess) batch_ms += m;
-    }
-    for (hipEvent_t e : bev) hipEventDestroy(e);
-    bev.clear();
-  };
   double best = INFINITY;
   int ep = 0;
   int rc = HGX_OK;
@@ -901,41 +1057,31 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
         break;
       }
     }
-    hipMemsetAsync(dloss, 0, sizeof(double), ctx->stream);
-    for (int64_t base = 0; base < nbatches; base += CB) {
+    (void)hipMemsetAsync(dloss, 0, sizeof(double), ctx->stream);
+    for (int64_t c = 0; c < nchunks && rc == HGX_OK; c++) {
+      const int64_t base = c * CB;
       const int nbc = (int)std::min<int64_t>(CB, nbatches - base);
-      hipLaunchKernelGGL(set_ctr, dim3(1), dim3(1), 0, ctx->stream, a.ctr,
-                         (int)base, nbc);
-      hipLaunchKernelGGL(train_prep, dim3(nbc), dim3(kTB),
-                         (size_t)P * sizeof(unsigned long long), ctx->stream, a,
-                         base, nbc, P);
-      hipEvent_t e0, e1;
-      hipEventCreate(&e0);
-      hipEventCreate(&e1);
-      bev.push_back(e0);
-      bev.push_back(e1);
-      hipEventRecord(e0, ctx->stream);
+      hipLaunchKernelGGL(train_prep, dim3(CB), dim3(kTB),
+                         (size_t)P * sizeof(unsigned long long), ctx->stream,
+                         a, base, nbc, P);
+      (void)hipEventRecord(bev[2 * c], ctx->stream);
       if (use_graph) {
-        for (int g = 0; g < nbc; g += GB) {
-          if (hipGraphLaunch(gexec, ctx->stream) != hipSuccess) {
+        for (int g = 0; g * GB < nbc; g++) {
+          if (hipGraphLaunch(res.gexec[g], ctx->stream) != hipSuccess) {
             rc = hgx_fail(ctx, HGX_EHIP, "graph launch failed");
             break;
           }
         }
       } else {
-        for (int g = 0; g < nbc; g++) {
-          hipLaunchKernelGGL(k1, dim3(nblk1), dim3(kTB), 0, ctx->stream, a);
-          hipLaunchKernelGGL(k2, dim3(grid2), dim3(kTB), 0, ctx->stream, a);
-        }
+        launch_run(0, nbc);
       }
-      hipEventRecord(e1, ctx->stream);
-      if (rc) break;
-      hipLaunchKernelGGL(loss_partial, dim3(kLossBlocks), dim3(kTB), 0,
-                         ctx->stream, a.lossbuf, (int64_t)nbc * nblk1, dpart);
-      hipLaunchKernelGGL(loss_final, dim3(1), dim3(kLossBlocks), 0,
-                         ctx->stream, dpart, dloss);
+      (void)hipEventRecord(bev[2 * c + 1], ctx->stream);
     }
     if (rc) break;
+    hipLaunchKernelGGL(loss_partial, dim3(kLossBlocks), dim3(kTB), 0,
+                       ctx->stream, a.lossbuf, nbatches * nblk1, dpart);
+    hipLaunchKernelGGL(loss_final, dim3(1), dim3(kLossBlocks), 0, ctx->stream,
+                       dpart, dloss);
     double lsum = 0.0;
     if (hipMemcpyAsync(&lsum, dloss, sizeof(double), hipMemcpyDeviceToHost,
                        ctx->stream) != hipSuccess ||
@@ -944,7 +1090,11 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
                     hipGetErrorString(hipGetLastError()));
       break;
     }
-    flush_events();
+    for (int64_t c = 0; c < nchunks; c++) {
+      float m = 0.f;
+      if (hipEventElapsedTime(&m, bev[2 * c], bev[2 * c + 1]) == hipSuccess)
+        batch_ms += m;
+    }
     const double cur = lsum / (double)n;
     if (epoch_loss) epoch_loss[ep] = (float)cur;
     if (cur < best - (double)min_delta) {
@@ -956,11 +1106,17 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   }
   hipEventRecord(ctx->ev1, ctx->stream);
   hipEventSynchronize(ctx->ev1);
-  flush_events();
   float ms = 0.f;
   hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
-  if (gexec) hipGraphExecDestroy(gexec);
-  if (graph) hipGraphDestroy(graph);
+  if (tb.p && rc == HGX_OK) {
+    std::vector<unsigned long long> h(trace_bytes / 8);
+    if (hipMemcpy(h.data(), tb.p, trace_bytes, hipMemcpyDeviceToHost) == hipSuccess) {
+      if (FILE *f = fopen(trace_path, "wb")) {
+        fwrite(h.data(), 1, trace_bytes, f);
+        fclose(f);
+      }
+    }
+  }
   if (rc) return rc;
   HGX_LAUNCH_CHECK(ctx);
   ctx->train_ms = batch_ms;
