@@ -7,9 +7,10 @@ HOBE record, batch 256, fresh device shuffle) with the records, tables and
 incidence already resident in HBM. Reported beside it, from the same run:
 the algebraic-distance relaxation (k=10, 20 iterations) in algorithmic GB/s,
 HOBE sampling time, the roofline object of the dominant kernel (the per-batch
-train_fwd_bwd + train_update pair) and the CPU baseline (the oracle's
+train_fwd_bwd + train_update pair), the CPU baseline (the oracle's
 single-threaded trainer, oracle/hgref.c, on a bounded slice of the same
-records).
+records) and, in "algdist_c4", the relaxation on the power-law 10M/5M graph
+(the C4 shape; node-row sharded over RCCL when --gpus > 1).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -49,6 +50,8 @@ def parse():
   p.add_argument("--cpu-records", type=int, default=2_000_000,
                  help="records of the bounded CPU-baseline slice")
   p.add_argument("--no-cpu", action="store_true")
+  p.add_argument("--no-c4", action="store_true",
+                 help="skip the power-law 10M/5M alg-dist measurement")
   return p.parse_args()
 
 
@@ -191,6 +194,43 @@ def main():
                      f"oracle/hgref.c hgref_train single-threaded, "
                      f"{cpu_s:.1f} s"}
 
+  # ---- alg-dist on the power-law 10M/5M graph (C4 shape, k=10) ----
+  c4 = None
+  if not args.no_c4:
+    from hypergraphembedding_amd.synthetic import powerlaw_hypergraph
+    t = time.time()
+    big = powerlaw_hypergraph(seed=0)
+    c4_gen = time.time() - t
+    ctx.upload(big)
+    rs4 = np.random.RandomState(1)
+    bx0 = rs4.random_sample((big.N, k)).astype(np.float32)
+    by0 = rs4.random_sample((big.E, k)).astype(np.float32)
+    b_iter4 = 8.0 * big.nnz + (8.0 + 12.0 * k) * (big.N + big.E)
+    if world > 1:
+      alg_dist_sharded(ctx, big, bx0, by0, 2)  # warm
+      ms4 = alg_dist_sharded(ctx, big, bx0, by0, args.alg_iters)[2]
+      import torch
+      tt = torch.tensor([ms4], device="cuda")
+      dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+      ms4 = float(tt.item())
+    else:
+      ctx.alg_set(bx0, by0)
+      ctx.alg_run(2)  # warm
+      ctx.alg_set(bx0, by0)
+      ctx.alg_run(args.alg_iters)
+      ms4 = ctx.alg_stats()[0]
+    gbps4 = b_iter4 * args.alg_iters / (ms4 * 1e-3) / 1e9
+    c4 = {"graph": "power-law 10M nodes / 5M edges, node degree 1+Poisson(19), "
+                   "edge choice ~ rank^-0.8, seed 0 (libhgx host generator)",
+          "nodes": big.N, "edges": big.E, "nnz": big.nnz,
+          "max_edge": int(big.edge_size().max()), "k": k,
+          "iters": args.alg_iters,
+          "ms_per_iter": round(ms4 / args.alg_iters, 3),
+          "gbps": round(gbps4, 1), "bytes_per_iter": b_iter4,
+          "frac_of_hbm_peak": round(gbps4 / HBM_PEAK_GBPS, 4),
+          "sharded": world > 1, "graph_gen_s": round(c4_gen, 1)}
+    del big, bx0, by0
+
   if rank == 0:
     out = {
         "metric": METRIC,
@@ -223,6 +263,7 @@ def main():
                     "bytes_per_iter": bytes_iter,
                     "frac_of_hbm_peak": round(alg_gbps / HBM_PEAK_GBPS, 4),
                     "sharded": world > 1},
+        "algdist_c4": c4,
         "hobe_sampling_s": round(sample_s, 3),
         "graph_gen_s": round(gen_s, 2),
         "roofline": roofline,

@@ -63,6 +63,10 @@ SIGNATURES = {
     "hgx_train": (_int, [_vp, _int, _int, _f32, _f32, _int, _int, _f32, _u64,
                          _vp, _vp, _pint]),
     "hgx_train_last_stats": (_int, [_vp, _pdbl, _pi64, _pi64]),
+    "hgx_synth_powerlaw": (_int, [_i32, _i32, ctypes.c_double, ctypes.c_double,
+                                  _u64, _vp, _vp, _pi64,
+                                  ctypes.POINTER(ctypes.c_int32)]),
+    "hgx_csr_transpose": (_int, [_i32, _i32, _vp, _vp, _vp, _vp]),
 }
 
 
@@ -289,3 +293,34 @@ class Context:
     self._chk(lib().hgx_train_last_stats(self.h, ctypes.byref(ms),
                                          ctypes.byref(rec), ctypes.byref(bat)))
     return ms.value, rec.value, bat.value
+
+
+# ---- host utilities (no context, no device) --------------------------------
+def synth_powerlaw(N, E, mean_degree=20.0, exponent=0.8, seed=0):
+  """(rp_n, col_n, E_kept) of hgx_synth_powerlaw."""
+  rp = np.zeros(N + 1, np.int32)
+  nnz = ctypes.c_int64()
+  rc = lib().hgx_synth_powerlaw(N, E, mean_degree, exponent, seed, _ptr(rp),
+                                None, ctypes.byref(nnz), None)
+  if rc != HGX_OK:
+    _raise(rc, "hgx_synth_powerlaw failed")
+  col = np.empty(nnz.value, np.int32)
+  e_out = ctypes.c_int32()
+  rc = lib().hgx_synth_powerlaw(N, E, mean_degree, exponent, seed, _ptr(rp),
+                                _ptr(col), ctypes.byref(nnz),
+                                ctypes.byref(e_out))
+  if rc != HGX_OK:
+    _raise(rc, "hgx_synth_powerlaw failed")
+  return rp, col, int(e_out.value)
+
+
+def csr_transpose(nrow, ncol, rp, col):
+  rp = _c(rp, np.int32)
+  col = _c(col, np.int32)
+  rpt = np.empty(ncol + 1, np.int32)
+  colt = np.empty(col.size, np.int32)
+  rc = lib().hgx_csr_transpose(nrow, ncol, _ptr(rp), _ptr(col), _ptr(rpt),
+                               _ptr(colt))
+  if rc != HGX_OK:
+    _raise(rc, "hgx_csr_transpose: column index out of range")
+  return rpt, colt

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void algdist_half_narrow(
     int row0, int R, const int *__restrict__ rp, const int *__restrict__ col,
     const float *__restrict__ self_in, const float *__restrict__ src,
     float *__restrict__ out, const int *__restrict__ mm_prev, int src_affine,
-    int *__restrict__ mm_cur, int k) {
+    int *__restrict__ mm_cur, int k, int long_thresh) {
   constexpr int NV = KS / 4;
   __shared__ float s_m[KS], s_d[KS];
   load_affine(mm_prev, KS, k, s_m, s_d, true);
@@ -177,6 +177,7 @@ __global__ __launch_bounds__(kBlock) void algdist_half_narrow(
   for (int rr = blockIdx.x * GPB + tid / G; rr < R; rr += ngroups) {
     const int r = row0 + rr;
     const int beg = rp[r], end = rp[r + 1];
+    if (end - beg > long_thresh) continue;  // seg_partial + long_finish
     // own row early (MODE_FULL): its latency hides under the gathers
     // lane lg owns output vectors j = lg, lg + G, ...
     float4 self[NV];
@@ -262,6 +263,149 @@ __global__ __launch_bounds__(kBlock) void algdist_half_narrow(
     }
   }
   if (MODE == MODE_FULL && !(g_ablate & 1)) flush_minmax<KS>(lmn, lmx, k, mm_cur);
+}
+
+// Long rows, step 1: one wave per piece of `T` incidences of a long row
+// (LongRows): part[piece] = [sum w, sum w*src] over the piece, raw sums (the
+// affine of a scaled source commutes with the weighted mean; long_finish
+// applies it).
+template <int KS, int M>
+__global__ __launch_bounds__(kBlock) void algdist_seg_partial(
+    int nseg, const int2 *__restrict__ seg, int T, const int *__restrict__ rp,
+    const int *__restrict__ col, const float *__restrict__ src,
+    float *__restrict__ part) {
+  constexpr int NV = KS / 4;
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (kBlock / 64);
+  const float4 *src4 = reinterpret_cast<const float4 *>(src);
+  float4 *part4 = reinterpret_cast<float4 *>(part);
+  for (int s = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); s < nseg; s += nw) {
+    const int2 sg = seg[s];
+    const int beg = rp[sg.x] + sg.y * T, end = min(rp[sg.x + 1], beg + T);
+    float4 acc[NV];
+#pragma unroll
+    for (int j = 0; j < NV; j++) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float wsum = 0.f;
+    for (int base = beg + lane; base < end; base += 64 * M) {
+      int c[M];
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        const int t = base + 64 * m;
+        c[m] = t < end ? col[t] : -1;
+      }
+      float4 v[M][NV];
+#pragma unroll
+      for (int m = 0; m < M; m++)
+        if (c[m] >= 0) {
+#pragma unroll
+          for (int j = 0; j < NV; j++) v[m][j] = src4[(size_t)c[m] * NV + j];
+        }
+#pragma unroll
+      for (int m = 0; m < M; m++)
+        if (c[m] >= 0) {
+          const float w = v[m][0].x;
+          wsum += w;
+#pragma unroll
+          for (int j = 0; j < NV; j++) acc[j] = f4fma(w, v[m][j], acc[j]);
+        }
+    }
+    wsum = hgx::group_allreduce_sum<64>(wsum);
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+      acc[j].x = hgx::group_allreduce_sum<64>(acc[j].x);
+      acc[j].y = hgx::group_allreduce_sum<64>(acc[j].y);
+      acc[j].z = hgx::group_allreduce_sum<64>(acc[j].z);
+      acc[j].w = hgx::group_allreduce_sum<64>(acc[j].w);
+    }
+    acc[0].x = wsum;
+#pragma unroll
+    for (int j = 0; j < NV; j++)
+      if (j == lane) part4[(size_t)s * NV + j] = acc[j];
+  }
+}
+
+// Long rows, step 2: one wave per long row sums its pieces (lane-strided,
+// then a fixed tree: deterministic) and writes the row like the narrow
+// kernel's output stage (MODE_FULL, with min/max) or its partial
+// (MODE_PARTIAL).
+template <int KS, int MODE>
+__global__ __launch_bounds__(kBlock) void algdist_long_finish(
+    int nlong, const int *__restrict__ lrows, const int *__restrict__ loff,
+    const float *__restrict__ part, const int *__restrict__ rp,
+    const float *__restrict__ self_in, float *__restrict__ out,
+    const int *__restrict__ mm_prev, int src_affine, int *__restrict__ mm_cur,
+    int k) {
+  constexpr int NV = KS / 4;
+  __shared__ float s_m[KS], s_d[KS];
+  load_affine(mm_prev, KS, k, s_m, s_d, true);
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (kBlock / 64);
+  const float4 *part4 = reinterpret_cast<const float4 *>(part);
+  float lmn[KS], lmx[KS];
+#pragma unroll
+  for (int i = 0; i < KS; i++) {
+    lmn[i] = INFINITY;
+    lmx[i] = -INFINITY;
+  }
+  for (int j = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); j < nlong; j += nw) {
+    const int r = lrows[j], s0 = loff[j], s1 = loff[j + 1];
+    float4 acc[NV];
+#pragma unroll
+    for (int q = 0; q < NV; q++) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = s0 + lane; s < s1; s += 64) {
+#pragma unroll
+      for (int q = 0; q < NV; q++) {
+        const float4 p = part4[(size_t)s * NV + q];
+        acc[q].x += p.x;
+        acc[q].y += p.y;
+        acc[q].z += p.z;
+        acc[q].w += p.w;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NV; q++) {
+      acc[q].x = hgx::group_allreduce_sum<64>(acc[q].x);
+      acc[q].y = hgx::group_allreduce_sum<64>(acc[q].y);
+      acc[q].z = hgx::group_allreduce_sum<64>(acc[q].z);
+      acc[q].w = hgx::group_allreduce_sum<64>(acc[q].w);
+    }
+    float4 *op = reinterpret_cast<float4 *>(out) + (size_t)r * NV;
+    if (MODE == MODE_PARTIAL) {
+#pragma unroll
+      for (int q = 0; q < NV; q++)
+        if (q == lane) op[q] = acc[q];
+      continue;
+    }
+    const float inv_w = 1.0f / acc[0].x;
+    const int len = rp[r + 1] - rp[r];
+    const float4 *sp = reinterpret_cast<const float4 *>(self_in) + (size_t)r * NV;
+#pragma unroll
+    for (int q = 0; q < NV; q++) {
+      if (q != lane) continue;
+      const float4 sv4 = sp[q];
+      float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const int i = 4 * q + c;
+        float v;
+        if (i == 0) {
+          v = 1.0f / (float)len;
+        } else if (i <= k) {
+          const float sv = (f4get(sv4, c) - s_m[i]) * s_d[i];
+          float mv = f4get(acc[q], c) * inv_w;
+          if (src_affine) mv = (mv - s_m[i]) * s_d[i];
+          v = (sv + mv) * 0.5f;
+          lmn[i] = fminf(lmn[i], v);
+          lmx[i] = fmaxf(lmx[i], v);
+        } else {
+          v = 0.f;
+        }
+        f4set(o, c, v);
+      }
+      op[q] = o;
+    }
+  }
+  if (MODE == MODE_FULL) flush_minmax<KS>(lmn, lmx, k, mm_cur);
 }
 
 // Incidence-parallel half-sweep for narrow rows (KS <= 20). Rows are cut
@@ -644,7 +788,28 @@ int pick_g(double avg) {
 }
 
 using HalfFn = void (*)(int, int, const int *, const int *, const float *,
-                        const float *, float *, const int *, int, int *, int);
+                        const float *, float *, const int *, int, int *, int,
+                        int);
+using SegFn = void (*)(int, const int2 *, int, const int *, const int *,
+                       const float *, float *);
+using FinFn = void (*)(int, const int *, const int *, const float *,
+                       const int *, const float *, float *, const int *, int,
+                       int *, int);
+
+template <int MODE>
+bool long_fns(int ks, SegFn &seg, FinFn &fin) {
+  switch (ks) {
+#define HGX_LCASE(KSV)                                   \
+    case KSV:                                            \
+      seg = algdist_seg_partial<KSV, 4>;                 \
+      fin = algdist_long_finish<KSV, MODE>;              \
+      return true;
+    HGX_LCASE(4) HGX_LCASE(8) HGX_LCASE(12) HGX_LCASE(16) HGX_LCASE(20)
+#undef HGX_LCASE
+    default:
+      return false;
+  }
+}
 using FlatFn = void (*)(int, const int *, const int *, const int *,
                         const float *, const float *, float *, const int *, int,
                         int *, int);
@@ -701,7 +866,7 @@ HalfFn narrow_fn(int ks, int g) {
 int launch_half(hgx_ctx *ctx, int mode, int row0, int R, const int *rp,
                 const int *col, const float *self_in, const float *src,
                 float *out, const int *mm_prev, int src_affine, int *mm_cur,
-                double avg, const int *blk, int nblk) {
+                double avg, const int *blk, int nblk, LongRows *lr) {
   const int k = ctx->k, KS = ctx->ks;
   if (R <= 0) return HGX_OK;
   static const bool flat_env = [] {
@@ -714,13 +879,33 @@ int launch_half(hgx_ctx *ctx, int mode, int row0, int R, const int *rp,
                        dim3(kBlock), 0, ctx->stream, nblk, blk, rp, col,
                        self_in, src, out, mm_prev, src_affine, mm_cur, k);
   } else if (KS <= 20) {
+    int thresh = INT_MAX;
+    if (lr && lr->nlong > 0) {
+      SegFn seg = nullptr;
+      FinFn fin = nullptr;
+      const bool ok = mode == MODE_FULL ? long_fns<MODE_FULL>(KS, seg, fin)
+                                        : long_fns<MODE_PARTIAL>(KS, seg, fin);
+      if (ok) {
+        thresh = lr->thresh;
+        HGX_TRY(hgx_ensure(ctx, lr->part, sizeof(float) * (size_t)lr->nseg * KS));
+        hipLaunchKernelGGL(seg, dim3(grid_for(lr->nseg, kBlock / 64, resident_grid(seg))),
+                           dim3(kBlock), 0, ctx->stream, lr->nseg,
+                           lr->seg.as<int2>(), lr->thresh, rp, col, src,
+                           lr->part.as<float>());
+        hipLaunchKernelGGL(fin, dim3(grid_for(lr->nlong, kBlock / 64, resident_grid(fin))),
+                           dim3(kBlock), 0, ctx->stream, lr->nlong,
+                           lr->rows.as<int>(), lr->off.as<int>(),
+                           lr->part.as<float>(), rp, self_in, out, mm_prev,
+                           src_affine, mm_cur, k);
+      }
+    }
     const int g = pick_g(avg);
     HalfFn fn = mode == MODE_FULL ? narrow_fn<MODE_FULL>(KS, g)
                                   : narrow_fn<MODE_PARTIAL>(KS, g);
     hipLaunchKernelGGL(fn, dim3(grid_for(R, kBlock / g, resident_grid(fn))),
                        dim3(kBlock), 0,
                        ctx->stream, row0, R, rp, col, self_in, src, out,
-                       mm_prev, src_affine, mm_cur, k);
+                       mm_prev, src_affine, mm_cur, k, thresh);
   } else {
     auto fn = mode == MODE_FULL ? algdist_half_wide<MODE_FULL>
                                 : algdist_half_wide<MODE_PARTIAL>;
@@ -844,11 +1029,13 @@ extern "C" int hgx_alg_run(hgx_ctx *ctx, int iters) {
     // node half: self x (scaled), gathered y (scaled)
     HGX_TRY(launch_half(ctx, MODE_FULL, 0, ctx->N, ctx->rp_n.as<int>(),
                         ctx->col_n.as<int>(), xc, yc, xn, prev, prev != nullptr,
-                        cur, ctx->avg_deg_n, ctx->blk_n.as<int>(), ctx->nblk_n));
+                        cur, ctx->avg_deg_n, ctx->blk_n.as<int>(), ctx->nblk_n,
+                        &ctx->long_n));
     // edge half: self y (scaled), gathered NEW x (raw)
     HGX_TRY(launch_half(ctx, MODE_FULL, 0, ctx->E, ctx->rp_e.as<int>(),
                         ctx->col_e.as<int>(), yc, xn, yn, prev, 0, cur,
-                        ctx->avg_deg_e, ctx->blk_e.as<int>(), ctx->nblk_e));
+                        ctx->avg_deg_e, ctx->blk_e.as<int>(), ctx->nblk_e,
+                        &ctx->long_e));
     ctx->xcur ^= 1;
     ctx->ycur ^= 1;
   }
@@ -954,6 +1141,8 @@ extern "C" int hgx_alg_shard_begin(hgx_ctx *ctx, int32_t row0, int32_t row1,
                                 ctx->nblk_sn));
     HGX_TRY(hgx_make_row_blocks(ctx, rpl.data(), 0, ctx->E, ctx->blk_el,
                                 ctx->nblk_el));
+    HGX_TRY(hgx_make_long_rows(ctx, rpn.data(), row0, row1, ctx->long_sn));
+    HGX_TRY(hgx_make_long_rows(ctx, rpl.data(), 0, ctx->E, ctx->long_el));
   }
   ctx->row0 = row0;
   ctx->row1 = row1;
@@ -978,7 +1167,7 @@ extern "C" int hgx_alg_shard_node(hgx_ctx *ctx, int it) {
   HGX_TRY(launch_half(ctx, MODE_FULL, ctx->row0, ctx->row1 - ctx->row0,
                       ctx->rp_n.as<int>(), ctx->col_n.as<int>(), xc, yc, xn,
                       prev, prev != nullptr, cur, ctx->avg_deg_n,
-                      ctx->blk_sn.as<int>(), ctx->nblk_sn));
+                      ctx->blk_sn.as<int>(), ctx->nblk_sn, &ctx->long_sn));
   return HGX_OK;
 }
 
@@ -991,7 +1180,7 @@ extern "C" int hgx_alg_shard_edge_partial(hgx_ctx *ctx, int it) {
   HGX_TRY(launch_half(ctx, MODE_PARTIAL, 0, ctx->E, ctx->rp_el.as<int>(),
                       ctx->col_el.as<int>(), nullptr, xn, ctx->ext_partial,
                       nullptr, 0, nullptr, avg, ctx->blk_el.as<int>(),
-                      ctx->nblk_el));
+                      ctx->nblk_el, &ctx->long_el));
   return HGX_OK;
 }
 

@@ -80,6 +80,8 @@ extern "C" int hgx_destroy(hgx_ctx *ctx) {
                     &ctx->nacc, &ctx->eacc, &ctx->s0, &ctx->s1, &ctx->s2,
                     &ctx->s3, &ctx->s4, &ctx->s5, &ctx->s6, &ctx->s7};
   for (DevBuf *b : bufs) hgx_release(*b);
+  for (LongRows *l : {&ctx->long_n, &ctx->long_e, &ctx->long_sn, &ctx->long_el})
+    for (DevBuf *b : {&l->seg, &l->off, &l->rows, &l->part}) hgx_release(*b);
   if (ctx->ev0) hipEventDestroy(ctx->ev0);
   if (ctx->ev1) hipEventDestroy(ctx->ev1);
   if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
@@ -152,6 +154,8 @@ extern "C" int hgx_upload_incidence(hgx_ctx *ctx, int32_t N, int32_t E,
   }
   HGX_TRY(hgx_make_row_blocks(ctx, rowptr_n, 0, N, ctx->blk_n, ctx->nblk_n));
   HGX_TRY(hgx_make_row_blocks(ctx, rowptr_e, 0, E, ctx->blk_e, ctx->nblk_e));
+  HGX_TRY(hgx_make_long_rows(ctx, rowptr_n, 0, N, ctx->long_n));
+  HGX_TRY(hgx_make_long_rows(ctx, rowptr_e, 0, E, ctx->long_e));
   int32_t mn = 0, me = 0;
   for (int32_t r = 0; r < N; r++) mn = std::max(mn, rowptr_n[r + 1] - rowptr_n[r]);
   for (int32_t r = 0; r < E; r++) me = std::max(me, rowptr_e[r + 1] - rowptr_e[r]);
@@ -191,6 +195,42 @@ int hgx_make_row_blocks(hgx_ctx *ctx, const int32_t *rp, int32_t r0, int32_t r1,
   if (nblk < 0) nblk = 0;
   HGX_TRY(hgx_ensure(ctx, blk, sizeof(int32_t) * b.size()));
   HGX_HIP(ctx, hipMemcpy(blk.p, b.data(), sizeof(int32_t) * b.size(),
+                         hipMemcpyHostToDevice));
+  return HGX_OK;
+}
+
+int hgx_make_long_rows(hgx_ctx *ctx, const int32_t *rp, int32_t r0, int32_t r1,
+                       LongRows &out) {
+  static const int thresh = [] {
+    const char *e = getenv("HGX_ALG_LONG");  // diagnostic / tuning
+    const int v = e ? atoi(e) : 0;
+    return v >= 64 ? v : kLongRow;
+  }();
+  std::vector<int32_t> rows, off(1, 0);
+  std::vector<int32_t> seg;  // pairs {row, piece}
+  for (int32_t r = r0; r < r1; r++) {
+    const int64_t len = rp[r + 1] - rp[r];
+    if (len <= thresh) continue;
+    const int pieces = (int)((len + thresh - 1) / thresh);
+    rows.push_back(r);
+    for (int p = 0; p < pieces; p++) {
+      seg.push_back(r);
+      seg.push_back(p);
+    }
+    off.push_back(off.back() + pieces);
+  }
+  out.thresh = thresh;
+  out.nlong = (int)rows.size();
+  out.nseg = off.back();
+  if (out.nlong == 0) return HGX_OK;
+  HGX_TRY(hgx_ensure(ctx, out.rows, sizeof(int32_t) * rows.size()));
+  HGX_TRY(hgx_ensure(ctx, out.off, sizeof(int32_t) * off.size()));
+  HGX_TRY(hgx_ensure(ctx, out.seg, sizeof(int32_t) * seg.size()));
+  HGX_HIP(ctx, hipMemcpy(out.rows.p, rows.data(), sizeof(int32_t) * rows.size(),
+                         hipMemcpyHostToDevice));
+  HGX_HIP(ctx, hipMemcpy(out.off.p, off.data(), sizeof(int32_t) * off.size(),
+                         hipMemcpyHostToDevice));
+  HGX_HIP(ctx, hipMemcpy(out.seg.p, seg.data(), sizeof(int32_t) * seg.size(),
                          hipMemcpyHostToDevice));
   return HGX_OK;
 }

@@ -17,6 +17,20 @@ struct DevBuf {
   template <class T> T *as() const { return reinterpret_cast<T *>(p); }
 };
 
+// Rows longer than `thresh` incidences, split into pieces of `thresh`: the
+// alg-dist half sweep reduces each piece on its own wave (seg_partial) and
+// finishes the row from the piece partials (long_finish); the narrow kernel
+// skips them. Without this one power-law edge (~2% of all incidences at C4)
+// would sit on a single lane group for the whole sweep.
+struct LongRows {
+  DevBuf seg;   // int2 {row, piece} per piece
+  DevBuf off;   // nlong + 1: first piece of each long row
+  DevBuf rows;  // nlong long-row ids
+  DevBuf part;  // nseg x ks float partials [sum w, sum w*src]
+  int nlong = 0, nseg = 0, thresh = 0;
+};
+constexpr int kLongRow = 512;
+
 struct hgx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;      // stream every launch goes to
@@ -31,6 +45,7 @@ struct hgx_ctx {
   // row is a block of its own): row starts, nblk + 1 entries
   DevBuf blk_n, blk_e;
   int nblk_n = 0, nblk_e = 0;
+  LongRows long_n, long_e;
   double avg_deg_n = 0, avg_deg_e = 0;
   int32_t max_deg_n = 0, max_deg_e = 0;
 
@@ -44,6 +59,7 @@ struct hgx_ctx {
   int32_t row0 = 0, row1 = 0;
   DevBuf rp_el, col_el, blk_sn, blk_el;
   int nblk_sn = 0, nblk_el = 0;
+  LongRows long_sn, long_el;
   float *ext_partial = nullptr;  // E x ks
   int *ext_mm = nullptr;         // iters x 2 x ks
   int ext_iters = 0;
@@ -70,6 +86,9 @@ int hgx_fail(hgx_ctx *ctx, int code, const char *fmt, ...);
 // alg-dist row-block partition of rows [r0, r1) of a CSR (host side)
 int hgx_make_row_blocks(hgx_ctx *ctx, const int32_t *rp, int32_t r0, int32_t r1,
                         DevBuf &blk, int &nblk);
+// long rows of rows [r0, r1) of a CSR (host side)
+int hgx_make_long_rows(hgx_ctx *ctx, const int32_t *rp, int32_t r0, int32_t r1,
+                       LongRows &out);
 int hgx_ensure(hgx_ctx *ctx, DevBuf &b, size_t bytes);
 void hgx_release(DevBuf &b);
 

@@ -4,7 +4,8 @@
   1 + Poisson(19) (mean 20); each node's edges drawn uniformly without
   duplicates; nnz ~ 2.0e6, mean edge size ~ 40.
 * powerlaw (C4/C5): N=10 000 000, E=5 000 000; node degree 1 + Poisson(19);
-  edge choice proportional to rank^-0.8 (Zipf-like edge sizes).
+  edge choice proportional to rank^-0.8 (Zipf-like edge sizes). Built by
+  libhgx's host generator (numpy sorts of 2e8 keys take minutes).
 
 Both return an :class:`Incidence` directly (no proto: a 2e8-incidence proto
 is beyond Python protobuf). Edges that receive no node are dropped, so every
@@ -60,16 +61,13 @@ def random_hypergraph(N=100_000, E=50_000, mean_degree=20, seed=0):
 
 def powerlaw_hypergraph(N=10_000_000, E=5_000_000, mean_degree=20,
                         exponent=0.8, seed=0):
-  rng = np.random.default_rng(seed)
-  deg = 1 + rng.poisson(mean_degree - 1, N)
-  rows = np.repeat(np.arange(N, dtype=np.int64), deg)
-  w = np.arange(1, E + 1, dtype=np.float64) ** (-exponent)
-  cdf = np.cumsum(w)
-  cdf /= cdf[-1]
-  draw = lambda n, r: np.minimum(np.searchsorted(cdf, r.random(n)), E - 1)
-  cols = draw(rows.size, rng)
-  rows, cols = _dedup_rows(rows, cols, E, draw, rng)
-  return _finish(N, E, rows, cols)
+  """C4/C5 shape, generated natively (libhgx hgx_synth_powerlaw: alias-table
+  Zipf draws, counting-sort transpose; ~2e8 incidences in seconds)."""
+  from . import _hgx
+  rp_n, col_n, E_kept = _hgx.synth_powerlaw(N, E, float(mean_degree),
+                                           float(exponent), seed)
+  rp_e, col_e = _hgx.csr_transpose(N, E_kept, rp_n, col_n)
+  return Incidence(N, E_kept, rp_n, col_n, rp_e, col_e)
 
 
 CONFIGS = {

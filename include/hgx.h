@@ -157,6 +157,20 @@ int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr, float eps,
 int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
                          int64_t *batches);
 
+/* ---- host utilities (bench / test data; not reference entry points) --- *
+ * Power-law synthetic incidence of SURVEY.md §8(d) (C4/C5): node degree
+ * 1 + Poisson(mean_degree - 1), distinct edges per node drawn with
+ * probability proportional to rank^-exponent; edges no node picked are
+ * dropped and the rest renumbered (*E_out). Call with col_n == NULL to get
+ * rowptr_n (N+1) and *nnz, then again with col_n (nnz) to fill the sorted
+ * columns. Deterministic for `seed`. No context, no device. */
+int hgx_synth_powerlaw(int32_t N, int32_t E, double mean_degree,
+                       double exponent, uint64_t seed, int32_t *rowptr_n,
+                       int32_t *col_n, int64_t *nnz, int32_t *E_out);
+/* CSR transpose by counting sort (rows of the result sorted). */
+int hgx_csr_transpose(int32_t nrow, int32_t ncol, const int32_t *rowptr,
+                      const int32_t *col, int32_t *rowptr_t, int32_t *col_t);
+
 #ifdef __cplusplus
 }
 #endif

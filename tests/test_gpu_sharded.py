@@ -25,20 +25,28 @@ def _free_port():
   return p
 
 
-def _worker(rank, world, port, out_path, iters):
+def _graph(name):
+  if name == "tiny":
+    from conftest import golden_incidence as gi
+    return gi("csr_tiny.npz")
+  from hypergraphembedding_amd.synthetic import powerlaw_hypergraph
+  return powerlaw_hypergraph(N=20_000, E=10_000, seed=5)  # long edge rows
+
+
+def _worker(rank, world, port, out_path, iters, graph="tiny"):
   import torch
   import torch.distributed as dist
   import sys
   root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
   sys.path[:0] = [root, os.path.join(root, "oracle"), os.path.join(root, "tests")]
-  from conftest import golden_incidence as gi
+  from test_gpu_sharded import _graph
   from hypergraphembedding_amd import _hgx
   from hypergraphembedding_amd.algebraic_distance import alg_dist_sharded
   os.environ["MASTER_ADDR"] = "127.0.0.1"
   os.environ["MASTER_PORT"] = str(port)
   dist.init_process_group("gloo", rank=rank, world_size=world)
   torch.cuda.set_device(0)
-  inc = gi("csr_tiny.npz")
+  inc = _graph(graph)
   r = O.Rng(0)
   x0, y0 = r.random((inc.N, 10)), r.random((inc.E, 10))
   ctx = _hgx.Context(0)
@@ -67,3 +75,22 @@ def test_sharded_algdist_matches_reference(tmp_path, world):
     assert np.array_equal(y, ys[0])  # edge coords replicated identically
   assert np.abs(x - z["x_20"]).max() <= 1e-4
   assert np.abs(ys[0] - z["y_20"]).max() <= 1e-4
+
+
+def test_sharded_algdist_powerlaw_long_rows(tmp_path):
+  import torch.multiprocessing as mp
+  world, iters = 2, 10
+  out = str(tmp_path / "shard")
+  mp.start_processes(_worker, args=(world, _free_port(), out, iters, "powerlaw"),
+                     nprocs=world, join=True, start_method="spawn")
+  inc = _graph("powerlaw")
+  r = O.Rng(0)
+  x0, y0 = r.random((inc.N, 10)), r.random((inc.E, 10))
+  xr, yr = O.algdist(inc, x0, y0, iters)
+  x = np.zeros((inc.N, 10), np.float32)
+  for rk in range(world):
+    d = np.load(out + f".{rk}.npz")
+    x[int(d["r0"]):int(d["r1"])] = d["x"]
+    y = d["y"]
+  assert np.abs(x - xr).max() <= 1e-4
+  assert np.abs(y - yr).max() <= 1e-4
