@@ -229,6 +229,16 @@ def main():
           "gbps": round(gbps4, 1), "bytes_per_iter": b_iter4,
           "frac_of_hbm_peak": round(gbps4 / HBM_PEAK_GBPS, 4),
           "sharded": world > 1, "graph_gen_s": round(c4_gen, 1)}
+    # 128-B line traffic of the same kernels from the committed PMC run
+    # (TCC_MISS x 128 B; random gathers move whole lines, tools/
+    # gather_granularity.hip), against this run's time
+    prof = os.path.join(ROOT, "profiles", "r01_pmc_algdist_c4.json")
+    if os.path.exists(prof) and world == 1:
+      with open(prof) as f:
+        kern = json.load(f)["kernels"]
+      lines = sum(v.get("TCC_MISS_sum", 0.0) for v in kern.values()) * 128.0
+      c4["l2_miss_line_bytes_per_iter"] = lines
+      c4["line_gbps"] = round(lines / (ms4 / args.alg_iters * 1e-3) / 1e9, 1)
     del big, bx0, by0
 
   if rank == 0:

@@ -1,6 +1,6 @@
 """Trainer timing experiments: one process, variants selected through the
 diagnostic env knobs read by each hgx_train call (HGX_TRAIN_ABLATE,
-HGX_TRAIN_TB1, HGX_NO_GRAPH). Prints us/batch per variant."""
+HGX_TRAIN_TB1, HGX_GRAPH). Prints us/batch per variant."""
 import os, sys, time
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -25,12 +25,12 @@ tgt[np.arange(n), kind] = rs.uniform(0, 1, n)
 ctx = _hgx.Context(0)
 ctx.records_set(idx, tgt)
 ctx.model_init(d, N + 2, E + 2, seed=1)
-ENV = {"base": {}, "tb64": {"HGX_TRAIN_TB1": "64"}, "nograph": {"HGX_NO_GRAPH": "1"}}
+ENV = {"base": {}, "tb64": {"HGX_TRAIN_TB1": "64"}, "graph": {"HGX_GRAPH": "1"}}
 for b in (1, 2, 3, 4, 8, 16, 32, 4 | 8, 16 | 32, 4 | 8 | 16 | 32):
   ENV[f"ab{b}"] = {"HGX_TRAIN_ABLATE": str(b)}
 for v in variants:
   env = ENV[v] if v in ENV else dict(kv.split("=") for kv in v.split("+"))
-  for k in ("HGX_TRAIN_ABLATE", "HGX_TRAIN_TB1", "HGX_NO_GRAPH",
+  for k in ("HGX_TRAIN_ABLATE", "HGX_TRAIN_TB1", "HGX_GRAPH",
             "HGX_TRAIN_SERIAL", "HGX_TRAIN_G2"):
     os.environ.pop(k, None)
   os.environ.update(env)

@@ -1,0 +1,48 @@
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
+tools/perf_train.py into profiles/<round>_pmc_train.json: HBM bytes per
+batch step (train_fwd_bwd + train_update), gfx950 FETCH correction x2
+(MI355X_MICROARCH.md, HBM section). Usage:
+  python tools/pmc_train_summary.py FETCH_CSV WRITE_CSV OUT_JSON d"""
+import csv, json, sys
+import numpy as np
+
+fetch_csv, write_csv, out, d = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+
+
+def per_kernel(path, counter):
+  vals = {}
+  for r in csv.DictReader(open(path)):
+    if r["Counter_Name"] != counter:
+      continue
+    name = r["Kernel_Name"]
+    for key in ("train_fwd_bwd", "train_update"):
+      if key in name:
+        vals.setdefault(key, []).append(float(r["Counter_Value"]))
+  return {k: float(np.mean(v)) for k, v in vals.items()}, \
+      {k: len(v) for k, v in vals.items()}
+
+
+f, nf = per_kernel(fetch_csv, "FETCH_SIZE")
+w, nw = per_kernel(write_csv, "WRITE_SIZE")
+hbm = 1024 * (2 * sum(f.values()) + sum(w.values()))
+alg = 256 * (224 * d + 68)
+res = {
+    "round": 1,
+    "command": ("rocprofv3 --pmc FETCH_SIZE (pass 1) / "
+                "--pmc WRITE_SIZE (pass 2) --output-format csv -- python "
+                f"tools/perf_train.py {d} 400000"),
+    "note": ("Per batch of 256 records at d=%d on 100k/50k-row tables, summed over "
+             "the two per-batch kernels, mean over all launches. FETCH_SIZE / "
+             "WRITE_SIZE are KB; gfx950 correction: FETCH doubled (wide 16-B-per-"
+             "lane reads are tallied at half), WRITE as is. Infinity-Cache hits "
+             "are counted by these counters. Collected on the trainer-only script "
+             "(same kernels and shapes as bench.py; --pmc on the full bench.py "
+             "crashed inside the profiler in round 1)." % d),
+    "launches": {"fetch": nf, "write": nw},
+    "fetch_kb_per_batch": f,
+    "write_kb_per_batch": w,
+    "hbm_bytes_per_batch": int(round(hbm)),
+    "algorithmic_bytes_per_batch": alg,
+}
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res, indent=1))
