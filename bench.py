@@ -52,6 +52,11 @@ def parse():
   p.add_argument("--no-cpu", action="store_true")
   p.add_argument("--no-c4", action="store_true",
                  help="skip the power-law 10M/5M alg-dist measurement")
+  p.add_argument("--dist-backend", default="nccl",
+                 help="torch.distributed backend for --gpus > 1 (nccl = RCCL; "
+                      "gloo only to rehearse several ranks on one GPU)")
+  p.add_argument("--one-device", action="store_true",
+                 help="every rank uses GPU 0 (rehearsal on a 1-GPU box)")
   return p.parse_args()
 
 
@@ -61,12 +66,17 @@ def main():
   rank = int(os.environ.get("RANK", "0"))
   local = int(os.environ.get("LOCAL_RANK", "0"))
   dist = None
+  if args.one_device:
+    local = 0
   if world > 1:
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.dist_backend == "nccl":
+      dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+      dist.init_process_group(args.dist_backend)
 
   def barrier():
     if dist is not None:
@@ -263,8 +273,9 @@ def main():
             "records_per_epoch": n, "batch": args.batch, "dim": args.dim,
             "num_neighbors": args.num_neighbors,
             "num_samples": args.num_samples,
-            "parallelism": ("replicas (training), node-row sharded + RCCL "
-                            "all-reduce (alg-dist)" if world > 1 else
+            "parallelism": (f"replicas (training), node-row sharded + "
+                            f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend}"
+                            f" all-reduce (alg-dist)" if world > 1 else
                             "single GPU"),
         },
         "algdist": {"k": k, "iters": args.alg_iters,

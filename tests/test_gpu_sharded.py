@@ -94,3 +94,40 @@ def test_sharded_algdist_powerlaw_long_rows(tmp_path):
     y = d["y"]
   assert np.abs(x - xr).max() <= 1e-4
   assert np.abs(y - yr).max() <= 1e-4
+
+
+def _nccl_worker(rank, world, port, out_path):
+  import torch
+  import torch.distributed as dist
+  import sys
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  sys.path[:0] = [root, os.path.join(root, "oracle"), os.path.join(root, "tests")]
+  from test_gpu_sharded import _graph
+  from hypergraphembedding_amd import _hgx
+  from hypergraphembedding_amd.algebraic_distance import alg_dist_sharded
+  os.environ["MASTER_ADDR"] = "127.0.0.1"
+  os.environ["MASTER_PORT"] = str(port)
+  torch.cuda.set_device(0)
+  dist.init_process_group("nccl", rank=rank, world_size=world,
+                          device_id=torch.device("cuda", 0))
+  inc = _graph("tiny")
+  r = O.Rng(0)
+  x0, y0 = r.random((inc.N, 10)), r.random((inc.E, 10))
+  ctx = _hgx.Context(0)
+  (r0, r1, xo), y, ms = alg_dist_sharded(ctx, inc, x0, y0, 20)
+  np.savez(out_path, r0=r0, r1=r1, x=xo, y=y)
+  dist.destroy_process_group()
+
+
+def test_sharded_algdist_rccl_single_rank(tmp_path):
+  """The bench's RCCL path (nccl backend, collectives on the shared torch
+  stream) with one rank: the only RCCL configuration a 1-GPU box can run."""
+  import torch.multiprocessing as mp
+  out = str(tmp_path / "nccl.npz")
+  mp.start_processes(_nccl_worker, args=(1, _free_port(), out), nprocs=1,
+                     join=True, start_method="spawn")
+  z = golden("algdist_tiny.npz")
+  d = np.load(out)
+  assert int(d["r0"]) == 0 and int(d["r1"]) == d["x"].shape[0]
+  assert np.abs(d["x"] - z["x_20"]).max() <= 1e-4
+  assert np.abs(d["y"] - z["y_20"]).max() <= 1e-4
