@@ -1,0 +1,111 @@
+"""Parity at BASELINE.json's single-GPU size (C3: random 100k nodes / 50k
+edges, nnz 2.0e6), through checks whose cost does not grow with the stream:
+  * alg-dist, 20 iterations, against the float64 oracle (max-abs 1e-4);
+  * HOBE stream: exact per-row counts min(S, |pattern row|) and pair
+    validity on a random sample of rows, total count = the sum over all rows;
+  * trainer: bitwise determinism of a full epoch (same init, same shuffle
+    seed -> identical tables) and a decreasing epoch loss.
+"""
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c3():
+  from hypergraphembedding_amd.synthetic import random_hypergraph
+  return random_hypergraph(seed=0)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+  from hypergraphembedding_amd import _hgx
+  c = _hgx.Context(0)
+  yield c
+  c.close()
+
+
+def _coords(inc, k=10):
+  r = O.Rng(7)
+  return r.random((inc.N, k)), r.random((inc.E, k))
+
+
+def test_c3_algdist_vs_oracle(ctx, c3):
+  x0, y0 = _coords(c3)
+  xr, yr = O.algdist(c3, x0, y0, 20)
+  ctx.upload(c3)
+  x, y = ctx.alg_dist(x0, y0, 20)
+  assert np.abs(x - xr).max() <= 1e-4
+  assert np.abs(y - yr).max() <= 1e-4
+
+
+def _two_hop(rp_a, col_a, rp_b, col_b, r):
+  """columns of row r of (A B) as a set (A, B in CSR)."""
+  mids = col_a[rp_a[r]:rp_a[r + 1]]
+  return np.unique(np.concatenate([col_b[rp_b[m]:rp_b[m + 1]] for m in mids]))
+
+
+def test_c3_hobe_stream_counts_and_pairs(ctx, c3):
+  inc, S, K = c3, 200, 5
+  ctx.upload(inc)
+  x0, y0 = _coords(inc)
+  ctx.alg_set(x0, y0)
+  ctx.alg_run(20)
+  n = ctx.sample_hobe(99, K, S)
+  idx, tgt = ctx.records_get()
+  assert idx.shape == (n, 4 + 2 * K)
+  ln, le, rn, re = (idx[:, i] for i in range(4))
+  nn = (ln > 0) & (rn > 0)
+  ee = (le > 0) & (re > 0)
+  ne = (ln > 0) & (re > 0) & (rn == 0)
+  assert int(nn.sum() + ee.sum() + ne.sum()) == n  # every record one kind
+  cnt_nn = np.bincount(ln[nn] - 1, minlength=inc.N)
+  cnt_ee = np.bincount(le[ee] - 1, minlength=inc.E)
+  rs = np.random.RandomState(0)
+  for v in rs.choice(inc.N, 64, replace=False):
+    row = _two_hop(inc.rp_n, inc.col_n, inc.rp_e, inc.col_e, v)  # A A^T
+    assert cnt_nn[v] == min(S, row.size)
+    got = rn[nn][ln[nn] - 1 == v] - 1
+    assert np.unique(got).size == got.size and np.isin(got, row).all()
+  for e in rs.choice(inc.E, 64, replace=False):
+    row = _two_hop(inc.rp_e, inc.col_e, inc.rp_n, inc.col_n, e)  # A^T A
+    assert cnt_ee[e] == min(S, row.size)
+    got = re[ee][le[ee] - 1 == e] - 1
+    assert np.unique(got).size == got.size and np.isin(got, row).all()
+  # probabilities are in [0, 1]; the targets not of a record's kind are 0
+  assert tgt.min() >= 0 and tgt.max() <= 1
+  assert np.all(tgt[nn, 1:] == 0) and np.all(tgt[ee][:, [0, 2]] == 0)
+  # neighbours: nn_k in N(e = re), ne_k in E(v = ln)
+  sel = np.flatnonzero(ne)[rs.choice(int(ne.sum()), 2000, replace=False)]
+  for i in sel:
+    v, e = ln[i] - 1, re[i] - 1
+    nodes_e = inc.col_e[inc.rp_e[e]:inc.rp_e[e + 1]]
+    edges_v = inc.col_n[inc.rp_n[v]:inc.rp_n[v + 1]]
+    assert np.isin(idx[i, 4:4 + K] - 1, nodes_e).all()
+    assert np.isin(idx[i, 4 + K:] - 1, edges_v).all()
+
+
+def test_c3_trainer_deterministic_and_learning(ctx, c3):
+  from hypergraphembedding_amd import _hgx
+  inc = c3
+  ctx.upload(inc)
+  x0, y0 = _coords(inc)
+  ctx.alg_set(x0, y0)
+  ctx.alg_run(20)
+  ctx.sample_hobe(5, 5, 200)
+  tabs = []
+  for _ in range(2):
+    ctx.model_init(128, inc.N + 1, inc.E + 1, seed=3)
+    ctx.train(batch=256, max_epochs=1, loss=_hgx.LOSS_MSE, act=_hgx.ACT_RELU,
+              min_delta=-1e30, shuffle_seed=11)
+    tabs.append(ctx.model_get())
+  assert np.array_equal(tabs[0][0], tabs[1][0])
+  assert np.array_equal(tabs[0][1], tabs[1][1])
+  ctx.model_init(128, inc.N + 1, inc.E + 1, seed=3)
+  losses = ctx.train(batch=256, max_epochs=3, loss=_hgx.LOSS_MSE,
+                     act=_hgx.ACT_RELU, min_delta=-1e30, shuffle_seed=11)
+  assert len(losses) == 3 and losses[2] < losses[1] < losses[0]
