@@ -23,6 +23,7 @@ from .hg2v_sample import (AlgebraicDistanceSamples, BooleanSamples,
 from .hg2v_weighting import UniformWeight, WeightByNeighborhood
 from .hg2v_model import (BooleanModel, KerasModelToEmbedding,
                          UnweightedFloatModel)
+from .proto_native import read_incidence, write_embedding
 from .embedding import (COMBINATION_OPTIONS, DEBUG_SUMMARY_OPTIONS,
                         EMBEDDING_OPTIONS, CombineEmbeddings, Embed,
                         EmbedHg2vAlgDist, EmbedHg2vBoolean)
@@ -43,4 +44,6 @@ __all__ = [
     "AddNodeToEdge", "RemoveNodeFromEdge", "RemoveNode", "RemoveEdge",
     "CreateRandomHyperGraph", "FromSparseMatrix", "IsEmpty", "ToCsrMatrix",
     "ToEdgeCsrMatrix", "ToCscMatrix", "Relabel", "CompressRange", "Incidence",
+    # native proto I/O
+    "read_incidence", "write_embedding",
 ]

@@ -67,6 +67,14 @@ SIGNATURES = {
                                   _u64, _vp, _vp, _pi64,
                                   ctypes.POINTER(ctypes.c_int32)]),
     "hgx_csr_transpose": (_int, [_i32, _i32, _vp, _vp, _vp, _vp]),
+    "hgx_proto_parse_hypergraph": (_int, [_vp, _i64, ctypes.POINTER(_vp),
+                                          ctypes.POINTER(_i32),
+                                          ctypes.POINTER(_i32), _pi64]),
+    "hgx_proto_hypergraph_fill": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "hgx_proto_hypergraph_free": (None, [_vp]),
+    "hgx_proto_write_embedding": (_int, [_i64, _vp, _vp, _i64, _vp, _vp, _int,
+                                         ctypes.c_char_p, _vp, _i64, _pi64]),
+    "hgx_host_last_error": (ctypes.c_char_p, []),
 }
 
 
@@ -324,3 +332,60 @@ def csr_transpose(nrow, ncol, rp, col):
   if rc != HGX_OK:
     _raise(rc, "hgx_csr_transpose: column index out of range")
   return rpt, colt
+
+
+def _host_raise(rc):
+  _raise(rc, lib().hgx_host_last_error().decode(errors="replace"))
+
+
+def parse_hypergraph(buf):
+  """Serialized Hypergraph bytes (bytes / memoryview / uint8 array) ->
+  dict of compressed-incidence arrays (hgx_proto_parse_hypergraph)."""
+  a = np.frombuffer(buf, dtype=np.uint8)
+  h = _vp()
+  n, e, nnz = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+  rc = lib().hgx_proto_parse_hypergraph(_ptr(a) if a.size else None, a.size,
+                                        ctypes.byref(h), ctypes.byref(n),
+                                        ctypes.byref(e), ctypes.byref(nnz))
+  if rc != HGX_OK:
+    _host_raise(rc)
+  try:
+    out = {"N": n.value, "E": e.value,
+           "rp_n": np.empty(n.value + 1, np.int32),
+           "col_n": np.empty(nnz.value, np.int32),
+           "node_ids": np.empty(n.value, np.int64),
+           "edge_ids": np.empty(e.value, np.int64),
+           "node_weight": np.empty(n.value, np.float32),
+           "edge_weight": np.empty(e.value, np.float32)}
+    rc = lib().hgx_proto_hypergraph_fill(
+        h, _ptr(out["rp_n"]), _ptr(out["col_n"]), _ptr(out["node_ids"]),
+        _ptr(out["edge_ids"]), _ptr(out["node_weight"]),
+        _ptr(out["edge_weight"]))
+    if rc != HGX_OK:
+      _host_raise(rc)
+  finally:
+    lib().hgx_proto_hypergraph_free(h)
+  return out
+
+
+def write_embedding_bytes(node_ids, node_tab, edge_ids, edge_tab, method_name):
+  """HypergraphEmbedding wire bytes (hgx_proto_write_embedding)."""
+  node_ids = _c(node_ids, np.int64)
+  edge_ids = _c(edge_ids, np.int64)
+  node_tab = _c(node_tab, np.float32)
+  edge_tab = _c(edge_tab, np.float32)
+  d = int(node_tab.shape[1]) if node_tab.ndim == 2 else int(edge_tab.shape[1])
+  assert node_tab.shape == (node_ids.size, d) and edge_tab.shape == (edge_ids.size, d)
+  name = None if method_name is None else method_name.encode()
+  ln = ctypes.c_int64()
+  args = (node_ids.size, _ptr(node_ids), _ptr(node_tab), edge_ids.size,
+          _ptr(edge_ids), _ptr(edge_tab), d, name)
+  rc = lib().hgx_proto_write_embedding(*args, None, 0, ctypes.byref(ln))
+  if rc != HGX_OK:
+    _host_raise(rc)
+  out = np.empty(ln.value, np.uint8)
+  rc = lib().hgx_proto_write_embedding(*args, _ptr(out), out.size,
+                                       ctypes.byref(ln))
+  if rc != HGX_OK:
+    _host_raise(rc)
+  return out

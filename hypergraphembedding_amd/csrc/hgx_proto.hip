@@ -1,0 +1,336 @@
+// Native hypergraph.proto wire-format reader and HypergraphEmbedding writer
+// (SURVEY.md §8f rank 1). Host code only.
+//
+// Reader: a serialized `Hypergraph` (hypergraph.proto:6-23) goes straight to
+// the compressed incidence that Incidence.from_hypergraph builds from the
+// parsed message. That is CompressRange (hypergraph_util.py:223-244:
+// sorted keys -> 0..n-1) over the union of every node's `edges` list
+// (Relabel, hypergraph_util.py:208-212), with duplicates dropped, plus the
+// float weights (default 1). Map semantics follow protobuf: a repeated key
+// keeps its last entry; `edges` may be packed or not; unknown fields are
+// skipped. Python protobuf needs minutes for the 2e8-incidence C4 graph and
+// refuses messages over 2 GiB. This needs one pass and a sort.
+//
+// Writer: a `HypergraphEmbedding` (hypergraph.proto:26-35) from the device
+// tables, keyed by the original ids, entries in ascending key order.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "hgx.h"
+
+namespace {
+
+thread_local std::string g_host_err;
+
+int host_fail(int code, const std::string &msg) {
+  g_host_err = msg;
+  return code;
+}
+
+struct Reader {
+  const uint8_t *p, *end;
+  bool ok = true;
+  uint64_t varint() {
+    uint64_t v = 0;
+    for (int s = 0; s < 64 && p < end; s += 7) {
+      const uint8_t b = *p++;
+      v |= (uint64_t)(b & 0x7f) << s;
+      if (!(b & 0x80)) return v;
+    }
+    ok = false;
+    return 0;
+  }
+  uint32_t fixed32() {
+    if (end - p < 4) {
+      ok = false;
+      return 0;
+    }
+    uint32_t v;
+    memcpy(&v, p, 4);
+    p += 4;
+    return v;
+  }
+  // returns the sub-range of a length-delimited field
+  Reader sub() {
+    const uint64_t n = varint();
+    Reader r{p, p};
+    if (!ok || n > (uint64_t)(end - p)) {
+      ok = false;
+      return r;
+    }
+    r.end = p + n;
+    p += n;
+    return r;
+  }
+  void skip(int wt) {
+    switch (wt) {
+      case 0: varint(); break;
+      case 1:
+        if (end - p < 8) ok = false;
+        else p += 8;
+        break;
+      case 2: sub(); break;
+      case 5: fixed32(); break;
+      default: ok = false;
+    }
+  }
+};
+
+struct NodeRec {
+  int32_t key;
+  float weight;
+  int64_t off;  // into the edge-id pool
+  int32_t cnt;
+};
+
+}  // namespace
+
+struct hgx_hg {
+  int32_t N = 0, E = 0;
+  int64_t nnz = 0;
+  std::vector<int32_t> rp_n, col_n;
+  std::vector<int64_t> node_ids, edge_ids;
+  std::vector<float> node_w, edge_w;
+};
+
+extern "C" const char *hgx_host_last_error(void) { return g_host_err.c_str(); }
+
+extern "C" int hgx_proto_parse_hypergraph(const uint8_t *buf, int64_t len,
+                                          hgx_hg **out, int32_t *N, int32_t *E,
+                                          int64_t *nnz) {
+  if (!out || (len > 0 && !buf) || len < 0)
+    return host_fail(HGX_EINVAL, "null buffer or handle");
+  *out = nullptr;
+  std::vector<NodeRec> nodes;
+  std::vector<int32_t> pool;
+  std::vector<std::pair<int32_t, float>> edges;  // (key, weight)
+  Reader r{buf, buf + len};
+  while (r.ok && r.p < r.end) {
+    const uint64_t tag = r.varint();
+    const int field = (int)(tag >> 3), wt = (int)(tag & 7);
+    if ((field == 1 || field == 2) && wt == 2) {
+      Reader e = r.sub();
+      int32_t key = 0;
+      float weight = 1.0f;
+      const int64_t off = (int64_t)pool.size();
+      while (e.ok && e.p < e.end) {
+        const uint64_t t = e.varint();
+        const int f = (int)(t >> 3), w = (int)(t & 7);
+        if (f == 1 && w == 0) {
+          key = (int32_t)e.varint();
+        } else if (f == 2 && w == 2) {  // NodeData / EdgeData
+          Reader v = e.sub();  // a repeated value field merges into the first
+          while (v.ok && v.p < v.end) {
+            const uint64_t tv = v.varint();
+            const int fv = (int)(tv >> 3), wv = (int)(tv & 7);
+            if (fv == 1 && wv == 0) {
+              const int32_t x = (int32_t)v.varint();
+              if (field == 1) pool.push_back(x);
+            } else if (fv == 1 && wv == 2) {  // packed
+              Reader pk = v.sub();
+              while (pk.ok && pk.p < pk.end) {
+                const int32_t x = (int32_t)pk.varint();
+                if (field == 1) pool.push_back(x);
+              }
+              if (!pk.ok) v.ok = false;
+            } else if (fv == 3 && wv == 5) {
+              const uint32_t bits = v.fixed32();
+              memcpy(&weight, &bits, 4);
+            } else {
+              v.skip(wv);
+            }
+          }
+          if (!v.ok) e.ok = false;
+        } else {
+          e.skip(w);
+        }
+      }
+      if (!e.ok) r.ok = false;
+      if (field == 1)
+        nodes.push_back({key, weight, off, (int32_t)((int64_t)pool.size() - off)});
+      else
+        edges.push_back({key, weight});
+    } else {
+      r.skip(wt);
+    }
+  }
+  if (!r.ok) return host_fail(HGX_EINVAL, "malformed Hypergraph message");
+
+  // last entry per key wins (protobuf map semantics); stable order by key
+  auto keep_last = [](auto &v, auto key_of) {
+    std::vector<size_t> idx(v.size());
+    for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
+      return key_of(v[a]) < key_of(v[b]);
+    });
+    std::vector<typename std::decay<decltype(v)>::type::value_type> outv;
+    outv.reserve(idx.size());
+    for (size_t i = 0; i < idx.size(); i++) {
+      if (i + 1 < idx.size() && key_of(v[idx[i]]) == key_of(v[idx[i + 1]])) continue;
+      outv.push_back(v[idx[i]]);
+    }
+    v.swap(outv);
+  };
+  keep_last(nodes, [](const NodeRec &n) { return n.key; });
+  keep_last(edges, [](const std::pair<int32_t, float> &e) { return e.first; });
+
+  auto *h = new hgx_hg();
+  h->N = (int32_t)nodes.size();
+  h->E = (int32_t)edges.size();
+  h->node_ids.resize(h->N);
+  h->node_w.resize(h->N);
+  h->edge_ids.resize(h->E);
+  h->edge_w.resize(h->E);
+  std::vector<int32_t> ekeys(h->E);
+  for (int32_t i = 0; i < h->E; i++) {
+    ekeys[i] = edges[i].first;
+    h->edge_ids[i] = edges[i].first;
+    h->edge_w[i] = edges[i].second;
+  }
+  h->rp_n.assign((size_t)h->N + 1, 0);
+  h->col_n.reserve(pool.size());
+  std::vector<int32_t> row;
+  for (int32_t i = 0; i < h->N; i++) {
+    const NodeRec &n = nodes[i];
+    h->node_ids[i] = n.key;
+    h->node_w[i] = n.weight;
+    row.clear();
+    for (int32_t t = 0; t < n.cnt; t++) {
+      const int32_t key = pool[n.off + t];
+      auto it = std::lower_bound(ekeys.begin(), ekeys.end(), key);
+      if (it == ekeys.end() || *it != key) {
+        delete h;
+        return host_fail(HGX_EINVAL, "node " + std::to_string(n.key) +
+                                         " lists edge " + std::to_string(key) +
+                                         " missing from hypergraph.edge");
+      }
+      row.push_back((int32_t)(it - ekeys.begin()));
+    }
+    std::sort(row.begin(), row.end());
+    row.erase(std::unique(row.begin(), row.end()), row.end());
+    h->col_n.insert(h->col_n.end(), row.begin(), row.end());
+    if ((int64_t)h->col_n.size() >= INT32_MAX) {
+      delete h;
+      return host_fail(HGX_EUNSUP, "incidence count exceeds int32 CSR range");
+    }
+    h->rp_n[i + 1] = (int32_t)h->col_n.size();
+  }
+  h->nnz = (int64_t)h->col_n.size();
+  *out = h;
+  if (N) *N = h->N;
+  if (E) *E = h->E;
+  if (nnz) *nnz = h->nnz;
+  return HGX_OK;
+}
+
+extern "C" int hgx_proto_hypergraph_fill(const hgx_hg *h, int32_t *rowptr_n,
+                                         int32_t *col_n, int64_t *node_ids,
+                                         int64_t *edge_ids, float *node_weight,
+                                         float *edge_weight) {
+  if (!h) return host_fail(HGX_EINVAL, "null hypergraph handle");
+  if (rowptr_n) std::copy(h->rp_n.begin(), h->rp_n.end(), rowptr_n);
+  if (col_n) std::copy(h->col_n.begin(), h->col_n.end(), col_n);
+  if (node_ids) std::copy(h->node_ids.begin(), h->node_ids.end(), node_ids);
+  if (edge_ids) std::copy(h->edge_ids.begin(), h->edge_ids.end(), edge_ids);
+  if (node_weight) std::copy(h->node_w.begin(), h->node_w.end(), node_weight);
+  if (edge_weight) std::copy(h->edge_w.begin(), h->edge_w.end(), edge_weight);
+  return HGX_OK;
+}
+
+extern "C" void hgx_proto_hypergraph_free(hgx_hg *h) { delete h; }
+
+namespace {
+
+size_t varint_len(uint64_t v) {
+  size_t n = 1;
+  while (v >= 0x80) {
+    v >>= 7;
+    n++;
+  }
+  return n;
+}
+uint8_t *put_varint(uint8_t *p, uint64_t v) {
+  while (v >= 0x80) {
+    *p++ = (uint8_t)(v | 0x80);
+    v >>= 7;
+  }
+  *p++ = (uint8_t)v;
+  return p;
+}
+// int32 keys are varint-encoded as sign-extended 64-bit
+uint64_t key_bits(int64_t k) { return (uint64_t)(int64_t)(int32_t)k; }
+
+// one map<int32, Embedding> entry: key (field 1), value (field 2) =
+// Embedding{ repeated float values = 1 } unpacked (proto2 default)
+size_t entry_body_len(int64_t key, int d) {
+  const size_t emb = (size_t)d * 5;  // tag 0x0d + fixed32 per value
+  return 1 + varint_len(key_bits(key)) + 1 + varint_len(emb) + emb;
+}
+
+uint8_t *put_entry(uint8_t *p, int field, int64_t key, const float *v, int d) {
+  const size_t body = entry_body_len(key, d);
+  p = put_varint(p, (uint64_t)(field << 3 | 2));
+  p = put_varint(p, body);
+  *p++ = 0x08;  // key, varint
+  p = put_varint(p, key_bits(key));
+  *p++ = 0x12;  // value, length-delimited
+  p = put_varint(p, (size_t)d * 5);
+  for (int i = 0; i < d; i++) {
+    *p++ = 0x0d;
+    memcpy(p, v + i, 4);
+    p += 4;
+  }
+  return p;
+}
+
+}  // namespace
+
+extern "C" int hgx_proto_write_embedding(
+    int64_t n_nodes, const int64_t *node_ids, const float *node_tab,
+    int64_t n_edges, const int64_t *edge_ids, const float *edge_tab, int d,
+    const char *method_name, uint8_t *out, int64_t cap, int64_t *len) {
+  if (!len || d < 0 || n_nodes < 0 || n_edges < 0)
+    return host_fail(HGX_EINVAL, "bad embedding arguments");
+  if ((n_nodes && (!node_ids || !node_tab)) || (n_edges && (!edge_ids || !edge_tab)))
+    return host_fail(HGX_EINVAL, "null id or table buffer");
+  // ids in ascending order (deterministic serialisation)
+  auto order = [](int64_t n, const int64_t *ids) {
+    std::vector<int64_t> o(n);
+    for (int64_t i = 0; i < n; i++) o[i] = i;
+    std::sort(o.begin(), o.end(), [&](int64_t a, int64_t b) { return ids[a] < ids[b]; });
+    return o;
+  };
+  const std::vector<int64_t> on = order(n_nodes, node_ids), oe = order(n_edges, edge_ids);
+  size_t total = 0;
+  for (int64_t i = 0; i < n_nodes; i++) {
+    const size_t b = entry_body_len(node_ids[i], d);
+    total += 1 + varint_len(b) + b;
+  }
+  for (int64_t i = 0; i < n_edges; i++) {
+    const size_t b = entry_body_len(edge_ids[i], d);
+    total += 1 + varint_len(b) + b;
+  }
+  total += 1 + varint_len(key_bits(d));
+  const size_t mlen = method_name ? strlen(method_name) : 0;
+  if (method_name) total += 1 + varint_len(mlen) + mlen;
+  *len = (int64_t)total;
+  if (!out) return HGX_OK;
+  if (cap < (int64_t)total) return host_fail(HGX_EINVAL, "output buffer too small");
+  uint8_t *p = out;
+  for (int64_t j : on) p = put_entry(p, 1, node_ids[j], node_tab + (size_t)j * d, d);
+  for (int64_t j : oe) p = put_entry(p, 2, edge_ids[j], edge_tab + (size_t)j * d, d);
+  *p++ = 0x18;  // dim
+  p = put_varint(p, key_bits(d));
+  if (method_name) {
+    *p++ = 0x22;  // method_name
+    p = put_varint(p, mlen);
+    memcpy(p, method_name, mlen);
+    p += mlen;
+  }
+  return (size_t)(p - out) == total ? HGX_OK
+                                    : host_fail(HGX_EINVAL, "internal size mismatch");
+}

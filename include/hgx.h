@@ -167,6 +167,31 @@ int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
 int hgx_synth_powerlaw(int32_t N, int32_t E, double mean_degree,
                        double exponent, uint64_t seed, int32_t *rowptr_n,
                        int32_t *col_n, int64_t *nnz, int32_t *E_out);
+/* Native hypergraph.proto reader (Hypergraph, hypergraph.proto:6-23): the
+ * serialized message -> the compressed incidence of
+ * CompressRange(hg) (hypergraph_util.py:223-244) over every node's `edges`
+ * list (Relabel, :208-212), duplicates dropped, plus weights (default 1).
+ * Parse, read sizes, fill (rowptr_n N+1, col_n nnz, ids/weights N or E;
+ * any pointer may be NULL), free. Errors: hgx_host_last_error(). */
+typedef struct hgx_hg hgx_hg;
+int hgx_proto_parse_hypergraph(const uint8_t *buf, int64_t len, hgx_hg **out,
+                               int32_t *N, int32_t *E, int64_t *nnz);
+int hgx_proto_hypergraph_fill(const hgx_hg *h, int32_t *rowptr_n,
+                              int32_t *col_n, int64_t *node_ids,
+                              int64_t *edge_ids, float *node_weight,
+                              float *edge_weight);
+void hgx_proto_hypergraph_free(hgx_hg *h);
+/* Native HypergraphEmbedding writer (hypergraph.proto:26-35): rows of
+ * node_tab (n_nodes x d) keyed by node_ids, likewise edges, dim, and
+ * method_name (NULL = unset), entries in ascending id order. out == NULL
+ * returns the size in *len; then call again with cap >= *len. */
+int hgx_proto_write_embedding(int64_t n_nodes, const int64_t *node_ids,
+                              const float *node_tab, int64_t n_edges,
+                              const int64_t *edge_ids, const float *edge_tab,
+                              int d, const char *method_name, uint8_t *out,
+                              int64_t cap, int64_t *len);
+/* Message of the last failed host utility call on this thread. */
+const char *hgx_host_last_error(void);
 /* CSR transpose by counting sort (rows of the result sorted). */
 int hgx_csr_transpose(int32_t nrow, int32_t ncol, const int32_t *rowptr,
                       const int32_t *col, int32_t *rowptr_t, int32_t *col_t);

@@ -1,0 +1,127 @@
+"""Native hypergraph.proto reader / HypergraphEmbedding writer (libhgx host
+code, CPU only) against Python protobuf on the same messages."""
+
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from hypergraphembedding_amd import (AddNodeToEdge, CreateRandomHyperGraph,
+                                     Hypergraph, HypergraphEmbedding, Incidence,
+                                     Relabel)
+from hypergraphembedding_amd.algebraic_distance import coords_to_embedding
+from hypergraphembedding_amd.proto_native import (embedding_bytes,
+                                                  read_incidence,
+                                                  write_embedding)
+
+
+def _same_incidence(a, b):
+  assert (a.N, a.E) == (b.N, b.E)
+  for f in ("rp_n", "col_n", "rp_e", "col_e", "node_ids", "edge_ids",
+            "node_weight", "edge_weight"):
+    assert np.array_equal(getattr(a, f), getattr(b, f)), f
+
+
+def test_read_reference_fixture(tmp_path):
+  path = os.path.join(GOLDEN, "snap_youtube_tiny.hypergraph.pb")
+  hg = Hypergraph()
+  with open(path, "rb") as f:
+    hg.ParseFromString(f.read())
+  _same_incidence(read_incidence(path), Incidence.from_hypergraph(hg))
+  with open(path, "rb") as f:
+    _same_incidence(read_incidence(f.read()), Incidence.from_hypergraph(hg))
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_read_random_messages(seed):
+  """Messages built field by field: sparse and negative int32 ids, weights,
+  names, duplicate edges in a node list, edges no node references."""
+  rnd = random.Random(seed)
+  base = CreateRandomHyperGraph(rnd.randint(1, 40), rnd.randint(1, 30), 0.2)
+  nmap = {n: rnd.randint(-2**31, 2**31 - 1) for n in base.node}
+  emap = {e: rnd.randint(-1000, 10**6) for e in base.edge}
+  hg = Hypergraph()
+  for n, nd in base.node.items():
+    hg.node[nmap[n]].edges.extend(emap[e] for e in nd.edges)
+  for e, ed in base.edge.items():
+    hg.edge[emap[e]].nodes.extend(nmap[n] for n in ed.nodes)
+  hg.edge[10**7].name = "unreferenced"
+  for n in list(hg.node)[:3]:
+    hg.node[n].weight = rnd.random()
+    hg.node[n].name = "n%d" % n
+    if hg.node[n].edges:
+      hg.node[n].edges.append(hg.node[n].edges[0])
+  for e in list(hg.edge)[:3]:
+    hg.edge[e].weight = rnd.random()
+  hg.name = "g%d" % seed
+  _same_incidence(read_incidence(hg.SerializeToString()),
+                  Incidence.from_hypergraph(hg))
+
+
+def test_read_packed_edges_and_map_last_entry_wins():
+  from google.protobuf.internal import encoder
+  # hand-built wire bytes: node 5 -> edges [7, 9] packed, then node 5 again
+  # -> [9] (map semantics: the last entry wins); edges 7 and 9; name field
+  def ld(field, payload):
+    return encoder._VarintBytes(field << 3 | 2) + encoder._VarintBytes(len(payload)) + payload
+  def node_entry(key, edges):
+    packed = b"".join(encoder._VarintBytes(x) for x in edges)
+    nd = ld(1, packed)
+    return ld(1, b"\x08" + encoder._VarintBytes(key) + ld(2, nd))
+  def edge_entry(key):
+    return ld(2, b"\x08" + encoder._VarintBytes(key) + ld(2, b""))
+  buf = node_entry(5, [7, 9]) + edge_entry(7) + edge_entry(9) + \
+      node_entry(5, [9]) + ld(3, b"name")
+  hg = Hypergraph()
+  hg.ParseFromString(buf)
+  assert list(hg.node[5].edges) == [9]
+  _same_incidence(read_incidence(buf), Incidence.from_hypergraph(hg))
+
+
+def test_read_errors():
+  hg = Hypergraph()
+  AddNodeToEdge(hg, 1, 2)
+  del hg.edge[2]  # node lists an edge missing from hypergraph.edge
+  with pytest.raises(AssertionError):
+    read_incidence(hg.SerializeToString())
+  with pytest.raises(AssertionError):
+    read_incidence(b"\x0a\xff\xff\xff")  # truncated length-delimited field
+  empty = read_incidence(b"")
+  assert (empty.N, empty.E, empty.nnz) == (0, 0, 0)
+
+
+def test_write_embedding_matches_protobuf(tmp_path):
+  rnd = np.random.RandomState(0)
+  hg = CreateRandomHyperGraph(30, 20, 0.2)
+  hg = Relabel(hg, {n: 3 * n + 40 for n in hg.node}, {e: 7 * e + 1 for e in hg.edge})
+  inc = Incidence.from_hypergraph(hg)
+  d = 5
+  x = rnd.standard_normal((inc.N, d)).astype(np.float32)
+  y = rnd.standard_normal((inc.E, d)).astype(np.float32)
+  want = coords_to_embedding(inc, x, y, d, "HG2V_ALG_DIST")
+  got = HypergraphEmbedding()
+  got.ParseFromString(embedding_bytes(inc, x, y, "HG2V_ALG_DIST").tobytes())
+  assert got == want
+  p = tmp_path / "e.pb"
+  n = write_embedding(str(p), inc, x, y, "X")
+  assert p.stat().st_size == n
+  back = HypergraphEmbedding()
+  back.ParseFromString(p.read_bytes())
+  assert back.method_name == "X" and back.dim == d
+  assert np.array_equal(np.array(back.node[int(inc.node_ids[3])].values, np.float32), x[3])
+
+
+def test_native_powerlaw_roundtrip_scale():
+  """A 200k-incidence message through both parsers (scale check)."""
+  from hypergraphembedding_amd.synthetic import powerlaw_hypergraph
+  inc = powerlaw_hypergraph(N=10_000, E=5_000, seed=2)
+  hg = Hypergraph()
+  for v in range(inc.N):
+    hg.node[v].edges.extend(inc.col_n[inc.rp_n[v]:inc.rp_n[v + 1]].tolist())
+  for e in range(inc.E):
+    hg.edge[e].nodes.extend(inc.col_e[inc.rp_e[e]:inc.rp_e[e + 1]].tolist())
+  got = read_incidence(hg.SerializeToString())
+  _same_incidence(got, Incidence.from_hypergraph(hg))
+  assert np.array_equal(got.col_n, inc.col_n)
