@@ -249,6 +249,65 @@ def main():
       lines = sum(v.get("TCC_MISS_sum", 0.0) for v in kern.values()) * 128.0
       c4["l2_miss_line_bytes_per_iter"] = lines
       c4["line_gbps"] = round(lines / (ms4 / args.alg_iters * 1e-3) / 1e9, 1)
+    # ---- FOBE on the same graph (C4 shape), d=256, one GPU ----
+    # Quota S on a seeded 2% of node rows and edge rows (others 0: the
+    # reference's per-row quota int(weight * S) with weights 1 / 0). Every
+    # 2-hop row of a node in a power-law edge is union-sampled.
+    rsq = np.random.RandomState(2)
+    S4, K4, d4 = args.num_samples, args.num_neighbors, 256
+    nq4 = np.where(rsq.random_sample(big.N) < 0.02, S4, 0).astype(np.int32)
+    eq4 = np.where(rsq.random_sample(big.E) < 0.02, S4, 0).astype(np.int32)
+    sync()
+    t = time.perf_counter()
+    n4 = ctx.sample_fobe(4000 + rank, K4, nq4, eq4)
+    sync()
+    fobe_sample_s = time.perf_counter() - t
+    union_rows, _ = ctx.sample_stats()
+    ctx.model_init(d4, big.N + 1, big.E + 1, seed=11 + rank)
+    ctx.train(batch=args.batch, max_epochs=1, loss=_hgx.LOSS_KLD,
+              act=_hgx.ACT_SIGMOID, min_delta=-1e30, shuffle_seed=1)  # warm
+    sync()
+    t = time.perf_counter()
+    ctx.train(batch=args.batch, max_epochs=1, loss=_hgx.LOSS_KLD,
+              act=_hgx.ACT_SIGMOID, min_delta=-1e30, shuffle_seed=2)
+    sync()
+    t4 = time.perf_counter() - t
+    ms4t, rec4, bat4 = ctx.train_stats()
+    fobe4 = {"records": n4, "rows_sampled": int((nq4 > 0).sum() + (eq4 > 0).sum()),
+             "union_sampled_rows": union_rows,
+             "sampling_s": round(fobe_sample_s, 3), "dim": d4,
+             "train_records_per_s": round(n4 / t4, 1),
+             "per_batch_us": round(ms4t * 1e3 / max(bat4, 1), 2),
+             "loss": "KLD", "act": "sigmoid"}
+    if rank == 0 and world == 1 and not args.no_cpu:
+      # CPU port on a 100k-record slice of the same stream (ids compacted to
+      # the rows it touches, which only helps the CPU's caches)
+      sys.path.insert(0, os.path.join(ROOT, "oracle"))
+      import oracle as O
+      idx4, tgt4 = ctx.records_get()
+      sel = np.random.RandomState(3).permutation(n4)[:100_000]
+      ci, ct = idx4[sel].copy(), tgt4[sel].copy()
+      del idx4, tgt4
+      R4 = 4 + 2 * K4
+      node_cols = [0, 2] + list(range(4, 4 + K4))
+      edge_cols = [1, 3] + list(range(4 + K4, R4))
+      for cols in (node_cols, edge_cols):
+        u, inv = np.unique(ci[:, cols], return_inverse=True)
+        ci[:, cols] = inv.reshape(ci[:, cols].shape).astype(np.int32) + (u[0] != 0)
+      init = np.random.RandomState(4)
+      nt4 = init.uniform(-0.05, 0.05, (int(ci[:, node_cols].max()) + 2, d4)).astype(np.float32)
+      et4 = init.uniform(-0.05, 0.05, (int(ci[:, edge_cols].max()) + 2, d4)).astype(np.float32)
+      t = time.perf_counter()
+      O.train(ci, ct, K4, nt4, et4, O.LOSS_KLD, O.ACT_SIGMOID,
+              batch=args.batch, max_epochs=1, min_delta=-1e30)
+      cpu4_s = time.perf_counter() - t
+      fobe4["cpu_port_records_per_s"] = round(ci.shape[0] / cpu4_s, 1)
+      fobe4["cpu_port_sample"] = (f"{ci.shape[0]} records of this stream, d={d4}, "
+                                  f"1 epoch, oracle/hgref.c single-threaded, "
+                                  f"{cpu4_s:.1f} s")
+      fobe4["vs_cpu_port"] = round(fobe4["train_records_per_s"] /
+                                   fobe4["cpu_port_records_per_s"], 1)
+    c4["fobe_d256"] = fobe4
     del big, bx0, by0
 
   if rank == 0:

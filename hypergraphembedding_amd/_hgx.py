@@ -55,6 +55,7 @@ SIGNATURES = {
     "hgx_incidence_weights": (_int, [_vp, _int, ctypes.c_double, _vp, _vp]),
     "hgx_sample_fobe": (_int, [_vp, _u64, _int, _vp, _vp, _vp, _vp, _pi64]),
     "hgx_sample_hobe": (_int, [_vp, _u64, _int, _int, _pi64]),
+    "hgx_sample_last_stats": (_int, [_vp, _pi64, _pi64]),
     "hgx_records_set": (_int, [_vp, _i64, _int, _vp, _vp]),
     "hgx_records_info": (_int, [_vp, _pi64, _pint]),
     "hgx_records_get": (_int, [_vp, _vp, _vp]),
@@ -246,6 +247,13 @@ class Context:
     self._chk(lib().hgx_sample_hobe(self.h, seed & (2**64 - 1), K, S,
                                     ctypes.byref(n)))
     return n.value
+
+  def sample_stats(self):
+    """(union-sampled 2-hop rows, fallbacks to expansion) of the last call."""
+    u, f = ctypes.c_int64(), ctypes.c_int64()
+    self._chk(lib().hgx_sample_last_stats(self.h, ctypes.byref(u),
+                                          ctypes.byref(f)))
+    return u.value, f.value
 
   def records_set(self, idx, tgt):
     idx = _c(idx, np.int32)

@@ -66,6 +66,9 @@ struct hgx_ctx {
   double alg_ms = 0, alg_bytes = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 
+  // sampler diagnostics of the last hgx_sample_* call
+  int64_t sample_union_rows = 0, sample_fallback_rows = 0;
+
   // ---- records (SamplesToModelInput layout) ----
   int64_t n_rec = 0;
   int K = 0;

@@ -17,6 +17,22 @@
 // select. The chosen columns are written sorted (deterministic for a seed).
 // The uniform draws come from a counter-based hash, so the sampled SET has
 // the reference's distribution but not numpy's MT19937 stream.
+//
+// Large 2-hop rows (A*A^T, A^T*A with more than `reject_w` expansion paths,
+// e.g. every node of a power-law edge with 1e6 members) are not expanded.
+// They are sampled from the union U = U_m S_m (S_m = row m of the second
+// factor, m over row r of the first) by Karp-Luby rejection:
+//   1. draw a path uniformly: m with probability |S_m| / W, c uniform in S_m;
+//   2. accept iff m is the FIRST set holding c, i.e.
+//      m == min(row r of l1 ∩ row c of l1) (for both patterns the second
+//      factor is the transpose of the first);
+//   3. distinct accepted columns are kept in draw order until q are held.
+// Step 2 makes every c in U equally likely per draw; step 3 (sequential
+// draws, repeats rejected) yields a uniform q-subset, which is the
+// distribution of np.random.choice(U, q, replace=False). Draws are processed
+// in rounds of 256 in thread order, so the result is deterministic for a
+// seed. A row whose union turns out smaller than q (no progress for 32
+// rounds) falls back to expansion.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -51,6 +67,8 @@ struct SampleArgs {
   int *row_ctr;              // dynamic row queue
   uint64_t seed;
   int lds_bitmap;            // 1 -> bitmap in dynamic LDS
+  int64_t reject_w;          // 2-hop rows with more paths: rejection sampling
+  int *stats;                // [0] rows sampled by rejection, [1] fallbacks
 };
 
 __device__ int block_scan_excl(int v, int *total, int *s_ws) {
@@ -198,9 +216,141 @@ __device__ void bitonic_sort_int(int *a, int n) {
   }
 }
 
+// smallest element of sorted a[0..na) that is also in sorted b[0..nb)
+// (INT_MAX if none): walk the shorter list, binary-search the longer one
+__device__ int first_common(const int *a, int na, const int *b, int nb) {
+  if (na > nb) {
+    const int *t = a;
+    a = b;
+    b = t;
+    const int tn = na;
+    na = nb;
+    nb = tn;
+  }
+  int lo = 0;
+  for (int i = 0; i < na; i++) {
+    const int x = a[i];
+    int hi = nb;
+    while (lo < hi) {  // first b[j] >= x, from the previous position on
+      const int mid = (lo + hi) >> 1;
+      if (b[mid] < x) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo == nb) return INT_MAX;
+    if (b[lo] == x) return x;
+  }
+  return INT_MAX;
+}
+
+struct RejState {
+  unsigned long long key[kSB];
+  int flag[kSB];
+  int cand[kSB];
+  int wsum_ws[kSB / 64];
+  long long wtot;
+  int wmax;
+};
+
+// Karp-Luby union sampling of row r (see the header). Fills S.sel[0..q) and
+// sets their bitmap bits; returns false if the union looks smaller than q.
+__device__ bool reject_row(const SampleArgs &A, int r, int q, unsigned *bm,
+                           SharedState &S, RejState &J, long long W, int wmax) {
+  const int tid = threadIdx.x;
+  const int b1 = A.l1.rp[r], e1 = A.l1.rp[r + 1], n1 = e1 - b1;
+  const bool small = n1 <= kSB;
+  if (small) {  // exact path draws: prefix of |S_m| over row r in LDS
+    const int i1 = b1 + tid;
+    int id1 = -1, sz = 0;
+    if (tid < n1) {
+      id1 = A.l1.col[i1];
+      sz = A.l2.rp[id1 + 1] - A.l2.rp[id1];
+    }
+    int tot;
+    const int o1 = block_scan_excl(sz, &tot, S.ws);
+    S.a_id[tid] = id1;
+    S.a_off[tid] = o1;
+  }
+  if (tid == 0) S.nsel = 0;
+  __syncthreads();
+  int stall = 0;
+  for (int round = 0; round < 4096; round++) {
+    const uint64_t base = ((uint64_t)(uint32_t)r << 32) ^ ((uint64_t)round << 12);
+    const uint64_t h = hgx::rand64(A.seed, 0x300 + A.pattern, base + tid);
+    const uint64_t h2 = hgx::mix64(h ^ 0x51ed27ull);
+    int m = -1, c = -1;
+    if (small) {
+      const int w = (int)hgx::bounded(h, (uint32_t)W);
+      const int j = upper_find(S.a_off, n1, w);
+      m = S.a_id[j];
+      c = A.l2.col[A.l2.rp[m] + (w - S.a_off[j])];
+    } else {  // m uniform, accepted with |S_m| / max |S_m|
+      m = A.l1.col[b1 + (int)hgx::bounded(h, (uint32_t)n1)];
+      const int sz = A.l2.rp[m + 1] - A.l2.rp[m];
+      if ((uint32_t)(h2 >> 32) % (uint32_t)wmax < (uint32_t)sz)
+        c = A.l2.col[A.l2.rp[m] + (int)hgx::bounded(h2, (uint32_t)sz)];
+    }
+    int cand = INT_MAX;
+    if (c >= 0 && !(bm[c >> 5] & (1u << (c & 31)))) {
+      const int f = first_common(A.l1.col + b1, n1, A.l1.col + A.l1.rp[c],
+                                 A.l1.rp[c + 1] - A.l1.rp[c]);
+      if (f == m) cand = c;
+    }
+    // repeats inside the round: keep the lowest thread (sort (col, tid))
+    J.key[tid] = ((unsigned long long)(unsigned)cand << 32) | (unsigned)tid;
+    __syncthreads();
+    for (int size = 2; size <= kSB; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const int t = tid;
+        if (t < kSB / 2) {
+          const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+          const bool up = (lo & size) == 0;
+          const unsigned long long x = J.key[lo], y = J.key[hi];
+          if ((x > y) == up) {
+            J.key[lo] = y;
+            J.key[hi] = x;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    {
+      const unsigned long long k = J.key[tid];
+      const int col = (int)(k >> 32);
+      const bool fresh = col != INT_MAX &&
+                         (tid == 0 || (int)(J.key[tid - 1] >> 32) != col);
+      J.flag[(int)(k & 0xffffffffu)] = fresh ? 1 : 0;
+    }
+    __syncthreads();
+    int total;
+    const int rank = block_scan_excl(J.flag[tid], &total, S.ws);
+    const int need = q - S.nsel;
+    if (J.flag[tid] && rank < need) {
+      S.sel[S.nsel + rank] = cand;
+      atomicOr(&bm[cand >> 5], 1u << (cand & 31));
+    }
+    __syncthreads();
+    const int got = min(total, need);
+    if (tid == 0) S.nsel += got;
+    __syncthreads();
+    if (S.nsel >= q) return true;
+    stall = got ? 0 : stall + 1;
+    if (stall >= 32) break;
+  }
+  // give back the bits and let expansion handle the row
+  for (int i = tid; i < S.nsel; i += kSB) {
+    const int c = S.sel[i];
+    bm[c >> 5] = 0u;
+  }
+  __syncthreads();
+  return false;
+}
+
 __global__ __launch_bounds__(kSB) void sample_rows(SampleArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned s_dyn[];
   __shared__ SharedState S;
+  __shared__ RejState J;
+  __shared__ long long s_rw[kSB / 64];
+  __shared__ int s_rm[kSB / 64];
   __shared__ int s_row;
   const int tid = threadIdx.x;
   const int nwords = (A.ncols + 31) >> 5;
@@ -224,8 +374,54 @@ __global__ __launch_bounds__(kSB) void sample_rows(SampleArgs A) {
       __syncthreads();
       continue;
     }
+    if (A.levels == 2 && q <= kSelCap && A.reject_w > 0) {
+      // path count W and max |S_m| of the row (block reductions)
+      const int b1 = A.l1.rp[r], e1 = A.l1.rp[r + 1];
+      long long w = 0;
+      int wm = 0;
+      for (int t = b1 + tid; t < e1; t += kSB) {
+        const int id = A.l1.col[t];
+        const int sz = A.l2.rp[id + 1] - A.l2.rp[id];
+        w += sz;
+        wm = max(wm, sz);
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        w += __shfl_xor(w, off);
+        wm = max(wm, __shfl_xor(wm, off));
+      }
+      if ((tid & 63) == 0) {
+        s_rw[tid >> 6] = w;
+        s_rm[tid >> 6] = wm;
+      }
+      __syncthreads();
+      long long W = 0;
+      int wmax = 0;
+#pragma unroll
+      for (int i = 0; i < kSB / 64; i++) {
+        W += s_rw[i];
+        wmax = max(wmax, s_rm[i]);
+      }
+      __syncthreads();
+      if (W > A.reject_w && W < (1ll << 31) && reject_row(A, r, q, bm, S, J, W, wmax)) {
+        if (tid == 0) atomicAdd(&A.stats[0], 1);
+        bitonic_sort_int(S.sel, q);
+        for (int i = tid; i < q; i += kSB) out[i] = S.sel[i];
+        if (tid == 0) A.out_cnt[r] = q;
+        for (int i = tid; i < q; i += kSB) {
+          const int c = S.sel[i];
+          bm[c >> 5] = 0u;
+        }
+        __syncthreads();
+        continue;
+      }
+      if (W > A.reject_w && tid == 0) atomicAdd(&A.stats[1], 1);
+      if (tid == 0) S.nsel = 0;
+      __syncthreads();
+    }
     expand_row(A, r, bm, list, S);
     __syncthreads();
+    if (tid == 0 && S.cnt > A.list_cap) atomicOr(&A.stats[2], 1);
     const int cnt = (int)min((int64_t)S.cnt, A.list_cap);
     const int m = min(q, cnt);
     if (m < cnt) {
@@ -463,13 +659,25 @@ int run_pattern(hgx_ctx *ctx, int pattern, const int32_t *host_quota,
   const int nwords = (a.ncols + 31) / 32;
   const bool lds = (size_t)nwords * 4 <= 48 * 1024;
   int nwg = 1024;
-  const int64_t list_cap = a.ncols;
+  {
+    // 2-hop rows with more expansion paths than this are union-sampled
+    // (HGX_SAMPLE_REJECT_W overrides; 0 disables)
+    const char *e = getenv("HGX_SAMPLE_REJECT_W");
+    a.reject_w = e ? atoll(e) : (int64_t)1 << 15;
+  }
+  // the distinct list only serves expanded rows: with union sampling on,
+  // 2-hop rows expand at most reject_w paths (a fallback row that does not
+  // fit is reported, never truncated)
+  const int64_t list_cap =
+      (a.levels == 2 && a.reject_w > 0)
+          ? std::min<int64_t>(a.ncols, std::max<int64_t>(2 * a.reject_w, 65536))
+          : a.ncols;
   while (nwg > 64 && (double)nwg * (list_cap * 4 + (lds ? 0 : nwords * 4)) > 4e9)
     nwg /= 2;
   HGX_TRY(hgx_ensure(ctx, ctx->s3, sizeof(int) * (size_t)nwg * list_cap + 16));
   if (!lds) HGX_TRY(hgx_ensure(ctx, ctx->s4, sizeof(unsigned) * (size_t)nwg * nwords));
   HGX_TRY(hgx_ensure(ctx, ctx->s0, 16));
-  HGX_HIP(ctx, hipMemsetAsync(ctx->s0.p, 0, sizeof(int), ctx->stream));
+  HGX_HIP(ctx, hipMemsetAsync(ctx->s0.p, 0, 16, ctx->stream));
   a.quota = po.q.as<int>();
   a.quota_all = quota_all;
   a.cap_off = po.cap_off.as<int64_t>();
@@ -481,9 +689,22 @@ int run_pattern(hgx_ctx *ctx, int pattern, const int32_t *host_quota,
   a.row_ctr = ctx->s0.as<int>();
   a.seed = seed;
   a.lds_bitmap = lds;
+  a.stats = ctx->s0.as<int>() + 1;  // [0] union-sampled rows, [1] fallbacks, [2] overflow
   hipLaunchKernelGGL(sample_rows, dim3(nwg), dim3(kSB),
                      lds ? (size_t)nwords * 4 : 0, ctx->stream, a);
   HGX_LAUNCH_CHECK(ctx);
+  {
+    int st[3] = {0, 0, 0};
+    HGX_HIP(ctx, hipMemcpyAsync(st, a.stats, sizeof(st), hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->sample_union_rows += st[0];
+    ctx->sample_fallback_rows += st[1];
+    HGX_CHECK(ctx, st[2] == 0, HGX_EUNSUP,
+              "a sampled row has more than %lld distinct columns "
+              "(raise HGX_SAMPLE_REJECT_W or disable union sampling)",
+              (long long)list_cap);
+  }
   HGX_TRY(hgx_ensure(ctx, po.rec_off, sizeof(int64_t) * (R + 1)));
   HGX_TRY(excl_scan_i32_to_i64(ctx, po.cnt.as<int>(), po.rec_off.as<int64_t>(),
                                R, &po.total));
@@ -583,6 +804,7 @@ extern "C" int hgx_sample_fobe(hgx_ctx *ctx, uint64_t seed, int K,
   HGX_TRY(check_quota(ctx, node_quota, ctx->N, "node"));
   HGX_TRY(check_quota(ctx, edge_quota, ctx->E, "edge"));
   HGX_HIP(ctx, hipSetDevice(ctx->device));
+  ctx->sample_union_rows = ctx->sample_fallback_rows = 0;
   // BooleanSamples order (hg2v_sample.py:156-194): nn, ee, ne(node rows),
   // ne(edge rows, swapped); then negatives (:198-240).
   PatOut nn, ee, ne_n, ne_e;
@@ -634,6 +856,7 @@ extern "C" int hgx_sample_hobe(hgx_ctx *ctx, uint64_t seed, int K, int S,
   HGX_CHECK(ctx, K >= 1 && K <= 16, HGX_EUNSUP, "num_neighbors %d outside [1,16]", K);
   HGX_CHECK(ctx, S >= 0, HGX_EINVAL, "num_samples must be >= 0 (hg2v_sample.py:647)");
   HGX_HIP(ctx, hipSetDevice(ctx->device));
+  ctx->sample_union_rows = ctx->sample_fallback_rows = 0;
   // AlgebraicDistanceSamples order (hg2v_sample.py:658-715)
   PatOut nn, ee, ne_n, ne_e;
   HGX_TRY(run_pattern(ctx, PAT_NN, nullptr, S, seed, nn));
@@ -653,5 +876,13 @@ extern "C" int hgx_sample_hobe(hgx_ctx *ctx, uint64_t seed, int K, int S,
   HGX_TRY(hgx_hobe_fill_probs(ctx, 2, o_ne, total));
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (n_records) *n_records = total;
+  return HGX_OK;
+}
+
+extern "C" int hgx_sample_last_stats(hgx_ctx *ctx, int64_t *union_rows,
+                                     int64_t *fallback_rows) {
+  if (!ctx) return HGX_EINVAL;
+  if (union_rows) *union_rows = ctx->sample_union_rows;
+  if (fallback_rows) *fallback_rows = ctx->sample_fallback_rows;
   return HGX_OK;
 }

@@ -129,6 +129,11 @@ int hgx_sample_fobe(hgx_ctx *ctx, uint64_t seed, int K,
  * coords: quota S for every row, nn/ee/ne probabilities as above. */
 int hgx_sample_hobe(hgx_ctx *ctx, uint64_t seed, int K, int S,
                     int64_t *n_records);
+/* Of the last hgx_sample_* call: 2-hop rows sampled from the union by
+ * rejection (rows whose expansion exceeds HGX_SAMPLE_REJECT_W paths,
+ * default 32768) and rows that fell back to expansion. */
+int hgx_sample_last_stats(hgx_ctx *ctx, int64_t *union_rows,
+                          int64_t *fallback_rows);
 int hgx_records_set(hgx_ctx *ctx, int64_t n, int K, const int32_t *idx,
                     const float *tgt);
 int hgx_records_info(hgx_ctx *ctx, int64_t *n, int *K);

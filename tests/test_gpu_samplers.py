@@ -24,6 +24,18 @@ from conftest import golden
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["expand", "union"])
+def mode(request, monkeypatch):
+  """expand: every row's 2-hop expansion is materialised (default for these
+  small graphs); union: 2-hop rows with more than 1 path are union-sampled
+  by Karp-Luby rejection (the path large power-law rows take)."""
+  if request.param == "union":
+    monkeypatch.setenv("HGX_SAMPLE_REJECT_W", "1")
+  else:
+    monkeypatch.setenv("HGX_SAMPLE_REJECT_W", "0")
+  return request.param
+
+
 @pytest.fixture(scope="module")
 def ctx():
   from hypergraphembedding_amd import _hgx
@@ -55,7 +67,7 @@ def _check_distinct(rows, cols):
   assert np.unique(key).size == key.size
 
 
-def test_fobe_tiny_counts_validity(ctx, tiny_inc):
+def test_fobe_tiny_counts_validity(ctx, tiny_inc, mode):
   inc = tiny_inc
   S, K = 200, 5
   ctx.upload(inc)
@@ -99,6 +111,8 @@ def test_fobe_tiny_counts_validity(ctx, tiny_inc):
   nbe = idx[gne, 4 + K:] - 1
   assert _pairs_valid(at, np.repeat(e, K), nbn.ravel())
   assert _pairs_valid(a, np.repeat(v, K), nbe.ravel())
+  union_rows, _ = ctx.sample_stats()
+  assert (union_rows > 0) == (mode == "union")
   # targets: 1 on the record's own head, 0 elsewhere (unweighted FOBE)
   assert np.all(tgt[gnn, 0] == 1) and np.all(tgt[gee, 1] == 1)
   assert np.all(tgt[gne, 2] == 1)
@@ -170,7 +184,7 @@ def test_hobe_small_counts_and_probs(ctx, small_inc):
   _check_distinct(e[n_node:], v[n_node:])
 
 
-def test_sampler_uniformity_chi_square(ctx, small_inc):
+def test_sampler_uniformity_chi_square(ctx, small_inc, mode):
   """Inclusion frequency of every column of a row is q/|row| over seeds."""
   ctx.upload(small_inc)
   a, at = small_inc.to_scipy()
@@ -198,7 +212,7 @@ def test_sampler_uniformity_chi_square(ctx, small_inc):
   assert chi.pvalue > 1e-4, (chi, obs)
 
 
-def test_sampler_deterministic_for_seed(ctx, small_inc):
+def test_sampler_deterministic_for_seed(ctx, small_inc, mode):
   ctx.upload(small_inc)
   nq = np.full(small_inc.N, 5, np.int32)
   eq = np.full(small_inc.E, 5, np.int32)
@@ -210,3 +224,34 @@ def test_sampler_deterministic_for_seed(ctx, small_inc):
   c = ctx.records_get()
   assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
   assert not np.array_equal(a[0], c[0])
+
+
+def test_fobe_powerlaw_union_rows(ctx, monkeypatch):
+  """Power-law edges make 2-hop rows far too large to expand: those rows are
+  union-sampled; exact per-row counts min(S, |union|) and pair validity are
+  checked on sampled rows, with unions computed from the CSR."""
+  from hypergraphembedding_amd.synthetic import powerlaw_hypergraph
+  monkeypatch.setenv("HGX_SAMPLE_REJECT_W", "4096")
+  inc = powerlaw_hypergraph(N=20_000, E=10_000, seed=4)
+  S, K = 200, 5
+  ctx.upload(inc)
+  nq = np.full(inc.N, S, np.int32)
+  eq = np.full(inc.E, S, np.int32)
+  ctx.sample_fobe(21, K, nq, eq)
+  union_rows, fallbacks = ctx.sample_stats()
+  assert union_rows > 1000
+  idx, tgt = ctx.records_get()
+  gnn, gee, _ = _blocks(idx, tgt, K)
+  rs = np.random.RandomState(1)
+  for kind, rp1, c1, rp2, c2, nrow, lcol, rcol, sel in (
+      ("nn", inc.rp_n, inc.col_n, inc.rp_e, inc.col_e, inc.N, 0, 2, gnn),
+      ("ee", inc.rp_e, inc.col_e, inc.rp_n, inc.col_n, inc.E, 1, 3, gee)):
+    left = idx[sel, lcol] - 1
+    right = idx[sel, rcol] - 1
+    cnt = np.bincount(left, minlength=nrow)
+    for r in rs.choice(nrow, 80, replace=False):
+      mids = c1[rp1[r]:rp1[r + 1]]
+      union = np.unique(np.concatenate([c2[rp2[m]:rp2[m + 1]] for m in mids]))
+      assert cnt[r] == min(S, union.size), (kind, r)
+      got = right[left == r]
+      assert np.unique(got).size == got.size and np.isin(got, union).all()
