@@ -655,22 +655,31 @@ int env_int(const char *name, int dflt) {
   return v && v[0] ? atoi(v) : dflt;
 }
 
+template <int L, int VPL, int TB>
+KFn fwd_spec(int K, int loss, int act) {
+  if (K == 5 && loss == 0 && act == 0) return train_fwd_bwd<L, VPL, 5, true, 1, TB>;
+  if (K == 5 && loss == 1 && act == 1) return train_fwd_bwd<L, VPL, 5, true, 2, TB>;
+  return nullptr;
+}
+
 template <int L, int VPL>
-KFn fwd_for(int K, int loss, int act) {
-  if (K == 5 && loss == 0 && act == 0) return train_fwd_bwd<L, VPL, 5, true, 1, kTB>;
-  if (K == 5 && loss == 1 && act == 1) return train_fwd_bwd<L, VPL, 5, true, 2, kTB>;
+KFn fwd_for(int K, int loss, int act, int tb1) {
+  KFn f = tb1 == 512 ? fwd_spec<L, VPL, 512>(K, loss, act)
+                     : fwd_spec<L, VPL, kTB>(K, loss, act);
+  if (f) return f;
   if (K <= 2) return train_fwd_bwd<L, VPL, 2, false, 0, kTB>;
   if (K <= 5) return train_fwd_bwd<L, VPL, 5, false, 0, kTB>;
   if (K <= 8) return train_fwd_bwd<L, VPL, 8, false, 0, kTB>;
   return train_fwd_bwd<L, VPL, 16, false, 0, kTB>;
 }
 
-bool pick_kernels(int L, int VPL, int K, int loss, int act, KFn &k1, KFn &k2) {
+bool pick_kernels(int L, int VPL, int K, int loss, int act, int &tb1, KFn &k1,
+                  KFn &k2) {
 #define HGX_CASE(LL, VV)                                                     \
   if (L == LL && VPL == VV) {                                                \
     k1 = env_int("HGX_TRAIN_GENERIC", 0) == 1                                \
              ? train_fwd_bwd<LL, VV, 16, false, 0, kTB>                      \
-             : fwd_for<LL, VV>(K, loss, act);                                \
+             : fwd_for<LL, VV>(K, loss, act, tb1);                           \
     k2 = train_update<LL, VV>;                                               \
     return true;                                                             \
   }
@@ -861,9 +870,15 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
 
   int L, VPL;
   geometry(ctx->d, L, VPL);
-  const int tb1 = kTB;
+  // K1 workgroup size: 8 records per workgroup measured best (d=128: 256
+  // threads, 10.5 us/batch vs 11.0 at 128 / 12.8 at 64 / 10.9 at 512;
+  // d=256: 512 threads, 13.6 vs 14.7 at 256). Specialised FOBE/HOBE
+  // kernels only; HGX_TRAIN_TB1=256|512 overrides.
+  int tb1 = env_int("HGX_TRAIN_TB1", L >= 64 ? 512 : kTB);
+  if (tb1 != 512) tb1 = kTB;
+  if (!(K == 5 && loss == act) || env_int("HGX_TRAIN_GENERIC", 0) == 1) tb1 = kTB;
   KFn k1 = nullptr, k2 = nullptr;
-  HGX_CHECK(ctx, pick_kernels(L, VPL, K, loss, act, k1, k2), HGX_EUNSUP,
+  HGX_CHECK(ctx, pick_kernels(L, VPL, K, loss, act, tb1, k1, k2), HGX_EUNSUP,
             "no kernel for d=%d", ctx->d);
   {
     const int ab = env_int("HGX_TRAIN_ABLATE", 0);
