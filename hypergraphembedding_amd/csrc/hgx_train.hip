@@ -338,18 +338,18 @@ __device__ __forceinline__ void adagrad4(float4 &p, float4 &ac, float4 g,
 // The last two workgroups: the padding row 0 of the node / edge table, its
 // gradient = the sum of the nblk1 per-K1-workgroup partials, loaded by all
 // 256 threads at once and tree-summed in LDS (fixed order: deterministic).
-template <int L, int VPL>
-__global__ __launch_bounds__(kTB) void train_update(TrainArgs a, int cb) {
-  constexpr int GPB = kTB / L;
+template <int L, int VPL, int TB>
+__global__ __launch_bounds__(TB) void train_update(TrainArgs a, int cb) {
+  constexpr int GPB = TB / L;
   unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (g_trace) ts[0] = __builtin_amdgcn_s_memrealtime();
   const int dp = a.dp, SB = a.SB;
   const int2 bm = a.bmeta[cb];
   if (blockIdx.x >= gridDim.x - 2) {
-    __shared__ float4 s_part[kTB];
+    __shared__ float4 s_part[TB];
     const int table = blockIdx.x - (gridDim.x - 2);
     const int NC = dp / 4;                  // float4 columns, <= 256
-    const int TPC = kTB / NC;               // threads per column (>= 1)
+    const int TPC = TB / NC;               // threads per column (>= 1)
     const int col = threadIdx.x % NC, sub = threadIdx.x / NC;
     float4 *P = reinterpret_cast<float4 *>(table ? a.etab : a.ntab);
     float4 *A = reinterpret_cast<float4 *>(table ? a.eacc : a.nacc);
@@ -673,14 +673,14 @@ KFn fwd_for(int K, int loss, int act, int tb1) {
   return train_fwd_bwd<L, VPL, 16, false, 0, kTB>;
 }
 
-bool pick_kernels(int L, int VPL, int K, int loss, int act, int &tb1, KFn &k1,
-                  KFn &k2) {
+bool pick_kernels(int L, int VPL, int K, int loss, int act, int &tb1, int tb2,
+                  KFn &k1, KFn &k2) {
 #define HGX_CASE(LL, VV)                                                     \
   if (L == LL && VPL == VV) {                                                \
     k1 = env_int("HGX_TRAIN_GENERIC", 0) == 1                                \
              ? train_fwd_bwd<LL, VV, 16, false, 0, kTB>                      \
              : fwd_for<LL, VV>(K, loss, act, tb1);                           \
-    k2 = train_update<LL, VV>;                                               \
+    k2 = tb2 == 512 ? train_update<LL, VV, 512> : train_update<LL, VV, kTB>; \
     return true;                                                             \
   }
   HGX_CASE(1, 1) HGX_CASE(2, 1) HGX_CASE(4, 1) HGX_CASE(8, 1)
@@ -877,8 +877,12 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   int tb1 = env_int("HGX_TRAIN_TB1", L >= 64 ? 512 : kTB);
   if (tb1 != 512) tb1 = kTB;
   if (!(K == 5 && loss == act) || env_int("HGX_TRAIN_GENERIC", 0) == 1) tb1 = kTB;
+  // K2 workgroup size: 512 threads measured best (d=128: 10.2 vs 10.6
+  // us/batch at 256 and 10.5 at 1024; d=256: 12.6 vs 13.5 / 12.7)
+  int tb2 = env_int("HGX_TRAIN_TB2", 512);
+  if (tb2 != 512) tb2 = kTB;
   KFn k1 = nullptr, k2 = nullptr;
-  HGX_CHECK(ctx, pick_kernels(L, VPL, K, loss, act, tb1, k1, k2), HGX_EUNSUP,
+  HGX_CHECK(ctx, pick_kernels(L, VPL, K, loss, act, tb1, tb2, k1, k2), HGX_EUNSUP,
             "no kernel for d=%d", ctx->d);
   {
     const int ab = env_int("HGX_TRAIN_ABLATE", 0);
@@ -911,7 +915,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   }
   const int RPB = tb1 / L;
   const int nblk1 = (batch + RPB - 1) / RPB;
-  const int GPB2 = kTB / L;
+  const int GPB2 = tb2 / L;
   // one unique-row task per group, plus the two padding-row workgroups
   const int grid2 = (SB + GPB2 - 1) / GPB2 + 2;
   const int64_t nbatches = (n + batch - 1) / batch;
@@ -1013,7 +1017,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   auto launch_run = [&](int cb0, int nrun) {
     for (int b = cb0; b < cb0 + nrun; b++) {
       hipLaunchKernelGGL(k1, dim3(nblk1), dim3(tb1), 0, ctx->stream, a, b);
-      hipLaunchKernelGGL(k2, dim3(grid2), dim3(kTB), 0, ctx->stream, a, b);
+      hipLaunchKernelGGL(k2, dim3(grid2), dim3(tb2), 0, ctx->stream, a, b);
     }
   };
   if (use_graph) {
