@@ -345,6 +345,10 @@ def main():
                     "sharded": world > 1},
         "algdist_c4": c4,
         "hobe_sampling_s": round(sample_s, 3),
+        # EmbedHg2vAlgDist's default job (alg-dist 20 iterations, HOBE
+        # sampling, 10 epochs) from the measured parts
+        "end_to_end_records_per_s": round(
+            n * 10 / (alg_ms * 1e-3 + sample_s + 10 * elapsed / args.steps), 1),
         "graph_gen_s": round(gen_s, 2),
         "roofline": roofline,
         "cpu_baseline": cpu,
