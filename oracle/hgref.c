@@ -587,6 +587,205 @@ int64_t hgref_hobe_sample(hgref_rng *s, int64_t N, int64_t E,
 }
 
 /* ------------------------------------------------------------------------- */
+/* Weighted-Jaccard samples (HG2V_ADJ_JAC / HG2V_NEIGH_JAC),                 */
+/* WeightedJaccardSamples (hg2v_sample.py:395-510), run_in_parallel=False.   */
+/* Features are per-incidence values on A's pattern: fn[] in node-major     */
+/* (A) order (node2features, N x E), fe[] in edge-major (A^T) order          */
+/* (edge2features, E x N), as UniformWeight / WeightByNeighborhood build.    */
+/* ------------------------------------------------------------------------- */
+
+/* SparseWeightedJaccard (hg2v_sample.py:250-273): over the sorted union of
+ * both supports, num += min, den += max (the `x < y` branch), float32
+ * sequential (0 + np.float32 -> float32); 0 if den == 0. */
+static float swj(const int32_t *ac, const float *av, int64_t na,
+                 const int32_t *bc, const float *bv, int64_t nb) {
+  float num = 0.0f, den = 0.0f;
+  int64_t i = 0, j = 0;
+  while (i < na || j < nb) {
+    float x, y;
+    if (j >= nb || (i < na && ac[i] < bc[j])) { x = av[i++]; y = 0.0f; }
+    else if (i >= na || bc[j] < ac[i]) { x = 0.0f; y = bv[j++]; }
+    else { x = av[i++]; y = bv[j++]; }
+    if (x < y) { num += x; den += y; }
+    else { num += y; den += x; }
+  }
+  if (den == 0.0f) return 0.0f;
+  return num / den;
+}
+
+/* GetAllCentroids / CentroidFromRows (hg2v_sample.py:276-326): row r =
+ * (sum over t in row r of idx2targets, ascending, of targets2features row
+ * t) / len(row r), float32 (scipy's ones @ sub-matrix adds rows in order),
+ * stored as CSR with sorted columns, zeros dropped (.nonzero()). */
+typedef struct {
+  int64_t *p;
+  int32_t *j;
+  float *v;
+} fcsr;
+
+static fcsr centroids(int64_t R, const int32_t *rp, const int32_t *col,
+                      int64_t ncols, const int32_t *frp, const int32_t *fcol,
+                      const float *fval) {
+  fcsr C;
+  float *acc = (float *)calloc(ncols > 0 ? ncols : 1, sizeof(float));
+  char *seen = (char *)calloc(ncols > 0 ? ncols : 1, 1);
+  int32_t *touched = (int32_t *)malloc(sizeof(int32_t) * (ncols > 0 ? ncols : 1));
+  int64_t cap = 1024, nnz = 0;
+  C.p = (int64_t *)malloc(sizeof(int64_t) * (R + 1));
+  C.j = (int32_t *)malloc(sizeof(int32_t) * cap);
+  C.v = (float *)malloc(sizeof(float) * cap);
+  C.p[0] = 0;
+  for (int64_t r = 0; r < R; r++) {
+    int64_t nt = 0;
+    const int32_t len = rp[r + 1] - rp[r];
+    for (int32_t q = rp[r]; q < rp[r + 1]; q++) {
+      const int32_t t = col[q];
+      for (int32_t z = frp[t]; z < frp[t + 1]; z++) {
+        const int32_t c = fcol[z];
+        if (!seen[c]) { seen[c] = 1; touched[nt++] = c; }
+        acc[c] = acc[c] + fval[z];
+      }
+    }
+    /* sorted column order */
+    for (int64_t a = 1; a < nt; a++) {
+      int32_t x = touched[a];
+      int64_t b = a - 1;
+      while (b >= 0 && touched[b] > x) { touched[b + 1] = touched[b]; b--; }
+      touched[b + 1] = x;
+    }
+    if (nnz + nt > cap) {
+      while (nnz + nt > cap) cap *= 2;
+      C.j = (int32_t *)realloc(C.j, sizeof(int32_t) * cap);
+      C.v = (float *)realloc(C.v, sizeof(float) * cap);
+    }
+    for (int64_t a = 0; a < nt; a++) {
+      const int32_t c = touched[a];
+      const float val = acc[c] / (float)len;
+      if (val != 0.0f) { C.j[nnz] = c; C.v[nnz] = val; nnz++; }
+      acc[c] = 0.0f;
+      seen[c] = 0;
+    }
+    C.p[r + 1] = nnz;
+  }
+  free(acc); free(seen); free(touched);
+  return C;
+}
+
+static void fcsr_free(fcsr *C) { free(C->p); free(C->j); free(C->v); }
+
+/* Exposed for tests: centroid CSR of rows R of (rp, col) over the features
+ * (frp, fcol, fval). Call with out_j == NULL for nnz (out_p filled). */
+int64_t hgref_centroids(int64_t R, const int32_t *rp, const int32_t *col,
+                        int64_t ncols, const int32_t *frp, const int32_t *fcol,
+                        const float *fval, int64_t *out_p, int32_t *out_j,
+                        float *out_v) {
+  fcsr C = centroids(R, rp, col, ncols, frp, fcol, fval);
+  const int64_t nnz = C.p[R];
+  if (out_p) memcpy(out_p, C.p, sizeof(int64_t) * (R + 1));
+  if (out_j) memcpy(out_j, C.j, sizeof(int32_t) * nnz);
+  if (out_v) memcpy(out_v, C.v, sizeof(float) * nnz);
+  fcsr_free(&C);
+  return nnz;
+}
+
+/* kind 0 nn, 1 ee, 2 ne; cn = node2edge_centroid (N rows over nodes),
+ * ce = edge2node_centroid (E rows over edges). */
+static float jac_prob(int kind, int32_t a, int32_t b, const int32_t *rp_n,
+                      const int32_t *col_n, const float *fn,
+                      const int32_t *rp_e, const int32_t *col_e,
+                      const float *fe, const fcsr *cn, const fcsr *ce) {
+  if (kind == 0)  /* SameTypeJaccardSample over node2features */
+    return swj(col_n + rp_n[a], fn + rp_n[a], rp_n[a + 1] - rp_n[a],
+               col_n + rp_n[b], fn + rp_n[b], rp_n[b + 1] - rp_n[b]);
+  if (kind == 1)
+    return swj(col_e + rp_e[a], fe + rp_e[a], rp_e[a + 1] - rp_e[a],
+               col_e + rp_e[b], fe + rp_e[b], rp_e[b + 1] - rp_e[b]);
+  /* DiffTypeJaccardSample (:343-392): v = a, e = b */
+  const float pn = swj(col_n + rp_n[a], fn + rp_n[a], rp_n[a + 1] - rp_n[a],
+                       ce->j + ce->p[b], ce->v + ce->p[b], ce->p[b + 1] - ce->p[b]);
+  const float pe = swj(col_e + rp_e[b], fe + rp_e[b], rp_e[b + 1] - rp_e[b],
+                       cn->j + cn->p[a], cn->v + cn->p[a], cn->p[a + 1] - cn->p[a]);
+  return pn * pe;
+}
+
+int64_t hgref_jaccard_sample(hgref_rng *s, int64_t N, int64_t E,
+                             const int32_t *rp_n, const int32_t *col_n,
+                             const int32_t *rp_e, const int32_t *col_e,
+                             const float *fn, const float *fe,
+                             const int32_t *node_q, const int32_t *edge_q,
+                             int K, int64_t cap, int32_t *idx, float *tgt) {
+  recbuf rb = {K, 0, cap, idx, tgt};
+  pat A = pat_view(N, rp_n, col_n), AT = pat_view(E, rp_e, col_e);
+  pairs P = {0, 0, NULL, NULL};
+  int64_t overflow = 0;
+  pat NN = spgemm_pattern(N, A.p, A.j, N, AT.p, AT.j);           /* :436 */
+  sample_pattern(s, &NN, N, node_q, 0, 0, &P, 0);                /* :439 */
+  for (int64_t t = 0; t < P.n; t++) {
+    int32_t *r = rec_slot(&rb);
+    if (!r) { overflow = 1; break; }
+    r[0] = P.a[t] + 1; r[2] = P.b[t] + 1;
+    rb.tgt[rb.n * 3 + 0] = jac_prob(0, P.a[t], P.b[t], rp_n, col_n, fn, rp_e,
+                                    col_e, fe, NULL, NULL);
+    rb.n++;
+  }
+  P.n = 0;
+  pat EE = spgemm_pattern(E, AT.p, AT.j, E, A.p, A.j);           /* :461 */
+  sample_pattern(s, &EE, E, edge_q, 0, 0, &P, 0);                /* :464 */
+  for (int64_t t = 0; t < P.n; t++) {
+    int32_t *r = rec_slot(&rb);
+    if (!r) { overflow = 1; break; }
+    r[1] = P.a[t] + 1; r[3] = P.b[t] + 1;
+    rb.tgt[rb.n * 3 + 1] = jac_prob(1, P.a[t], P.b[t], rp_n, col_n, fn, rp_e,
+                                    col_e, fe, NULL, NULL);
+    rb.n++;
+  }
+  /* :481-491 centroids: node2edge_centroid over edge2features (nodes),
+   * edge2node_centroid over node2features (edges) */
+  fcsr cn = centroids(N, rp_n, col_n, N, rp_e, col_e, fe);
+  fcsr ce = centroids(E, rp_e, col_e, E, rp_n, col_n, fn);
+  P.n = 0;
+  pat NNE = spgemm_pattern(N, NN.p, NN.j, E, A.p, A.j);          /* :493 */
+  sample_pattern(s, &NNE, E, node_q, 0, 0, &P, 0);
+  pat EEN = spgemm_pattern(E, EE.p, EE.j, N, AT.p, AT.j);        /* :498 */
+  sample_pattern(s, &EEN, N, edge_q, 0, 0, &P, 1);
+  hgref_rng w;  /* the single forked worker's copy of the parent stream */
+  hgref_rng_copy(&w, s);
+  for (int64_t t = 0; t < P.n; t++) {
+    int32_t v = P.a[t], e = P.b[t];
+    int32_t *r = rec_slot(&rb);
+    if (!r) { overflow = 1; break; }
+    r[0] = v + 1; r[3] = e + 1;
+    sample_neighbors(&w, A.j + A.p[v], A.p[v + 1] - A.p[v], K, r + 4 + K);
+    sample_neighbors(&w, AT.j + AT.p[e], AT.p[e + 1] - AT.p[e], K, r + 4);
+    rb.tgt[rb.n * 3 + 2] = jac_prob(2, v, e, rp_n, col_n, fn, rp_e, col_e, fe,
+                                    &cn, &ce);
+    rb.n++;
+  }
+  free(P.a); free(P.b);
+  fcsr_free(&cn); fcsr_free(&ce);
+  pat_free(&A); pat_free(&AT); pat_free(&NN); pat_free(&EE);
+  pat_free(&NNE); pat_free(&EEN);
+  return overflow ? -1 : rb.n;
+}
+
+/* Exposed: Jaccard probabilities for pair lists (kind 0/1/2 as above). */
+void hgref_jaccard_probs(int kind, int64_t n, const int32_t *pa,
+                         const int32_t *pb, int64_t N, int64_t E,
+                         const int32_t *rp_n, const int32_t *col_n,
+                         const int32_t *rp_e, const int32_t *col_e,
+                         const float *fn, const float *fe, float *out) {
+  fcsr cn = {0, 0, 0}, ce = {0, 0, 0};
+  if (kind == 2) {
+    cn = centroids(N, rp_n, col_n, N, rp_e, col_e, fe);
+    ce = centroids(E, rp_e, col_e, E, rp_n, col_n, fn);
+  }
+  for (int64_t t = 0; t < n; t++)
+    out[t] = jac_prob(kind, pa[t], pb[t], rp_n, col_n, fn, rp_e, col_e, fe,
+                      &cn, &ce);
+  if (kind == 2) { fcsr_free(&cn); fcsr_free(&ce); }
+}
+
+/* ------------------------------------------------------------------------- */
 /* Trainer: BooleanModel (hg2v_model.py:51-125, sigmoid heads + KLD) and      */
 /* UnweightedFloatModel (:129-203, relu heads + MSE), fit loop of            */
 /* embedding.py:269-305 -- Keras 2.x semantics restated (PARITY UNPINNED:    */

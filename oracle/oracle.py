@@ -72,6 +72,16 @@ def lib():
                               ctypes.c_float, ctypes.c_float, _int, _vp,
                               ctypes.c_float, _f32p,
                               ctypes.POINTER(ctypes.c_int)]
+    L.hgref_jaccard_sample.restype = _i64
+    L.hgref_jaccard_sample.argtypes = [_vp, _i64, _i64, _i32p, _i32p, _i32p,
+                                       _i32p, _f32p, _f32p, _i32p, _i32p, _int,
+                                       _i64, _i32p, _f32p]
+    L.hgref_jaccard_probs.argtypes = [_int, _i64, _i32p, _i32p, _i64, _i64,
+                                      _i32p, _i32p, _i32p, _i32p, _f32p, _f32p,
+                                      _f32p]
+    L.hgref_centroids.restype = _i64
+    L.hgref_centroids.argtypes = [_i64, _i32p, _i32p, _i64, _i32p, _i32p,
+                                  _f32p, _i64p, _vp, _vp]
     _lib = L
   return _lib
 
@@ -168,6 +178,50 @@ def hobe_sample(rng, inc, alg_node, alg_edge, S, K):
 
 
 HOBE_NN, HOBE_EE, HOBE_NE = 0, 1, 2
+JAC_NN, JAC_EE, JAC_NE = 0, 1, 2
+
+
+def jaccard_sample(rng, inc, fn, fe, node_q, edge_q, K):
+  """WeightedJaccardSamples (run_in_parallel=False) -> model input arrays.
+  fn / fe: feature values on A's pattern, node-major / edge-major order."""
+  fn = np.ascontiguousarray(fn, np.float32)
+  fe = np.ascontiguousarray(fe, np.float32)
+  node_q, edge_q = _q(node_q), _q(edge_q)
+  cap = 2 * int(node_q.sum()) + 2 * int(edge_q.sum()) + 1
+  idx = np.zeros((cap, 4 + 2 * K), np.int32)
+  tgt = np.zeros((cap, 3), np.float32)
+  n = lib().hgref_jaccard_sample(rng.h, inc.N, inc.E, inc.rp_n, inc.col_n,
+                                 inc.rp_e, inc.col_e, fn, fe, node_q, edge_q,
+                                 K, cap, idx, tgt)
+  assert n >= 0
+  return idx[:n].copy(), tgt[:n].copy()
+
+
+def jaccard_probs(kind, a, b, inc, fn, fe):
+  a = np.ascontiguousarray(a, np.int32)
+  b = np.ascontiguousarray(b, np.int32)
+  out = np.empty(a.size, np.float32)
+  lib().hgref_jaccard_probs(kind, a.size, a, b, inc.N, inc.E, inc.rp_n,
+                            inc.col_n, inc.rp_e, inc.col_e,
+                            np.ascontiguousarray(fn, np.float32),
+                            np.ascontiguousarray(fe, np.float32), out)
+  return out
+
+
+def centroids(R, rp, col, ncols, frp, fcol, fval):
+  """CSR (p int64, j, v) of GetAllCentroids."""
+  rp = np.ascontiguousarray(rp, np.int32)
+  col = np.ascontiguousarray(col, np.int32)
+  frp = np.ascontiguousarray(frp, np.int32)
+  fcol = np.ascontiguousarray(fcol, np.int32)
+  fval = np.ascontiguousarray(fval, np.float32)
+  p = np.empty(R + 1, np.int64)
+  nnz = lib().hgref_centroids(R, rp, col, ncols, frp, fcol, fval, p, None, None)
+  j = np.empty(nnz, np.int32)
+  v = np.empty(nnz, np.float32)
+  lib().hgref_centroids(R, rp, col, ncols, frp, fcol, fval, p, j.ctypes.data,
+                        v.ctypes.data)
+  return p, j, v
 
 
 def hobe_probs(kind, a, b, inc, alg_node, alg_edge):
