@@ -19,14 +19,16 @@ from .hypergraph_util import (AddNodeToEdge, CompressRange,
                               ToCsrMatrix, ToEdgeCsrMatrix)
 from .algebraic_distance import EmbedAlgebraicDistance
 from .hg2v_sample import (AlgebraicDistanceSamples, BooleanSamples,
-                          SamplesToModelInput, SimilarityRecord)
+                          SamplesToModelInput, SimilarityRecord,
+                          WeightedJaccardSamples)
 from .hg2v_weighting import UniformWeight, WeightByNeighborhood
 from .hg2v_model import (BooleanModel, KerasModelToEmbedding,
                          UnweightedFloatModel)
 from .proto_native import read_incidence, write_embedding
 from .embedding import (COMBINATION_OPTIONS, DEBUG_SUMMARY_OPTIONS,
                         EMBEDDING_OPTIONS, CombineEmbeddings, Embed,
-                        EmbedHg2vAlgDist, EmbedHg2vBoolean)
+                        EmbedHg2vAdjJaccard, EmbedHg2vAlgDist, EmbedHg2vBoolean,
+                        EmbedHg2vNeighborhoodWeightedJaccard)
 
 __all__ = [
     # proto
@@ -35,7 +37,8 @@ __all__ = [
     # embedding
     "Embed", "EMBEDDING_OPTIONS", "DEBUG_SUMMARY_OPTIONS",
     "COMBINATION_OPTIONS", "CombineEmbeddings", "EmbedHg2vBoolean",
-    "EmbedHg2vAlgDist", "EmbedAlgebraicDistance",
+    "EmbedHg2vAlgDist", "EmbedAlgebraicDistance", "EmbedHg2vAdjJaccard",
+    "EmbedHg2vNeighborhoodWeightedJaccard", "WeightedJaccardSamples",
     # hot-path pieces
     "BooleanSamples", "AlgebraicDistanceSamples", "SamplesToModelInput",
     "SimilarityRecord", "UniformWeight", "WeightByNeighborhood",

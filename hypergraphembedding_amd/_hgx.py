@@ -56,6 +56,10 @@ SIGNATURES = {
     "hgx_sample_fobe": (_int, [_vp, _u64, _int, _vp, _vp, _vp, _vp, _pi64]),
     "hgx_sample_hobe": (_int, [_vp, _u64, _int, _int, _pi64]),
     "hgx_sample_last_stats": (_int, [_vp, _pi64, _pi64]),
+    "hgx_features_set": (_int, [_vp, _vp, _vp]),
+    "hgx_sample_jaccard": (_int, [_vp, _u64, _int, _vp, _vp, _pi64]),
+    "hgx_jaccard_probs": (_int, [_vp, _int, _i64, _vp, _vp, _vp]),
+    "hgx_jaccard_centroids": (_int, [_vp, _int, _pi64, _vp, _vp, _vp]),
     "hgx_records_set": (_int, [_vp, _i64, _int, _vp, _vp]),
     "hgx_records_info": (_int, [_vp, _pi64, _pint]),
     "hgx_records_get": (_int, [_vp, _vp, _vp]),
@@ -247,6 +251,39 @@ class Context:
     self._chk(lib().hgx_sample_hobe(self.h, seed & (2**64 - 1), K, S,
                                     ctypes.byref(n)))
     return n.value
+
+  # weighted-Jaccard samplers
+  def features_set(self, node_major, edge_major):
+    fn, fe = _c(node_major, np.float32), _c(edge_major, np.float32)
+    assert fn.size == self.inc.nnz and fe.size == self.inc.nnz
+    self._chk(lib().hgx_features_set(self.h, _ptr(fn), _ptr(fe)))
+
+  def sample_jaccard(self, seed, K, node_q, edge_q):
+    nq, eq = _c(node_q, np.int32), _c(edge_q, np.int32)
+    n = ctypes.c_int64()
+    self._chk(lib().hgx_sample_jaccard(self.h, seed & (2**64 - 1), K, _ptr(nq),
+                                       _ptr(eq), ctypes.byref(n)))
+    return n.value
+
+  def jaccard_probs(self, kind, a, b):
+    a, b = _c(a, np.int32), _c(b, np.int32)
+    out = np.empty(a.size, np.float32)
+    self._chk(lib().hgx_jaccard_probs(self.h, kind, a.size, _ptr(a), _ptr(b),
+                                      _ptr(out)))
+    return out
+
+  def jaccard_centroids(self, which):
+    """(p int64, j int32, v float32) of the node (0) / edge (1) centroids."""
+    R = self.inc.N if which == 0 else self.inc.E
+    nnz = ctypes.c_int64()
+    self._chk(lib().hgx_jaccard_centroids(self.h, which, ctypes.byref(nnz),
+                                          None, None, None))
+    p = np.empty(R + 1, np.int64)
+    j = np.empty(nnz.value, np.int32)
+    v = np.empty(nnz.value, np.float32)
+    self._chk(lib().hgx_jaccard_centroids(self.h, which, ctypes.byref(nnz),
+                                          _ptr(p), _ptr(j), _ptr(v)))
+    return p, j, v
 
   def sample_stats(self):
     """(union-sampled 2-hop rows, fallbacks to expansion) of the last call."""

@@ -78,7 +78,9 @@ extern "C" int hgx_destroy(hgx_ctx *ctx) {
                     &ctx->blk_sn, &ctx->blk_el,
                     &ctx->rec_idx, &ctx->rec_tgt, &ctx->ntab, &ctx->etab,
                     &ctx->nacc, &ctx->eacc, &ctx->s0, &ctx->s1, &ctx->s2,
-                    &ctx->s3, &ctx->s4, &ctx->s5, &ctx->s6, &ctx->s7};
+                    &ctx->s3, &ctx->s4, &ctx->s5, &ctx->s6, &ctx->s7,
+                    &ctx->feat_n, &ctx->feat_e, &ctx->cn_p, &ctx->cn_j,
+                    &ctx->cn_v, &ctx->ce_p, &ctx->ce_j, &ctx->ce_v};
   for (DevBuf *b : bufs) hgx_release(*b);
   for (LongRows *l : {&ctx->long_n, &ctx->long_e, &ctx->long_sn, &ctx->long_el})
     for (DevBuf *b : {&l->seg, &l->off, &l->rows, &l->part}) hgx_release(*b);
@@ -168,6 +170,7 @@ extern "C" int hgx_upload_incidence(hgx_ctx *ctx, int32_t N, int32_t E,
   ctx->avg_deg_e = (double)nnz / E;
   ctx->k = 0;  // alg coords belong to the previous incidence
   ctx->n_rec = 0;
+  ctx->features_ok = ctx->centroids_ok = false;
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return HGX_OK;
 }

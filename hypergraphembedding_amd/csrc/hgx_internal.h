@@ -66,6 +66,12 @@ struct hgx_ctx {
   double alg_ms = 0, alg_bytes = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 
+  // weighted-Jaccard features (node-major / edge-major values on A's
+  // pattern) and the centroid CSRs built from them
+  DevBuf feat_n, feat_e, cn_p, cn_j, cn_v, ce_p, ce_j, ce_v;
+  int64_t cn_nnz = 0, ce_nnz = 0;
+  bool features_ok = false, centroids_ok = false;
+
   // sampler diagnostics of the last hgx_sample_* call
   int64_t sample_union_rows = 0, sample_fallback_rows = 0;
 

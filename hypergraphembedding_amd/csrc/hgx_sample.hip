@@ -879,6 +879,35 @@ extern "C" int hgx_sample_hobe(hgx_ctx *ctx, uint64_t seed, int K, int S,
   return HGX_OK;
 }
 
+// WeightedJaccardSamples pair blocks (hg2v_sample.py:436-505): nn (node
+// quotas), ee (edge quotas), ne from A A^T A rows (node quotas) then
+// A^T A A^T rows swapped (edge quotas); records allocated and emitted,
+// ne neighbours drawn; probabilities are left to the caller (hgx_jaccard).
+int hgx_sample_pairs4(hgx_ctx *ctx, uint64_t seed, int K, const int32_t *node_q,
+                      const int32_t *edge_q, int64_t *o_ee_out,
+                      int64_t *o_ne_out, int64_t *total_out) {
+  HGX_TRY(check_quota(ctx, node_q, ctx->N, "node"));
+  HGX_TRY(check_quota(ctx, edge_q, ctx->E, "edge"));
+  ctx->sample_union_rows = ctx->sample_fallback_rows = 0;
+  PatOut nn, ee, ne_n, ne_e;
+  HGX_TRY(run_pattern(ctx, PAT_NN, node_q, 0, seed, nn));
+  HGX_TRY(run_pattern(ctx, PAT_EE, edge_q, 0, seed, ee));
+  HGX_TRY(run_pattern(ctx, PAT_NNE, node_q, 0, seed, ne_n));
+  HGX_TRY(run_pattern(ctx, PAT_EEN, edge_q, 0, seed, ne_e));
+  const int64_t o_ee = nn.total, o_ne = o_ee + ee.total;
+  const int64_t o_en = o_ne + ne_n.total, total = o_en + ne_e.total;
+  HGX_TRY(alloc_records(ctx, total, K));
+  HGX_TRY(emit(ctx, REC_NN, nn, 0, 0.f));
+  HGX_TRY(emit(ctx, REC_EE, ee, o_ee, 0.f));
+  HGX_TRY(emit(ctx, REC_NE_NODE, ne_n, o_ne, 0.f));
+  HGX_TRY(emit(ctx, REC_NE_EDGE, ne_e, o_en, 0.f));
+  HGX_TRY(neighbors(ctx, o_ne, total, seed, 0x600));
+  *o_ee_out = o_ee;
+  *o_ne_out = o_ne;
+  *total_out = total;
+  return HGX_OK;
+}
+
 extern "C" int hgx_sample_last_stats(hgx_ctx *ctx, int64_t *union_rows,
                                      int64_t *fallback_rows) {
   if (!ctx) return HGX_EINVAL;

@@ -2,14 +2,16 @@
 
 Registry and signatures kept for the FOBE/HOBE path: ``Embed(args, hg)``
 (81-107), ``EMBEDDING_OPTIONS`` (423-444) with "ALG_DIST",
-"HG2V_BOOLEAN", "HG2V_ALG_DIST", "HG2V_BOOLEAN_NS", ``EmbedHg2vBoolean``
-(308-329), ``EmbedHg2vAlgDist`` (389-416), ``CombineEmbeddings`` (51-78).
+"HG2V_BOOLEAN", "HG2V_ALG_DIST", "HG2V_BOOLEAN_NS", "HG2V_ADJ_JAC",
+"HG2V_NEIGH_JAC", ``EmbedHg2vBoolean`` (308-329), ``EmbedHg2vAdjJaccard``
+(330-355), ``EmbedHg2vNeighborhoodWeightedJaccard`` (358-386),
+``EmbedHg2vAlgDist`` (389-416), ``CombineEmbeddings`` (51-78).
 
 ``_hypergraph2vec_skeleton`` (269-305) runs entirely on one device context:
 incidence upload -> sampler -> records stay in HBM -> tables initialised on
 device -> Keras-semantics fit -> rows idx+1 copied into the proto.
-The reference's other methods (SVD, NMF, node2vec, auto-encoder, Jaccard
-samplers) are outside this hot path: their keys raise like the reference's
+The reference's other methods (SVD, NMF, node2vec, auto-encoder) are
+outside this hot path: their keys raise like the reference's
 ``method_not_supported`` (419-420).
 """
 
@@ -20,7 +22,7 @@ import numpy as np
 from . import _hgx
 from .algebraic_distance import EmbedAlgebraicDistance, coords_to_embedding
 from .hg2v_model import Hg2vModel
-from .hg2v_sample import sample_fobe, sample_hobe
+from .hg2v_sample import sample_fobe, sample_hobe, sample_jaccard
 from .hypergraph_util import Incidence
 from .proto import HypergraphEmbedding
 from .runtime import get_context
@@ -174,6 +176,48 @@ def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
   return emb
 
 
+def _jaccard_embed(hypergraph, dimension, which, alpha, num_neighbors,
+                   num_samples, batch_size, epochs, debug_summary_path,
+                   disable_pbar):
+  """embedding.py:330-386: WeightedJaccardSamples over UniformWeight or
+  WeightByNeighborhood features, UnweightedFloatModel (relu, MSE)."""
+
+  def sampler_fn(inc, ctx):
+    ctx.upload(inc)
+    fn, fe = ctx.incidence_weights(which, float(alpha))
+    return sample_jaccard(inc, fn, fe, num_neighbors, num_samples, ctx=ctx)
+
+  return _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors,
+                                  sampler_fn, _hgx.LOSS_MSE, _hgx.ACT_RELU,
+                                  batch_size, epochs, debug_summary_path,
+                                  disable_pbar)
+
+
+def EmbedHg2vAdjJaccard(hypergraph, dimension, num_neighbors=5,
+                        num_samples=200, batch_size=256, epochs=10,
+                        debug_summary_path=None, disable_pbar=False):
+  """embedding.py:330-355 (UniformWeight features)."""
+  emb = _jaccard_embed(hypergraph, dimension, _hgx.WEIGHT_UNIFORM, 0.0,
+                       num_neighbors, num_samples, batch_size, epochs,
+                       debug_summary_path, disable_pbar)
+  emb.method_name = "HG2V_ADJ_JAC"
+  return emb
+
+
+def EmbedHg2vNeighborhoodWeightedJaccard(hypergraph, dimension, alpha=0,
+                                         num_neighbors=5, num_samples=200,
+                                         batch_size=256, epochs=10,
+                                         debug_summary_path=None,
+                                         disable_pbar=False):
+  """embedding.py:358-386 (WeightByNeighborhood(alpha) features)."""
+  assert 0 <= alpha <= 1
+  emb = _jaccard_embed(hypergraph, dimension, _hgx.WEIGHT_NEIGHBORHOOD, alpha,
+                       num_neighbors, num_samples, batch_size, epochs,
+                       debug_summary_path, disable_pbar)
+  emb.method_name = "HG2V_NEIGH_JAC"
+  return emb
+
+
 def method_not_supported(hypergraph, dim, **kwargs):
   raise RuntimeError(
       "Method not supported. Try making the embedding on your own.")
@@ -196,17 +240,19 @@ EMBEDDING_OPTIONS = {
     "N2V5_CLIQUE": method_not_supported,
     "N2V7_BIPARTIDE": method_not_supported,
     "N2V7_CLIQUE": method_not_supported,
-    "HG2V_ADJ_JAC": method_not_supported,
-    "HG2V_NEIGH_JAC": method_not_supported,
+    "HG2V_ADJ_JAC": EmbedHg2vAdjJaccard,
+    "HG2V_NEIGH_JAC": EmbedHg2vNeighborhoodWeightedJaccard,
     "metapath2vec++": method_not_supported,
     "deepwalk": method_not_supported,
     "LINE": method_not_supported,
     "BiNE": method_not_supported,
 }
 
-DEBUG_SUMMARY_OPTIONS = {"HG2V_BOOLEAN", "HG2V_ALG_DIST"}
+DEBUG_SUMMARY_OPTIONS = {"HG2V_BOOLEAN", "HG2V_ALG_DIST", "HG2V_ADJ_JAC",
+                         "HG2V_NEIGH_JAC"}
 
 __all__ = ["Embed", "EMBEDDING_OPTIONS", "DEBUG_SUMMARY_OPTIONS",
            "COMBINATION_OPTIONS", "CombineEmbeddings", "EmbedHg2vBoolean",
-           "EmbedHg2vAlgDist", "EmbedAlgebraicDistance",
+           "EmbedHg2vAlgDist", "EmbedAlgebraicDistance", "EmbedHg2vAdjJaccard",
+           "EmbedHg2vNeighborhoodWeightedJaccard",
            "CombineEmbeddingsViaConcatenation", "method_not_supported"]

@@ -17,6 +17,7 @@ numpy's global RNG, so np.random.seed(s) still makes runs reproducible.
 from collections import namedtuple
 
 import numpy as np
+import scipy.sparse as sp
 
 from . import _hgx
 from .hypergraph_util import Incidence
@@ -124,6 +125,57 @@ def AlgebraicDistanceSamples(hypergraph, algebraic_embedding, num_neighbors,
                      alg_coords=(x, y)).to_similarity_records()
 
 
+def _incidence_values(inc, m, node_major):
+  """Values of feature matrix m (node2features N x E, or edge2features
+  E x N) at the incidences of inc, in A's (node_major) or A^T's CSR order.
+  m must not have nonzeros outside the incidence pattern."""
+  m = sp.csr_matrix(m, dtype=np.float32)
+  if node_major:
+    rows = np.repeat(np.arange(inc.N), np.diff(inc.rp_n))
+    cols = inc.col_n
+    shape = (inc.N, inc.E)
+  else:
+    rows = np.repeat(np.arange(inc.E), np.diff(inc.rp_e))
+    cols = inc.col_e
+    shape = (inc.E, inc.N)
+  assert m.shape[0] >= shape[0] and m.shape[1] >= shape[1]
+  vals = np.asarray(m[rows, cols], dtype=np.float32).ravel()
+  outside = float(np.abs(m).sum()) - float(np.abs(vals).sum())
+  assert abs(outside) <= 1e-6 * max(1.0, float(np.abs(vals).sum())), \
+      "feature matrix has entries outside the incidence pattern"
+  return vals
+
+
+def sample_jaccard(inc, node_features, edge_features, num_neighbors,
+                   num_samples, ctx=None, seed=None):
+  """WeightedJaccardSamples on the device (features as per-incidence values,
+  node-major / edge-major); returns DeviceRecords."""
+  assert num_neighbors >= 1
+  assert num_samples >= 0
+  ctx = ctx or get_context()
+  ctx.upload(inc)
+  ctx.features_set(node_features, edge_features)
+  nq = _quotas(inc.node_weight, num_samples)
+  eq = _quotas(inc.edge_weight, num_samples)
+  n = ctx.sample_jaccard(numpy_seed() if seed is None else seed,
+                         num_neighbors, nq, eq)
+  return DeviceRecords(ctx, inc, n, num_neighbors)
+
+
+def WeightedJaccardSamples(hypergraph, node2features, edge2features,
+                           num_neighbors, num_samples, run_in_parallel=True,
+                           disable_pbar=False):
+  """hg2v_sample.py:395-510 (node2features N x E, edge2features E x N on
+  the compressed hypergraph's incidence pattern, e.g. UniformWeight /
+  WeightByNeighborhood)."""
+  del run_in_parallel, disable_pbar
+  inc = Incidence.from_hypergraph(hypergraph)
+  fn = _incidence_values(inc, node2features, True)
+  fe = _incidence_values(inc, edge2features, False)
+  return sample_jaccard(inc, fn, fe, num_neighbors,
+                        num_samples).to_similarity_records()
+
+
 def _same_type_dist_calc(indices, inc, alg_x, alg_y, is_edge, ctx=None):
   """hg2v_sample.py:527-543 for one pair (device computed, bit-exact)."""
   ctx = ctx or get_context()
@@ -206,5 +258,6 @@ def ModelInputToArrays(features, targets):
 
 
 __all__ = ["SimilarityRecord", "BooleanSamples", "AlgebraicDistanceSamples",
+           "WeightedJaccardSamples", "sample_jaccard",
            "SamplesToModelInput", "ModelInputToArrays", "DeviceRecords",
            "sample_fobe", "sample_hobe", "records_from_arrays"]

@@ -129,6 +129,25 @@ int hgx_sample_fobe(hgx_ctx *ctx, uint64_t seed, int K,
  * coords: quota S for every row, nn/ee/ne probabilities as above. */
 int hgx_sample_hobe(hgx_ctx *ctx, uint64_t seed, int K, int S,
                     int64_t *n_records);
+/* ---- weighted-Jaccard samples (HG2V_ADJ_JAC / HG2V_NEIGH_JAC) --------- *
+ * Replaces WeightedJaccardSamples (hg2v_sample.py:395-510) with
+ * SparseWeightedJaccard (:250-273) and GetAllCentroids (:276-326).
+ * Features: node2features / edge2features values on A's pattern (A's CSR
+ * order, A^T's CSR order), e.g. UniformWeight / WeightByNeighborhood
+ * (hg2v_weighting.py:137-198). Quotas are per row, int(weight * S). */
+int hgx_features_set(hgx_ctx *ctx, const float *node_major,
+                     const float *edge_major);
+int hgx_sample_jaccard(hgx_ctx *ctx, uint64_t seed, int K,
+                       const int32_t *node_quota, const int32_t *edge_quota,
+                       int64_t *n_records);
+/* kind 0 node-node, 1 edge-edge (SameTypeJaccardSample, :329-341), 2
+ * node-edge (DiffTypeJaccardSample, :343-392) for pairs (a[i], b[i]). */
+int hgx_jaccard_probs(hgx_ctx *ctx, int kind, int64_t n, const int32_t *a,
+                      const int32_t *b, float *out);
+/* The centroid CSR (which 0: node rows over nodes, 1: edge rows over
+ * edges); any output may be NULL (sizes first). */
+int hgx_jaccard_centroids(hgx_ctx *ctx, int which, int64_t *nnz,
+                          int64_t *rowptr, int32_t *col, float *val);
 /* Of the last hgx_sample_* call: 2-hop rows sampled from the union by
  * rejection (rows whose expansion exceeds HGX_SAMPLE_REJECT_W paths,
  * default 32768) and rows that fell back to expansion. */

@@ -234,9 +234,13 @@ def test_synthetic_generator_shape():
 # ---- registry / combination (embedding.py:51-107, 419-444) -----------------
 
 def test_registry_keys_and_unsupported():
+  from hypergraphembedding_amd.embedding import (
+      EmbedHg2vAdjJaccard, EmbedHg2vNeighborhoodWeightedJaccard)
   for key in ("ALG_DIST", "HG2V_BOOLEAN", "HG2V_ALG_DIST", "HG2V_BOOLEAN_NS"):
     assert callable(EMBEDDING_OPTIONS[key])
-  for key in ("SVD", "NMF", "AUTO_ENCODER", "N2V5_CLIQUE", "HG2V_ADJ_JAC"):
+  assert EMBEDDING_OPTIONS["HG2V_ADJ_JAC"] is EmbedHg2vAdjJaccard
+  assert EMBEDDING_OPTIONS["HG2V_NEIGH_JAC"] is EmbedHg2vNeighborhoodWeightedJaccard
+  for key in ("SVD", "NMF", "AUTO_ENCODER", "N2V5_CLIQUE", "N2V3_BIPARTIDE"):
     with pytest.raises(RuntimeError):
       EMBEDDING_OPTIONS[key](Hypergraph(), 2)
   with pytest.raises(RuntimeError):
