@@ -80,6 +80,8 @@ SIGNATURES = {
     "hgx_proto_write_embedding": (_int, [_i64, _vp, _vp, _i64, _vp, _vp, _int,
                                          ctypes.c_char_p, _vp, _i64, _pi64]),
     "hgx_host_last_error": (ctypes.c_char_p, []),
+    "hgx_proto_write_hypergraph": (_int, [_i32, _i32, _vp, _vp, _vp, _vp, _vp,
+                                          _vp, _vp, _i64, _pi64]),
 }
 
 
@@ -431,6 +433,23 @@ def write_embedding_bytes(node_ids, node_tab, edge_ids, edge_tab, method_name):
   out = np.empty(ln.value, np.uint8)
   rc = lib().hgx_proto_write_embedding(*args, _ptr(out), out.size,
                                        ctypes.byref(ln))
+  if rc != HGX_OK:
+    _host_raise(rc)
+  return out
+
+
+def write_hypergraph_bytes(inc):
+  """Hypergraph wire bytes of an Incidence (hgx_proto_write_hypergraph)."""
+  ids = (_c(inc.node_ids, np.int64), _c(inc.edge_ids, np.int64))
+  args = (inc.N, inc.E, _ptr(inc.rp_n), _ptr(inc.col_n), _ptr(inc.rp_e),
+          _ptr(inc.col_e), _ptr(ids[0]), _ptr(ids[1]))
+  ln = ctypes.c_int64()
+  rc = lib().hgx_proto_write_hypergraph(*args, None, 0, ctypes.byref(ln))
+  if rc != HGX_OK:
+    _host_raise(rc)
+  out = np.empty(ln.value, np.uint8)
+  rc = lib().hgx_proto_write_hypergraph(*args, _ptr(out), out.size,
+                                        ctypes.byref(ln))
   if rc != HGX_OK:
     _host_raise(rc)
   return out

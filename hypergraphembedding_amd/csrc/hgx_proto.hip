@@ -17,7 +17,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
-#include <unordered_map>
+#include <thread>
 #include <vector>
 
 #include "hgx.h"
@@ -79,6 +79,19 @@ struct Reader {
     }
   }
 };
+
+constexpr int kChunksP = 64;
+
+template <class F>
+void run_chunks(int n, F fn) {
+  const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; t++)
+    th.emplace_back([&, t] {
+      for (int c = t; c < n; c += nt) fn(c);
+    });
+  for (auto &x : th) x.join();
+}
 
 struct NodeRec {
   int32_t key;
@@ -160,8 +173,13 @@ extern "C" int hgx_proto_parse_hypergraph(const uint8_t *buf, int64_t len,
   }
   if (!r.ok) return host_fail(HGX_EINVAL, "malformed Hypergraph message");
 
-  // last entry per key wins (protobuf map semantics); stable order by key
+  // last entry per key wins (protobuf map semantics); order by key. Files
+  // written in key order (the common case) skip the sort.
   auto keep_last = [](auto &v, auto key_of) {
+    bool sorted = true;
+    for (size_t i = 1; i < v.size() && sorted; i++)
+      sorted = key_of(v[i - 1]) < key_of(v[i]);
+    if (sorted) return;
     std::vector<size_t> idx(v.size());
     for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
     std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
@@ -191,34 +209,68 @@ extern "C" int hgx_proto_parse_hypergraph(const uint8_t *buf, int64_t len,
     h->edge_ids[i] = edges[i].first;
     h->edge_w[i] = edges[i].second;
   }
-  h->rp_n.assign((size_t)h->N + 1, 0);
-  h->col_n.reserve(pool.size());
-  std::vector<int32_t> row;
-  for (int32_t i = 0; i < h->N; i++) {
-    const NodeRec &n = nodes[i];
-    h->node_ids[i] = n.key;
-    h->node_w[i] = n.weight;
-    row.clear();
-    for (int32_t t = 0; t < n.cnt; t++) {
-      const int32_t key = pool[n.off + t];
-      auto it = std::lower_bound(ekeys.begin(), ekeys.end(), key);
-      if (it == ekeys.end() || *it != key) {
-        delete h;
-        return host_fail(HGX_EINVAL, "node " + std::to_string(n.key) +
-                                         " lists edge " + std::to_string(key) +
-                                         " missing from hypergraph.edge");
+  // edge key -> compressed index: a direct table when the keys are dense
+  // enough, else binary search over the sorted keys
+  const int64_t kmin = h->E ? ekeys.front() : 0, kmax = h->E ? ekeys.back() : -1;
+  const bool dense = h->E && kmax - kmin < 8ll * h->E + 1024;
+  std::vector<int32_t> table;
+  if (dense) {
+    table.assign((size_t)(kmax - kmin + 1), -1);
+    for (int32_t i = 0; i < h->E; i++) table[(size_t)(ekeys[i] - kmin)] = i;
+  }
+  auto lookup = [&](int32_t key) -> int32_t {
+    if (dense) return (key < kmin || key > kmax) ? -1 : table[(size_t)(key - kmin)];
+    auto it = std::lower_bound(ekeys.begin(), ekeys.end(), key);
+    return (it == ekeys.end() || *it != key) ? -1 : (int32_t)(it - ekeys.begin());
+  };
+  // per node: map, sort, dedupe in place in the pool (node chunks on
+  // threads), then one prefix and a copy
+  std::vector<int32_t> cnt((size_t)h->N);
+  std::vector<int64_t> bad(kChunksP, -1);
+  const int32_t per = (h->N + kChunksP - 1) / kChunksP;
+  run_chunks(kChunksP, [&](int c) {
+    const int32_t v0 = std::min(h->N, c * per), v1 = std::min(h->N, v0 + per);
+    for (int32_t i = v0; i < v1; i++) {
+      const NodeRec &n = nodes[i];
+      int32_t *row = pool.data() + n.off;
+      for (int32_t t = 0; t < n.cnt; t++) {
+        const int32_t x = lookup(row[t]);
+        if (x < 0) {
+          bad[c] = ((int64_t)n.key << 32) | (uint32_t)row[t];
+          return;
+        }
+        row[t] = x;
       }
-      row.push_back((int32_t)(it - ekeys.begin()));
+      std::sort(row, row + n.cnt);
+      cnt[i] = (int32_t)(std::unique(row, row + n.cnt) - row);
     }
-    std::sort(row.begin(), row.end());
-    row.erase(std::unique(row.begin(), row.end()), row.end());
-    h->col_n.insert(h->col_n.end(), row.begin(), row.end());
-    if ((int64_t)h->col_n.size() >= INT32_MAX) {
+  });
+  for (int64_t x : bad)
+    if (x != -1) {
+      delete h;
+      return host_fail(HGX_EINVAL, "node " + std::to_string((int32_t)(x >> 32)) +
+                                       " lists edge " + std::to_string((int32_t)x) +
+                                       " missing from hypergraph.edge");
+    }
+  h->rp_n.assign((size_t)h->N + 1, 0);
+  int64_t run = 0;
+  for (int32_t i = 0; i < h->N; i++) {
+    h->node_ids[i] = nodes[i].key;
+    h->node_w[i] = nodes[i].weight;
+    run += cnt[i];
+    if (run >= INT32_MAX) {
       delete h;
       return host_fail(HGX_EUNSUP, "incidence count exceeds int32 CSR range");
     }
-    h->rp_n[i + 1] = (int32_t)h->col_n.size();
+    h->rp_n[i + 1] = (int32_t)run;
   }
+  h->col_n.resize((size_t)run);
+  run_chunks(kChunksP, [&](int c) {
+    const int32_t v0 = std::min(h->N, c * per), v1 = std::min(h->N, v0 + per);
+    for (int32_t i = v0; i < v1; i++)
+      std::copy(pool.data() + nodes[i].off, pool.data() + nodes[i].off + cnt[i],
+                h->col_n.data() + h->rp_n[i]);
+  });
   h->nnz = (int64_t)h->col_n.size();
   *out = h;
   if (N) *N = h->N;
@@ -331,6 +383,63 @@ extern "C" int hgx_proto_write_embedding(
     memcpy(p, method_name, mlen);
     p += mlen;
   }
+  return (size_t)(p - out) == total ? HGX_OK
+                                    : host_fail(HGX_EINVAL, "internal size mismatch");
+}
+
+// Hypergraph writer (bench / test data): node map entries {key, NodeData{
+// edges}} then edge map entries {key, EdgeData{nodes}}, repeated int32
+// unpacked (proto2's default, what Python protobuf writes), keys ascending
+// in the given id order, weights left at their default.
+namespace {
+size_t list_len(const int32_t *ids, const int64_t *map, int64_t n) {
+  size_t b = 0;
+  for (int64_t i = 0; i < n; i++) b += 1 + varint_len(key_bits(map[ids[i]]));
+  return b;
+}
+uint8_t *put_list_entry(uint8_t *p, int field, int64_t key, const int32_t *ids,
+                        const int64_t *map, int64_t n) {
+  const size_t inner = list_len(ids, map, n);
+  const size_t body = 1 + varint_len(key_bits(key)) + 1 + varint_len(inner) + inner;
+  p = put_varint(p, (uint64_t)(field << 3 | 2));
+  p = put_varint(p, body);
+  *p++ = 0x08;
+  p = put_varint(p, key_bits(key));
+  *p++ = 0x12;
+  p = put_varint(p, inner);
+  for (int64_t i = 0; i < n; i++) {
+    *p++ = 0x08;
+    p = put_varint(p, key_bits(map[ids[i]]));
+  }
+  return p;
+}
+size_t list_entry_len(int64_t key, const int32_t *ids, const int64_t *map, int64_t n) {
+  const size_t inner = list_len(ids, map, n);
+  const size_t body = 1 + varint_len(key_bits(key)) + 1 + varint_len(inner) + inner;
+  return 1 + varint_len(body) + body;
+}
+}  // namespace
+
+extern "C" int hgx_proto_write_hypergraph(
+    int32_t N, int32_t E, const int32_t *rp_n, const int32_t *col_n,
+    const int32_t *rp_e, const int32_t *col_e, const int64_t *node_ids,
+    const int64_t *edge_ids, uint8_t *out, int64_t cap, int64_t *len) {
+  if (!len || N < 0 || E < 0 || !rp_n || !col_n || !rp_e || !col_e || !node_ids ||
+      !edge_ids)
+    return host_fail(HGX_EINVAL, "bad hypergraph arguments");
+  size_t total = 0;
+  for (int32_t v = 0; v < N; v++)
+    total += list_entry_len(node_ids[v], col_n + rp_n[v], edge_ids, rp_n[v + 1] - rp_n[v]);
+  for (int32_t e = 0; e < E; e++)
+    total += list_entry_len(edge_ids[e], col_e + rp_e[e], node_ids, rp_e[e + 1] - rp_e[e]);
+  *len = (int64_t)total;
+  if (!out) return HGX_OK;
+  if (cap < (int64_t)total) return host_fail(HGX_EINVAL, "output buffer too small");
+  uint8_t *p = out;
+  for (int32_t v = 0; v < N; v++)
+    p = put_list_entry(p, 1, node_ids[v], col_n + rp_n[v], edge_ids, rp_n[v + 1] - rp_n[v]);
+  for (int32_t e = 0; e < E; e++)
+    p = put_list_entry(p, 2, edge_ids[e], col_e + rp_e[e], node_ids, rp_e[e + 1] - rp_e[e]);
   return (size_t)(p - out) == total ? HGX_OK
                                     : host_fail(HGX_EINVAL, "internal size mismatch");
 }

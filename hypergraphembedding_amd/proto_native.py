@@ -39,7 +39,8 @@ def read_incidence(src):
 
 
 def _from_parsed(p):
-  return Incidence(p["N"], p["E"], p["rp_n"], p["col_n"],
+  rp_e, col_e = _hgx.csr_transpose(p["N"], p["E"], p["rp_n"], p["col_n"])
+  return Incidence(p["N"], p["E"], p["rp_n"], p["col_n"], rp_e, col_e,
                    node_ids=p["node_ids"], edge_ids=p["edge_ids"],
                    node_weight=p["node_weight"], edge_weight=p["edge_weight"])
 

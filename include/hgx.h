@@ -214,6 +214,13 @@ int hgx_proto_write_embedding(int64_t n_nodes, const int64_t *node_ids,
                               const int64_t *edge_ids, const float *edge_tab,
                               int d, const char *method_name, uint8_t *out,
                               int64_t cap, int64_t *len);
+/* Hypergraph writer (test / bench data): compressed incidence + original
+ * ids -> wire bytes (repeated fields unpacked, proto2's default). */
+int hgx_proto_write_hypergraph(int32_t N, int32_t E, const int32_t *rowptr_n,
+                               const int32_t *col_n, const int32_t *rowptr_e,
+                               const int32_t *col_e, const int64_t *node_ids,
+                               const int64_t *edge_ids, uint8_t *out,
+                               int64_t cap, int64_t *len);
 /* Message of the last failed host utility call on this thread. */
 const char *hgx_host_last_error(void);
 /* CSR transpose by counting sort (rows of the result sorted). */

@@ -125,3 +125,18 @@ def test_native_powerlaw_roundtrip_scale():
   got = read_incidence(hg.SerializeToString())
   _same_incidence(got, Incidence.from_hypergraph(hg))
   assert np.array_equal(got.col_n, inc.col_n)
+
+
+def test_write_hypergraph_roundtrip():
+  from hypergraphembedding_amd import _hgx
+  from hypergraphembedding_amd.synthetic import powerlaw_hypergraph
+  inc = powerlaw_hypergraph(N=3_000, E=1_500, seed=6)
+  inc.node_ids = np.arange(inc.N, dtype=np.int64) * 3 - 4000
+  inc.edge_ids = np.arange(inc.E, dtype=np.int64) * 7 + 11
+  buf = _hgx.write_hypergraph_bytes(inc)
+  hg = Hypergraph()
+  hg.ParseFromString(buf.tobytes())
+  assert len(hg.node) == inc.N and len(hg.edge) == inc.E
+  _same_incidence(read_incidence(buf), Incidence.from_hypergraph(hg))
+  got = read_incidence(buf)
+  assert np.array_equal(got.col_n, inc.col_n) and np.array_equal(got.node_ids, inc.node_ids)
