@@ -266,3 +266,34 @@ def train(idx, tgt, K, node_tab, edge_tab, loss, act, batch=256, lr=0.01,
                     ea, loss, act, batch, lr, eps, max_epochs, pp, min_delta,
                     losses, ctypes.byref(ran))
   return nt, et, losses[:ran.value].copy(), na, ea
+
+
+_mt = None
+
+
+def train_mt(idx, tgt, K, node_tab, edge_tab, loss, act, batch=256, lr=0.01,
+             eps=1e-7, epochs=1, threads=0):
+  """Multi-threaded CPU baseline trainer (cpu_train_mt.c; records in the
+  given order). Updates copies of the tables; returns (nt, et, mean loss)."""
+  global _mt
+  if _mt is None:
+    build()
+    path = os.path.join(_HERE, "libcpumt.so")
+    if not os.path.exists(path):
+      subprocess.run(["make", "-C", _HERE, "-s"], check=True)
+    _mt = ctypes.CDLL(path)
+    _mt.cpu_train_mt.restype = _int
+    _mt.cpu_train_mt.argtypes = [_i64, _int, _i32p, _f32p, _int, _i64, _i64,
+                                 _f32p, _f32p, _f32p, _f32p, _int, _int, _int,
+                                 ctypes.c_float, ctypes.c_float, _int, _int,
+                                 ctypes.POINTER(ctypes.c_double)]
+  idx = np.ascontiguousarray(idx, np.int32)
+  tgt = np.ascontiguousarray(tgt, np.float32)
+  nt = np.ascontiguousarray(node_tab, np.float32).copy()
+  et = np.ascontiguousarray(edge_tab, np.float32).copy()
+  na, ea = np.zeros_like(nt), np.zeros_like(et)
+  lo = ctypes.c_double()
+  _mt.cpu_train_mt(idx.shape[0], K, idx, tgt, nt.shape[1], nt.shape[0],
+                   et.shape[0], nt, et, na, ea, loss, act, batch, lr, eps,
+                   epochs, threads, ctypes.byref(lo))
+  return nt, et, lo.value
