@@ -24,8 +24,9 @@ def test_train_mt_matches_oracle():
   nt = rs.uniform(-0.05, 0.05, (N + 2, d)).astype(np.float32)
   et = rs.uniform(-0.05, 0.05, (E + 2, d)).astype(np.float32)
   for loss, act in ((O.LOSS_MSE, O.ACT_RELU), (O.LOSS_KLD, O.ACT_SIGMOID)):
-    a_nt, a_et, _ = O.train(idx, tgt, K, nt, et, loss, act, max_epochs=1,
-                            min_delta=-1e30)
+    ref = O.train(idx, tgt, K, nt, et, loss, act, max_epochs=1,
+                  min_delta=-1e30)
+    a_nt, a_et = ref[0], ref[1]
     b_nt, b_et, _ = O.train_mt(idx, tgt, K, nt, et, loss, act, epochs=1,
                                threads=4)
     assert np.abs(a_nt - b_nt).max() < 1e-5
