@@ -29,7 +29,7 @@ res["proto_c4"] = {"bytes": int(buf.size), "nnz": big.nnz, "write_s": round(tw, 
                    "parse_s": round(tr, 2),
                    "parse_mb_per_s": round(buf.size / tr / 1e6, 1),
                    "parse_incidences_per_s": round(big.nnz / tr, 1),
-                   "cores": 1}
+                   "cores": "min(16, hardware_concurrency) threads"}
 del buf, inc, big
 # ---- proto reader vs Python protobuf, C3 ----
 c3 = random_hypergraph(seed=0)
