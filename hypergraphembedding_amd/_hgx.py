@@ -6,6 +6,7 @@ missing, every entry point raises.
 import ctypes
 import os
 import re
+import weakref
 
 import numpy as np
 
@@ -19,6 +20,7 @@ LOSS_KLD, LOSS_MSE = 0, 1
 ACT_SIGMOID, ACT_RELU = 0, 1
 HOBE_NN, HOBE_EE, HOBE_NE = 0, 1, 2
 WEIGHT_UNIFORM, WEIGHT_NEIGHBORHOOD, WEIGHT_DISTANCE = 0, 1, 2
+MLP_LP_CLASSIFIER, MLP_NE_SUPERVISED, MLP_NE_SEMI_SUPERVISED = 0, 1, 2
 
 _lib = None
 
@@ -82,6 +84,17 @@ SIGNATURES = {
     "hgx_host_last_error": (ctypes.c_char_p, []),
     "hgx_proto_write_hypergraph": (_int, [_i32, _i32, _vp, _vp, _vp, _vp, _vp,
                                           _vp, _vp, _i64, _pi64]),
+    "hgx_mlp_create": (_int, [_vp, _int, _int, _int, ctypes.POINTER(_vp)]),
+    "hgx_mlp_destroy": (_int, [_vp]),
+    "hgx_mlp_layers": (_int, [_vp, _pint, _vp]),
+    "hgx_mlp_set_weights": (_int, [_vp, _vp]),
+    "hgx_mlp_get_weights": (_int, [_vp, _vp]),
+    "hgx_mlp_set_tables": (_int, [_vp, _i64, _vp, _i64, _vp]),
+    "hgx_mlp_set_samples": (_int, [_vp, _i64, _vp, _vp, _vp]),
+    "hgx_mlp_fit": (_int, [_vp, _int, _int, _f32, _f32, _f32, _u64, _vp, _vp,
+                           _pint]),
+    "hgx_mlp_predict": (_int, [_vp, _int, _i64, _vp, _vp, _vp]),
+    "hgx_mlp_last_stats": (_int, [_vp, _pdbl, _pi64, _pi64, _pdbl]),
 }
 
 
@@ -142,9 +155,12 @@ class Context:
       _raise(rc, f"hgx_create(device={device}) failed: no usable HIP device")
     self.h = h
     self.device = device
+    self._engines = weakref.WeakSet()  # Mlp engines living on this context
 
   def close(self):
     if getattr(self, "h", None):
+      for e in list(getattr(self, "_engines", ())):
+        e.close()
       lib().hgx_destroy(self.h)
       self.h = None
 
@@ -348,6 +364,91 @@ class Context:
     self._chk(lib().hgx_train_last_stats(self.h, ctypes.byref(ms),
                                          ctypes.byref(rec), ctypes.byref(bat)))
     return ms.value, rec.value, bat.value
+
+
+class Mlp:
+  """One hgx_mlp engine (include/hgx.h, dense MLP section) on a Context."""
+
+  def __init__(self, ctx, kind, in_dim, out_dim=0):
+    self.ctx, self.kind, self.in_dim, self.out_dim = ctx, kind, in_dim, out_dim
+    h = _vp()
+    ctx._chk(lib().hgx_mlp_create(ctx.h, kind, in_dim, out_dim, ctypes.byref(h)))
+    self.h = h
+    ctx._engines.add(self)
+    n = ctypes.c_int()
+    ctx._chk(lib().hgx_mlp_layers(self.h, ctypes.byref(n), None))
+    sh = np.empty((n.value, 2), np.int32)
+    ctx._chk(lib().hgx_mlp_layers(self.h, ctypes.byref(n), _ptr(sh)))
+    self.shapes = [tuple(int(v) for v in r) for r in sh]
+
+  def close(self):
+    if getattr(self, "h", None):
+      lib().hgx_mlp_destroy(self.h)
+      self.h = None
+
+  def __del__(self):
+    try:
+      self.close()
+    except Exception:
+      pass
+
+  def num_weights(self):
+    return sum(k * n + n for k, n in self.shapes)
+
+  def set_weights(self, flat):
+    flat = _c(flat, np.float32)
+    assert flat.size == self.num_weights()
+    self.ctx._chk(lib().hgx_mlp_set_weights(self.h, _ptr(flat)))
+
+  def get_weights(self):
+    flat = np.empty(self.num_weights(), np.float32)
+    self.ctx._chk(lib().hgx_mlp_get_weights(self.h, _ptr(flat)))
+    return flat
+
+  def set_tables(self, node_tab, edge_tab):
+    nt, et = _c(node_tab, np.float32), _c(edge_tab, np.float32)
+    assert nt.ndim == 2 and et.ndim == 2
+    assert nt.shape[1] == self.in_dim and et.shape[1] == self.in_dim
+    self.ctx._chk(lib().hgx_mlp_set_tables(self.h, nt.shape[0], _ptr(nt),
+                                           et.shape[0], _ptr(et)))
+
+  def set_samples(self, node_row, edge_row, label):
+    nr, er = _c(node_row, np.int32), _c(edge_row, np.int32)
+    lab = _c(label, np.float32)
+    assert nr.shape == er.shape == lab.shape
+    self.ctx._chk(lib().hgx_mlp_set_samples(self.h, nr.size, _ptr(nr), _ptr(er),
+                                            _ptr(lab)))
+
+  def fit(self, batch=256, max_epochs=1, lr=0.01, eps=1e-7, min_delta=0.0,
+          seed=0, perms=None):
+    pp = None
+    if perms is not None:
+      pp = _c(perms, np.int64)
+      max_epochs = min(max_epochs, pp.shape[0])
+    losses = np.zeros(max(max_epochs, 1), np.float32)
+    ran = ctypes.c_int()
+    self.ctx._chk(lib().hgx_mlp_fit(self.h, batch, max_epochs, lr, eps,
+                                    min_delta, seed & (2**64 - 1), _ptr(pp),
+                                    _ptr(losses), ctypes.byref(ran)))
+    return losses[:ran.value].copy()
+
+  def predict(self, output, node_row=None, edge_row=None):
+    nr, er = _c(node_row, np.int32), _c(edge_row, np.int32)
+    n = (nr if nr is not None else er).size
+    shape = (n,) if output == 0 else (n, self.out_dim)
+    out = np.empty(shape, np.float32)
+    self.ctx._chk(lib().hgx_mlp_predict(self.h, output, n, _ptr(nr), _ptr(er),
+                                        _ptr(out)))
+    return out
+
+  def stats(self):
+    ms, fl = ctypes.c_double(), ctypes.c_double()
+    sm, bt = ctypes.c_int64(), ctypes.c_int64()
+    self.ctx._chk(lib().hgx_mlp_last_stats(self.h, ctypes.byref(ms),
+                                           ctypes.byref(sm), ctypes.byref(bt),
+                                           ctypes.byref(fl)))
+    return {"ms": ms.value, "samples": sm.value, "batches": bt.value,
+            "flops": fl.value}
 
 
 # ---- host utilities (no context, no device) --------------------------------

@@ -181,6 +181,59 @@ int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr, float eps,
 int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
                          int64_t *batches);
 
+/* ---- dense MLP engine (combiners + link-prediction classifier) --------- *
+ * Replaces the Keras models of
+ *   HGX_MLP_LP_CLASSIFIER       _TrainNodeEdgeEmbeddingClassifier +
+ *                               NodeEdgeEmbeddingPrediction
+ *                               (evaluation_util.py:471-552):
+ *                               [node | edge] -> Dense(in, relu) -> Dense(1,
+ *                               sigmoid); in = embedding.dim
+ *   HGX_MLP_NE_SUPERVISED       CombineEmbeddingsViaNodeEdgeClassifier(...,
+ *                               with_auto_encoder=False)
+ *                               (combine_embeddings_util.py:80-174); in =
+ *                               input_size, out = desired_dim
+ *   HGX_MLP_NE_SEMI_SUPERVISED  the same with with_auto_encoder=True
+ * Layers (Keras creation order; hgx_mlp_layers gives each kernel's K x N):
+ *   classifier: hidden, label
+ *   combiners:  pre_node, pre_edge, joint_node, joint_edge,
+ *               [post_node, post_edge, recovered_node, recovered_edge,]
+ *               hidden, label
+ * Weights travel flat: per layer the kernel (K x N, row-major) then the bias
+ * (N). Training = Keras fit: MSE, Adagrad(lr, eps, zero accumulators; a
+ * set_weights restarts them), batches sequential, Dropout(0.5) on the
+ * combiner inputs (mask from `seed`), EarlyStopping(monitor=loss,
+ * min_delta, patience=0). perms: NULL -> device shuffle per epoch, else
+ * max_epochs x n permutations. Samples reference table rows. */
+#define HGX_MLP_LP_CLASSIFIER 0
+#define HGX_MLP_NE_SUPERVISED 1
+#define HGX_MLP_NE_SEMI_SUPERVISED 2
+typedef struct hgx_mlp hgx_mlp;
+int hgx_mlp_create(hgx_ctx *ctx, int kind, int in_dim, int out_dim,
+                   hgx_mlp **out);
+int hgx_mlp_destroy(hgx_mlp *m);
+int hgx_mlp_layers(const hgx_mlp *m, int *n_layers, int32_t *shapes);
+int hgx_mlp_set_weights(hgx_mlp *m, const float *flat);
+int hgx_mlp_get_weights(hgx_mlp *m, float *flat);
+/* node_tab: node_rows x in_dim, edge_tab: edge_rows x in_dim (row-major) */
+int hgx_mlp_set_tables(hgx_mlp *m, int64_t node_rows, const float *node_tab,
+                       int64_t edge_rows, const float *edge_tab);
+/* (node row, edge row, label) per sample */
+int hgx_mlp_set_samples(hgx_mlp *m, int64_t n, const int32_t *node_row,
+                        const int32_t *edge_row, const float *label);
+int hgx_mlp_fit(hgx_mlp *m, int batch, int max_epochs, float lr, float eps,
+                float min_delta, uint64_t seed, const int64_t *perms,
+                float *epoch_loss, int *epochs_run);
+/* output 0: the label head per (node, edge) pair (n floats);
+ * 1 / 2: JointNode of node rows / JointEdge of edge rows (n x out_dim).
+ * Inference: no dropout. */
+int hgx_mlp_predict(hgx_mlp *m, int output, int64_t n, const int32_t *node_row,
+                    const int32_t *edge_row, float *out);
+/* Device time (ms, HIP events over the batch launches) of the last fit,
+ * samples and batches trained, algorithmic flops (fwd + bwd + weight
+ * gradients of the unpadded layers). */
+int hgx_mlp_last_stats(const hgx_mlp *m, double *ms, int64_t *samples,
+                       int64_t *batches, double *flops);
+
 /* ---- host utilities (bench / test data; not reference entry points) --- *
  * Power-law synthetic incidence of SURVEY.md §8(d) (C4/C5): node degree
  * 1 + Poisson(mean_degree - 1), distinct edges per node drawn with

@@ -297,3 +297,72 @@ def train_mt(idx, tgt, K, node_tab, edge_tab, loss, act, batch=256, lr=0.01,
                    et.shape[0], nt, et, na, ea, loss, act, batch, lr, eps,
                    epochs, threads, ctypes.byref(lo))
   return nt, et, lo.value
+
+_mlp = None
+
+
+def _mlp_lib():
+  global _mlp
+  if _mlp is None:
+    path = os.path.join(_HERE, "libmlpref.so")
+    src = os.path.join(_HERE, "mlpref.c")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+      subprocess.run(["make", "-C", _HERE, "-s", "libmlpref.so"], check=True)
+    L = ctypes.CDLL(path)
+    L.mlpref_num_weights.argtypes = [_int, _int, _int, ctypes.POINTER(_i64)]
+    L.mlpref_fit.restype = _int
+    L.mlpref_fit.argtypes = [_int, _int, _int, _f32p, _i64, _f32p, _i64, _f32p,
+                             _i64, _i32p, _i32p, _f32p, _int, _int,
+                             ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                             ctypes.c_uint64, _i64p, _i64, _f32p,
+                             ctypes.POINTER(ctypes.c_int)]
+    L.mlpref_predict.restype = _int
+    L.mlpref_predict.argtypes = [_int, _int, _int, _f32p, _i64, _f32p, _i64,
+                                 _f32p, _int, _i64, _vp, _vp, _f32p]
+    _mlp = L
+  return _mlp
+
+
+def mlp_num_weights(kind, in_dim, out_dim):
+  n = _i64()
+  _mlp_lib().mlpref_num_weights(kind, in_dim, out_dim, ctypes.byref(n))
+  return n.value
+
+
+def mlp_fit(kind, in_dim, out_dim, weights, node_tab, edge_tab, node_row,
+            edge_row, label, perms, batch=256, lr=0.01, eps=1e-7, min_delta=0.0,
+            seed=0, max_batches=0):
+  """mlpref.c: Keras-semantics fit of the combiner / classifier MLP with the
+  device's dropout masks; batches in `perms` order (epochs x n). Returns
+  (weights after training, epoch losses)."""
+  w = np.ascontiguousarray(weights, np.float32).copy()
+  nt = np.ascontiguousarray(node_tab, np.float32)
+  et = np.ascontiguousarray(edge_tab, np.float32)
+  nr = np.ascontiguousarray(node_row, np.int32)
+  er = np.ascontiguousarray(edge_row, np.int32)
+  lab = np.ascontiguousarray(label, np.float32)
+  perms = np.ascontiguousarray(perms, np.int64)
+  epochs = perms.shape[0]
+  losses = np.zeros(max(epochs, 1), np.float32)
+  ran = ctypes.c_int()
+  _mlp_lib().mlpref_fit(kind, in_dim, out_dim, w, nt.shape[0], nt, et.shape[0],
+                        et, nr.size, nr, er, lab, batch, epochs, lr, eps,
+                        min_delta, seed & (2**64 - 1), perms, max_batches,
+                        losses, ctypes.byref(ran))
+  return w, losses[:ran.value].copy()
+
+
+def mlp_predict(kind, in_dim, out_dim, weights, node_tab, edge_tab, output,
+                node_row=None, edge_row=None):
+  w = np.ascontiguousarray(weights, np.float32)
+  nt = np.ascontiguousarray(node_tab, np.float32)
+  et = np.ascontiguousarray(edge_tab, np.float32)
+  nr = None if node_row is None else np.ascontiguousarray(node_row, np.int32)
+  er = None if edge_row is None else np.ascontiguousarray(edge_row, np.int32)
+  n = (nr if nr is not None else er).size
+  out = np.empty(n if output == 0 else n * out_dim, np.float32)
+  _mlp_lib().mlpref_predict(kind, in_dim, out_dim, w, nt.shape[0], nt,
+                            et.shape[0], et, output, n,
+                            None if nr is None else nr.ctypes.data,
+                            None if er is None else er.ctypes.data, out)
+  return out if output == 0 else out.reshape(n, out_dim)
