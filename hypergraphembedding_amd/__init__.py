@@ -25,6 +25,11 @@ from .hg2v_weighting import UniformWeight, WeightByNeighborhood
 from .hg2v_model import (BooleanModel, KerasModelToEmbedding,
                          UnweightedFloatModel)
 from .proto_native import read_incidence, write_embedding
+from .combine_embeddings_util import (CombineEmbeddingsViaConcatenation,
+                                      CombineEmbeddingsViaNodeEdgeClassifier)
+from .evaluation_util import (EXPERIMENT_OPTIONS, CalculateCommunityPredictionMetrics,
+                              NodeEdgeEmbeddingPrediction, RemoveRandomConnections,
+                              RunLinkPredictionExperiment, SampleMissingConnections)
 from .embedding import (COMBINATION_OPTIONS, DEBUG_SUMMARY_OPTIONS,
                         EMBEDDING_OPTIONS, CombineEmbeddings, Embed,
                         EmbedHg2vAdjJaccard, EmbedHg2vAlgDist, EmbedHg2vBoolean,
@@ -49,4 +54,10 @@ __all__ = [
     "ToEdgeCsrMatrix", "ToCscMatrix", "Relabel", "CompressRange", "Incidence",
     # native proto I/O
     "read_incidence", "write_embedding",
+    # combiners and link-prediction evaluation
+    "CombineEmbeddingsViaConcatenation",
+    "CombineEmbeddingsViaNodeEdgeClassifier", "EXPERIMENT_OPTIONS",
+    "CalculateCommunityPredictionMetrics", "NodeEdgeEmbeddingPrediction",
+    "RemoveRandomConnections", "RunLinkPredictionExperiment",
+    "SampleMissingConnections",
 ]

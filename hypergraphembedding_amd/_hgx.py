@@ -95,6 +95,11 @@ SIGNATURES = {
                            _pint]),
     "hgx_mlp_predict": (_int, [_vp, _int, _i64, _vp, _vp, _vp]),
     "hgx_mlp_last_stats": (_int, [_vp, _pdbl, _pi64, _pi64, _pdbl]),
+    "hgx_pyrandom_sample_missing": (_int, [_vp, _i32, _i32, _vp, _vp, _i64,
+                                           _vp, _vp, _pi64]),
+    "hgx_pyrandom_remove_connections": (_int, [_vp, _i64, _vp, _vp, _vp, _vp,
+                                               ctypes.c_double, _vp, _pi64]),
+    "hgx_lp_last_error": (ctypes.c_char_p, []),
 }
 
 
@@ -554,3 +559,50 @@ def write_hypergraph_bytes(inc):
   if rc != HGX_OK:
     _host_raise(rc)
   return out
+
+
+# ---- Python-`random`-compatible link-prediction loops (host) ---------------
+def _mt_state(rnd):
+  ver, st, gauss = rnd.getstate()
+  return np.array(st, np.uint32), (ver, gauss)
+
+
+def _mt_restore(rnd, arr, meta):
+  rnd.setstate((meta[0], tuple(int(v) for v in arr), meta[1]))
+
+
+def _lp_chk(rc):
+  if rc != HGX_OK:
+    _raise(rc, lib().hgx_lp_last_error().decode())
+
+
+def pyrandom_sample_missing(rnd, n_nodes, n_edges, rowptr, col, num_samples):
+  """(node positions, edge positions) drawn as SampleMissingConnections
+  draws them with the `random.Random` instance `rnd` (advanced)."""
+  st, meta = _mt_state(rnd)
+  rp = _c(rowptr, np.int64)
+  cl = _c(col, np.int32)
+  npos = np.empty(max(num_samples, 1), np.int32)
+  epos = np.empty(max(num_samples, 1), np.int32)
+  got = ctypes.c_int64()
+  _lp_chk(lib().hgx_pyrandom_sample_missing(
+      _ptr(st), n_nodes, n_edges, _ptr(rp), _ptr(cl), num_samples, _ptr(npos),
+      _ptr(epos), ctypes.byref(got)))
+  _mt_restore(rnd, st, meta)
+  return npos[:got.value].copy(), epos[:got.value].copy()
+
+
+def pyrandom_remove_connections(rnd, pair_node, pair_edge, node_deg,
+                                edge_size, probability):
+  """Indices of the pairs RemoveRandomConnections removes, in order."""
+  st, meta = _mt_state(rnd)
+  pn, pe = _c(pair_node, np.int32), _c(pair_edge, np.int32)
+  nd = np.array(node_deg, np.int32)
+  es = np.array(edge_size, np.int32)
+  out = np.empty(max(pn.size, 1), np.int64)
+  got = ctypes.c_int64()
+  _lp_chk(lib().hgx_pyrandom_remove_connections(
+      _ptr(st), pn.size, _ptr(pn), _ptr(pe), _ptr(nd), _ptr(es),
+      float(probability), _ptr(out), ctypes.byref(got)))
+  _mt_restore(rnd, st, meta)
+  return out[:got.value].copy()

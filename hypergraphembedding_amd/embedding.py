@@ -21,6 +21,8 @@ import numpy as np
 
 from . import _hgx
 from .algebraic_distance import EmbedAlgebraicDistance, coords_to_embedding
+from .combine_embeddings_util import (CombineEmbeddingsViaConcatenation,
+                                      CombineEmbeddingsViaNodeEdgeClassifier)
 from .hg2v_model import Hg2vModel
 from .hg2v_sample import sample_fobe, sample_hobe, sample_jaccard
 from .hypergraph_util import Incidence
@@ -30,34 +32,16 @@ from .runtime import get_context
 log = logging.getLogger()
 
 COMBINATION_OPTIONS = [
-    "N_E_SUPERVISED",  # default @ 0 (reference); Keras MLP combiner, not here
+    "N_E_SUPERVISED",  # default @ 0 (reference)
     "N_E_SEMI_SUPERVISED",
     "CONCATENATE",
 ]
 
 
-def CombineEmbeddingsViaConcatenation(hypergraph, embeddings):
-  """combine_embeddings_util.py:27-41."""
-  emb = HypergraphEmbedding()
-  emb.dim = sum(e.dim for e in embeddings)
-  for node_idx in hypergraph.node:
-    vec = []
-    for e in embeddings:
-      vec.extend(e.node[node_idx].values)
-    emb.node[node_idx].values.extend(np.asarray(vec, np.float32).tolist())
-  for edge_idx in hypergraph.edge:
-    vec = []
-    for e in embeddings:
-      vec.extend(e.edge[edge_idx].values)
-    emb.edge[edge_idx].values.extend(np.asarray(vec, np.float32).tolist())
-  return emb
-
-
 def CombineEmbeddings(args, hypergraph, embeddings, disable_pbar=False):
-  """embedding.py:51-78. CONCATENATE is supported; the Keras MLP combiners
-  (N_E_SUPERVISED / N_E_SEMI_SUPERVISED) are the next component (SURVEY
-  §8f) and raise NotImplementedError here."""
-  del disable_pbar
+  """embedding.py:51-78: CONCATENATE, or the node/edge-classifier MLP
+  combiners (N_E_SUPERVISED, N_E_SEMI_SUPERVISED) on the MI355X dense-MLP
+  engine (combine_embeddings_util.py)."""
   assert len(embeddings) >= 1
   if len(embeddings) == 1:
     return embeddings[0]
@@ -66,9 +50,10 @@ def CombineEmbeddings(args, hypergraph, embeddings, disable_pbar=False):
     comb = CombineEmbeddingsViaConcatenation(hypergraph, embeddings)
     args.embedding_dimension = comb.dim
   elif strategy in ("N_E_SUPERVISED", "N_E_SEMI_SUPERVISED"):
-    raise NotImplementedError(
-        f"combination strategy {strategy} (Keras MLP combiner) is outside "
-        "the FOBE/HOBE hot path; use CONCATENATE")
+    comb = CombineEmbeddingsViaNodeEdgeClassifier(
+        hypergraph, embeddings, args.embedding_dimension,
+        with_auto_encoder=strategy == "N_E_SEMI_SUPERVISED",
+        disable_pbar=disable_pbar)
   else:
     raise ValueError("Args contains an illegal embedding-combination-strategy")
   comb.method_name = "_".join(args.embedding_method)

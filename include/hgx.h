@@ -274,6 +274,28 @@ int hgx_proto_write_hypergraph(int32_t N, int32_t E, const int32_t *rowptr_n,
                                const int32_t *col_e, const int64_t *node_ids,
                                const int64_t *edge_ids, uint8_t *out,
                                int64_t cap, int64_t *len);
+/* ---- link prediction, Python `random` semantics (host) ------------------ *
+ * state: the 625 ints of random.getstate()[1] (MT19937 words + position),
+ * advanced in place exactly as CPython's `random` would be.
+ * SampleMissingConnections (evaluation_util.py:125-158): nodes / edges are
+ * list positions (the map iteration order the caller saw); rowptr/col = each
+ * node's edges as sorted edge positions. Outputs the distinct accepted
+ * (node, edge) positions in insertion order (num_samples capacity). */
+int hgx_pyrandom_sample_missing(uint32_t *state, int32_t n_nodes,
+                                int32_t n_edges, const int64_t *rowptr,
+                                const int32_t *col, int64_t num_samples,
+                                int32_t *node_pos, int32_t *edge_pos,
+                                int64_t *n_out);
+/* RemoveRandomConnections (evaluation_util.py:84-122): pairs in the
+ * reference's node_edges order, current degrees (decremented in place);
+ * outputs the indices of the removed pairs in removal order. */
+int hgx_pyrandom_remove_connections(uint32_t *state, int64_t n_pairs,
+                                    const int32_t *pair_node,
+                                    const int32_t *pair_edge,
+                                    int32_t *node_deg, int32_t *edge_size,
+                                    double probability, int64_t *removed,
+                                    int64_t *n_removed);
+const char *hgx_lp_last_error(void);
 /* Message of the last failed host utility call on this thread. */
 const char *hgx_host_last_error(void);
 /* CSR transpose by counting sort (rows of the result sorted). */

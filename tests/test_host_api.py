@@ -270,6 +270,6 @@ def test_combine_concatenate():
   assert comb.method_name == "A_B"
   assert list(comb.node[1].values) == [1, 1.5, 11, 11.5]
   assert list(comb.edge[5].values) == [-5, 0, 5, 10]
-  args.embedding_combination_strategy = "N_E_SUPERVISED"
-  with pytest.raises(NotImplementedError):
+  args.embedding_combination_strategy = "NOT_A_STRATEGY"
+  with pytest.raises(ValueError):
     CombineEmbeddings(args, h, embs)
