@@ -145,13 +145,16 @@ def main():
   sync()
   t0 = time.perf_counter()
   dev_ms = 0.0
-  batches = 0
+  batches = fused_b = split_b = 0
   for s in range(args.steps):
     ctx.train(batch=args.batch, max_epochs=1, loss=_hgx.LOSS_MSE,
               act=_hgx.ACT_RELU, min_delta=-1e30, shuffle_seed=200 + s)
     ms, rec, bat = ctx.train_stats()
+    fz, sp = ctx.train_path_stats()
     dev_ms += ms
     batches += bat
+    fused_b += fz
+    split_b += sp
   barrier()
   sync()
   elapsed = time.perf_counter() - t0
@@ -163,7 +166,8 @@ def main():
   records = n * args.steps * world
   value = records / elapsed
 
-  # ---- roofline of the dominant kernel: one batch step (K1 + K2) ----
+  # ---- roofline of the dominant kernel: one batch step (train_fused, or
+  # K1 + K2 for the batches that do not pack) ----
   b_rec = 224.0 * args.dim + 68.0  # SURVEY §8d algorithmic bytes / record
   per_batch_ms = dev_ms / max(batches, 1)
   batch_bytes = b_rec * (n * args.steps / max(batches, 1))
@@ -176,7 +180,10 @@ def main():
   roofline = {"bound": "hbm", "achieved": round(achieved, 1),
               "peak": HBM_PEAK_GBPS, "unit": "GB/s",
               "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-              "kernel": "train_fwd_bwd+train_update (one batch step)",
+              "kernel": ("train_fused (one launch per batch step)" if fused_b
+                         else "train_fwd_bwd+train_update (one batch step)"),
+              "batch_steps": {"train_fused": fused_b,
+                              "train_fwd_bwd+train_update": split_b},
               "per_launch_us": round(per_batch_ms * 1e3, 2),
               "algorithmic_bytes_per_launch": round(batch_bytes)}
 

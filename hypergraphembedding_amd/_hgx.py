@@ -70,6 +70,7 @@ SIGNATURES = {
     "hgx_train": (_int, [_vp, _int, _int, _f32, _f32, _int, _int, _f32, _u64,
                          _vp, _vp, _pint]),
     "hgx_train_last_stats": (_int, [_vp, _pdbl, _pi64, _pi64]),
+    "hgx_train_path_stats": (_int, [_vp, _pi64, _pi64]),
     "hgx_synth_powerlaw": (_int, [_i32, _i32, ctypes.c_double, ctypes.c_double,
                                   _u64, _vp, _vp, _pi64,
                                   ctypes.POINTER(ctypes.c_int32)]),
@@ -369,6 +370,13 @@ class Context:
     self._chk(lib().hgx_train_last_stats(self.h, ctypes.byref(ms),
                                          ctypes.byref(rec), ctypes.byref(bat)))
     return ms.value, rec.value, bat.value
+
+  def train_path_stats(self):
+    """(fused, split) batch counts of the last train() call."""
+    f, sp = ctypes.c_int64(), ctypes.c_int64()
+    self._chk(lib().hgx_train_path_stats(self.h, ctypes.byref(f),
+                                         ctypes.byref(sp)))
+    return f.value, sp.value
 
 
 class Mlp:

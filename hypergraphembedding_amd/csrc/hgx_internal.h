@@ -86,6 +86,7 @@ struct hgx_ctx {
   DevBuf ntab, etab, nacc, eacc;
   double train_ms = 0, train_epoch_ms = 0;
   int64_t train_records = 0, train_batches = 0;
+  int64_t train_fused = 0, train_split = 0;
 
   // ---- scratch ----
   DevBuf s0, s1, s2, s3, s4, s5, s6, s7;

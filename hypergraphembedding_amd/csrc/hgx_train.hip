@@ -85,9 +85,26 @@ struct TrainArgs {
   int *inv, *ukey, *uoff, *ucount;
   int2 *bmeta;  // per chunk-local batch: {records (0 = no batch), global batch}
   int SB, nblk1;
+  int lstride;  // per-batch stride of lossbuf (>= the blocks of either path)
   float lr, eps;
   int loss, act;
+  // fused path (train_fused): records packed so that every row touched by
+  // more than one slot of a batch has all its slots in ONE workgroup.
+  // Per chunk-local batch: NBF workgroups x prpb groups of R ids / codes / 3
+  // targets, valid groups per workgroup, and whether the batch packed.
+  int fused, prpb, NBF, MS;
+  int *pidx, *pcode, *pnval, *pnblk, *pfast;
+  float *ptgt;
+  float *r0;  // [2 parity][2 table][p, acc][dp]: padding-row state handed on
+  float *gp;  // [2 parity][NBF][2 table][dp]: padding-row partials per block
 };
+
+// slot codes of the fused path (train_prep -> train_fused)
+constexpr unsigned kCodeMulti = 0x80000000u;  // row has >1 slot: LDS pos
+constexpr unsigned kCodeOwn = 0x40000000u;    // this slot applies the update
+constexpr int kPackB = 512;                   // max records per fused batch
+constexpr int kPackM = 1024;                  // max multi-slot rows per batch
+constexpr int kPackNBF = 64;                  // max fused workgroups per batch
 
 __device__ __forceinline__ bool slot_is_edge(int s, int K) {
   return s == 1 || s == 3 || s >= 4 + K;
@@ -313,7 +330,7 @@ __global__ __launch_bounds__(TB) void train_fwd_bwd(TrainArgs a, int cb) {
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int g = 0; g < RPB; g++) s += s_loss[g];
-    a.lossbuf[(size_t)bm.y * a.nblk1 + blockIdx.x] = s;
+    a.lossbuf[(size_t)bm.y * a.lstride + blockIdx.x] = s;
   }
   HGX_STAMP(ts[5]);
   trace_put(bm.y, 0, 6, ts);
@@ -331,6 +348,22 @@ __device__ __forceinline__ void adagrad4(float4 &p, float4 &ac, float4 g,
     aa[c] = na;
     pp[c] = __fsub_rn(pp[c], __fdiv_rn(__fmul_rn(lr, gv[c]),
                                        __fadd_rn(sqrtf(na), eps)));
+  }
+}
+
+// The same update with the hardware square root and reciprocal (<= 1 ulp
+// each; the fused step runs every row update of a record on one wave, where
+// the correctly rounded sequences cost ~30 instructions per element).
+__device__ __forceinline__ void adagrad4_hw(float4 &p, float4 &ac, float4 g,
+                                            float lr, float eps) {
+  float *pp = &p.x, *aa = &ac.x;
+  const float *gv = &g.x;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const float na = __fadd_rn(aa[c], __fmul_rn(gv[c], gv[c]));
+    aa[c] = na;
+    const float den = __fadd_rn(__builtin_amdgcn_sqrtf(na), eps);
+    pp[c] = __fsub_rn(pp[c], __fmul_rn(__fmul_rn(lr, gv[c]), __builtin_amdgcn_rcpf(den)));
   }
 }
 
@@ -433,6 +466,304 @@ __global__ __launch_bounds__(TB) void train_update(TrainArgs a, int cb) {
   trace_put(bm.y, 1, 4, ts);
 }
 
+// Padding-row (row 0) state for the fused path, computed by every workgroup
+// of a batch (identical inputs and order, so identical values): mode 0 ->
+// the tables hold it; mode 1 -> it is pending from the previous fused batch:
+// (p, acc) = Adagrad(r0src, sum of that batch's np per-workgroup partials).
+// row0_issue starts every load unconditionally (a load under a branch is
+// waited for at the join), first thing in the kernel; row0_finish sums in a
+// fixed order (thread `sub` of a column: partials sub, sub+TPC, ...; then
+// the TPC sums in order) and returns the column's (p, acc) on sub == 0.
+// col < 2L covers both tables (table = col / L, float4 column col % L).
+template <int L, int TB>
+struct Row0Loads {
+  static constexpr int NC = 2 * L, TPC = TB / NC, MAXPER = kPackNBF / TPC;
+  float4 gv[MAXPER];
+  float4 rp, ra, tp, ta;
+};
+
+template <int L, int TB>
+__device__ __forceinline__ void row0_issue_state(const TrainArgs &a,
+                                                 const float4 *r0src,
+                                                 Row0Loads<L, TB> &ld) {
+  using RL = Row0Loads<L, TB>;
+  static_assert(TB % RL::NC == 0, "workgroup covers whole columns");
+  const int col = threadIdx.x % RL::NC;
+  const int tab = col / L, c = col % L;
+  ld.rp = r0src[(tab * 2) * L + c];
+  ld.ra = r0src[(tab * 2 + 1) * L + c];
+  ld.tp = reinterpret_cast<const float4 *>(tab ? a.etab : a.ntab)[c];
+  ld.ta = reinterpret_cast<const float4 *>(tab ? a.eacc : a.nacc)[c];
+}
+
+// partials [0, nmax) of gpsrc (nmax <= kPackNBF), issued unconditionally
+// (index clamped: a branch around a load makes the compiler wait for it at
+// the join); row0_stage masks the clamped copies (the gp buffer is zeroed at
+// hgx_train entry, so it only ever holds finite partials).
+template <int L, int TB>
+__device__ __forceinline__ void row0_issue_partials(int nmax, const float4 *gpsrc,
+                                                    Row0Loads<L, TB> &ld) {
+  using RL = Row0Loads<L, TB>;
+  const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
+  const int last = max(nmax - 1, 0);
+#pragma unroll
+  for (int u = 0; u < RL::MAXPER; u++)
+    ld.gv[u] = gpsrc[(size_t)min(sub + u * RL::TPC, last) * RL::NC + col];
+}
+
+// this thread's fixed-order partial sum of partials [0, np) -> s_red
+template <int L, int TB>
+__device__ __forceinline__ void row0_stage(int np, const Row0Loads<L, TB> &ld,
+                                           float4 (*s_red)[2 * L]) {
+  using RL = Row0Loads<L, TB>;
+  const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
+  float4 g = f4(0.f);
+#pragma unroll
+  for (int u = 0; u < RL::MAXPER; u++) {
+    const float m = (float)(sub + u * RL::TPC < np);
+    const float4 v = ld.gv[u];
+    g = g + make_float4(v.x * m, v.y * m, v.z * m, v.w * m);
+  }
+  s_red[sub][col] = g;
+}
+
+// after row0_stage: the workgroup barrier, then the column owners (sub == 0)
+// add the TPC staged sums in order and apply Adagrad (mode 1)
+template <int L, int TB>
+__device__ __forceinline__ void row0_finish(const TrainArgs &a, int mode,
+                                            const Row0Loads<L, TB> &ld,
+                                            float4 (*s_red)[2 * L], float4 &p0,
+                                            float4 &a0) {
+  using RL = Row0Loads<L, TB>;
+  const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
+  __syncthreads();
+  p0 = mode ? ld.rp : ld.tp;
+  a0 = mode ? ld.ra : ld.ta;
+  if (sub == 0 && mode) {
+    float4 gs = f4(0.f);
+#pragma unroll
+    for (int j = 0; j < RL::TPC; j++) gs = gs + s_red[j][col];
+    adagrad4(p0, a0, gs, a.lr, a.eps);
+  }
+}
+
+// Fused batch step: K1 + K2 of one batch in ONE launch (no K1 -> K2
+// boundary, no per-slot gradient round trip through HBM).
+//  - train_prep packed the batch so that every row with several slots has
+//    them all in one workgroup; single-slot rows (most) are updated by their
+//    own group right after the backward pass, multi-slot rows by their first
+//    slot's group after an LDS exchange and a workgroup barrier, summing in
+//    sorted-slot order like train_update.
+//  - The padding row 0 (touched by nearly every record) is deferred: its
+//    per-workgroup partials go to gp[q & 1]; the NEXT fused launch (q + 1)
+//    folds them in (row0_issue/finish) before its gathers, train_row0_flush
+//    writes the final state back after the last fused batch of a run.
+// One L-lane group per record (dp == 4L), prpb = TB / L records per
+// workgroup, NBF workgroups; q = position in the run of consecutive fused
+// launches, mode = q > 0.
+template <int L, int KMAX, int MODE, int TB>
+__global__ __launch_bounds__(TB) void train_fused(TrainArgs a, int cb, int gb,
+                                                  int nb, int np, int q,
+                                                  int mode) {
+  constexpr int RPB = TB / L, R = 4 + 2 * KMAX, K = KMAX;
+  extern __shared__ float4 s_ms[];  // [MS][L]: gradients of multi-slot rows
+  __shared__ float4 s_z[2][RPB][L];
+  __shared__ float4 s_red[TB / (2 * L)][2 * L];
+  __shared__ float4 s_r0[2][L];
+  __shared__ float s_loss[RPB];
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (g_trace) ts[0] = __builtin_amdgcn_s_memrealtime();
+  const int grp = threadIdx.x / L, lane = threadIdx.x % L;
+  const int NBF = a.NBF;
+  if (g_tab & 64) mode = 0;  // ablation: no partial reads
+  // round trip 1 (kernel arguments only): the group's record ids, slot
+  // codes and targets, the workgroup's record count, the row-0 state and
+  // the np padding-row partials of the previous batch (np = its workgroup
+  // count, a kernel argument)
+  const size_t gi = ((size_t)cb * NBF + blockIdx.x) * RPB + grp;
+  const int *ri = a.pidx + gi * R;
+  const unsigned *rc = reinterpret_cast<const unsigned *>(a.pcode) + gi * R;
+  const float *yt = a.ptgt + gi * 3;
+  int row[R];
+  unsigned code[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    row[s] = ri[s];
+    code[s] = rc[s];
+  }
+  const float yt0 = yt[0], yt1 = yt[1], yt2 = yt[2];
+  const int nval = a.pnval[(size_t)cb * NBF + blockIdx.x];
+  if (!mode) np = 0;
+  const size_t par = (size_t)NBF * 2 * L;  // float4 per gp parity
+  Row0Loads<L, TB> r0l;
+  row0_issue_state<L, TB>(a, reinterpret_cast<const float4 *>(a.r0) + (q & 1) * 4 * L,
+                          r0l);
+  row0_issue_partials<L, TB>(np, reinterpret_cast<const float4 *>(a.gp) + ((q - 1) & 1) * par,
+                             r0l);
+  HGX_STAMP(ts[1]);
+  if (nval == 0) return;  // unused workgroup of this batch
+  const bool has = grp < nval;
+  // staged before the gathers: frees the partials' registers
+  row0_stage<L, TB>(np, r0l, s_red);
+  // round trip 2: every slot's table row and owner slots' accumulator
+  // rows. All unconditional (row 0 /
+  // non-owner slots read row 0, a hot line): a load under a branch is
+  // waited for at the join, which would serialise the gathers.
+  float4 Pv[R], Av[R];
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    const bool edge = slot_is_edge(s, K);
+    const float4 *T = reinterpret_cast<const float4 *>(edge ? a.etab : a.ntab);
+    const float4 *Ac = reinterpret_cast<const float4 *>(edge ? a.eacc : a.nacc);
+    const int arow = (code[s] & kCodeOwn) ? row[s] : 0;
+    Pv[s] = T[(size_t)row[s] * L + lane];
+    Av[s] = Ac[(size_t)arow * L + lane];
+  }
+  {
+    float4 p0, a0;
+    row0_finish<L, TB>(a, mode, r0l, s_red, p0, a0);
+    const int col = threadIdx.x % (2 * L), sub = threadIdx.x / (2 * L);
+    if (sub == 0) {
+      s_r0[col / L][col % L] = p0;
+      if (blockIdx.x == 0) {
+        float4 *r0d = reinterpret_cast<float4 *>(a.r0) + ((q + 1) & 1) * 4 * L;
+        r0d[(col / L) * 2 * L + col % L] = p0;
+        r0d[((col / L) * 2 + 1) * L + col % L] = a0;
+      }
+    }
+    __syncthreads();
+  }
+  HGX_STAMP(ts[2]);
+  float4 zN = f4(0.f), zE = f4(0.f);
+  float lrec = 0.f;
+  if (has) {
+#pragma unroll
+    for (int s = 0; s < R; s++)
+      if (row[s] == 0) Pv[s] = s_r0[slot_is_edge(s, K) ? 1 : 0][lane];
+    const float inv_b = 1.0f / (float)nb;
+    const float4 &Nl = Pv[0], &El = Pv[1], &Nr = Pv[2], &Er = Pv[3];
+    float z1 = group_sum<L>(dot4(Nl, Nr)), z2 = group_sum<L>(dot4(El, Er));
+    float za[K], zb[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      za[k] = group_sum<L>(dot4(Pv[4 + k], Nl));
+      zb[k] = group_sum<L>(dot4(Pv[4 + K + k], Er));
+    }
+    const int act = MODE == 1 ? 0 : 1;
+    const int lossk = MODE == 1 ? 0 : 1;
+    const float y1 = act_f(act, z1), y2 = act_f(act, z2);
+    float sa[K], sb[K], P = 0.f, Q = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      sa[k] = act_f(act, za[k]);
+      sb[k] = act_f(act, zb[k]);
+      P += sa[k];
+      Q += sb[k];
+    }
+    P = P / (float)K;
+    Q = Q / (float)K;
+    const float y3 = P * Q;
+    float l1, l2, l3, g1, g2, g3;
+    head_loss(lossk, y1, yt0, l1, g1);
+    head_loss(lossk, y2, yt1, l2, g2);
+    head_loss(lossk, y3, yt2, l3, g3);
+    lrec = l1 + l2 + l3;
+    HGX_STAMP(ts[3]);
+    g1 *= inv_b;
+    g2 *= inv_b;
+    g3 *= inv_b;
+    const float dz1 = g1 * act_d(act, z1, y1);
+    const float dz2 = g2 * act_d(act, z2, y2);
+    const float dP = g3 * Q / (float)K, dQ = g3 * P / (float)K;
+    auto emit = [&](int s, float4 g) {
+      if (row[s] == 0) {
+        if (slot_is_edge(s, K)) zE = zE + g;
+        else zN = zN + g;
+      } else if (code[s] & kCodeMulti) {
+        s_ms[(code[s] & 0xfffu) * L + lane] = g;
+      } else if (!(g_tab & 128)) {
+        const bool edge = slot_is_edge(s, K);
+        float4 pv = Pv[s], av = Av[s];
+        adagrad4_hw(pv, av, f4(0.f) + g, a.lr, a.eps);
+        reinterpret_cast<float4 *>(edge ? a.etab : a.ntab)[(size_t)row[s] * L + lane] = pv;
+        reinterpret_cast<float4 *>(edge ? a.eacc : a.nacc)[(size_t)row[s] * L + lane] = av;
+      }
+    };
+    float4 gln = fma4(dz1, Nr, f4(0.f)), gre = fma4(dz2, El, f4(0.f));
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const float da = dP * act_d(act, za[k], sa[k]);
+      const float db = dQ * act_d(act, zb[k], sb[k]);
+      gln = fma4(da, Pv[4 + k], gln);
+      gre = fma4(db, Pv[4 + K + k], gre);
+      emit(4 + k, fma4(da, Nl, f4(0.f)));
+      emit(4 + K + k, fma4(db, Er, f4(0.f)));
+    }
+    emit(0, gln);
+    emit(3, gre);
+    emit(2, fma4(dz1, Nl, f4(0.f)));
+    emit(1, fma4(dz2, Er, f4(0.f)));
+    HGX_STAMP(ts[4]);
+  }
+  s_z[0][grp][lane] = zN;
+  s_z[1][grp][lane] = zE;
+  if (lane == 0) s_loss[grp] = lrec;
+  __syncthreads();
+  if (has) {
+#pragma unroll
+    for (int s = 0; s < R; s++) {
+      const unsigned cd = code[s];
+      if (row[s] != 0 && (cd & kCodeMulti) && (cd & kCodeOwn)) {
+        const int pos = cd & 0xfffu, cnt = (cd >> 12) & 0xfffu;
+        float4 g = f4(0.f);
+        for (int j = 0; j < cnt; j++) g = g + s_ms[(pos + j) * L + lane];
+        const bool edge = slot_is_edge(s, K);
+        float4 pv = Pv[s], av = Av[s];
+        adagrad4_hw(pv, av, g, a.lr, a.eps);
+        reinterpret_cast<float4 *>(edge ? a.etab : a.ntab)[(size_t)row[s] * L + lane] = pv;
+        reinterpret_cast<float4 *>(edge ? a.eacc : a.nacc)[(size_t)row[s] * L + lane] = av;
+      }
+    }
+  }
+  HGX_STAMP(ts[5]);
+  float4 *gpd = reinterpret_cast<float4 *>(a.gp) + (q & 1) * par;
+  for (int t = threadIdx.x; t < 2 * L; t += TB) {
+    const int tab = t / L, j = t % L;
+    float4 sz = f4(0.f);
+    for (int g = 0; g < RPB; g++) sz = sz + s_z[tab][g][j];
+    gpd[((size_t)blockIdx.x * 2 + tab) * L + j] = sz;
+  }
+  if (threadIdx.x == 0) {
+    float sl = 0.f;
+    for (int g = 0; g < RPB; g++) sl += s_loss[g];
+    a.lossbuf[(size_t)gb * a.lstride + blockIdx.x] = sl;
+  }
+  HGX_STAMP(ts[6]);
+  trace_put(gb, 0, 7, ts);
+}
+
+// After the last launch q of a fused run: the pending padding-row update ->
+// row 0 of both tables and accumulators.
+template <int L, int TB>
+__global__ __launch_bounds__(TB) void train_row0_flush(TrainArgs a, int cb, int q) {
+  __shared__ float4 s_red[TB / (2 * L)][2 * L];
+  const size_t par = (size_t)a.NBF * 2 * L;
+  Row0Loads<L, TB> r0l;
+  row0_issue_state<L, TB>(a, reinterpret_cast<const float4 *>(a.r0) + ((q + 1) & 1) * 4 * L,
+                          r0l);
+  row0_issue_partials<L, TB>(a.NBF, reinterpret_cast<const float4 *>(a.gp) + (q & 1) * par,
+                             r0l);
+  row0_stage<L, TB>(a.pnblk[cb], r0l, s_red);
+  float4 p0, a0;
+  row0_finish<L, TB>(a, 1, r0l, s_red, p0, a0);
+  const int col = threadIdx.x % (2 * L), sub = threadIdx.x / (2 * L);
+  if (sub == 0) {
+    const int tab = col / L, c = col % L;
+    reinterpret_cast<float4 *>(tab ? a.etab : a.ntab)[c] = p0;
+    reinterpret_cast<float4 *>(tab ? a.eacc : a.nacc)[c] = a0;
+  }
+}
+
 // Block-wide exclusive scan of one int per thread.
 __device__ int block_exclusive_scan(int v, int *total, int *s_ws) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -452,6 +783,183 @@ __device__ int block_exclusive_scan(int v, int *total, int *s_ws) {
   __syncthreads();
   *total = tot;
   return base + inc - v;
+}
+
+// Fused-path packing of one batch (tail of train_prep, same workgroup, the
+// batch's (row, slot) keys sorted in LDS).
+//  1. Records that share a non-padding row are connected; components by
+//     min-label propagation with pointer jumping (bounded; no convergence ->
+//     the batch takes the two-kernel path).
+//  2. Components are placed whole, in order of their first record, into
+//     workgroups of prpb groups with at most MS multi-slot rows' slots each
+//     (first fit in sequence; a component too large for one workgroup, or
+//     more than NBF workgroups -> two-kernel path).
+//  3. Each slot gets a code: single-slot row -> kCodeOwn (its group applies
+//     Adagrad directly); multi-slot row -> kCodeMulti | LDS position, the
+//     row's slots on consecutive positions in sorted-slot order, the first
+//     also kCodeOwn | count << 12 (it sums them in that order and applies
+//     Adagrad: the same order and arithmetic as train_update).
+// Every serial step runs on thread 0 in record / sorted order: the packing is
+// a deterministic function of the batch.
+__device__ void pack_batch(const TrainArgs &a, int cb, int nb, int V, int P,
+                           const unsigned long long *s_key, int *s_ws) {
+  __shared__ int s_lab[kPackB], s_csz[kPackB], s_cms[kPackB], s_cblk[kPackB],
+      s_cfill[kPackB], s_cmoff[kPackB], s_grp[kPackB];
+  __shared__ int s_mrun[kPackM], s_mlen[kPackM], s_mbase[kPackM];
+  __shared__ int s_bfill[kPackNBF];
+  __shared__ int s_flag[2], s_ok;
+  const int R = a.R, RPB = a.prpb, NBF = a.NBF, MS = a.MS;
+  volatile int *lab = s_lab;
+  auto rowkey = [&](int t) { return (unsigned)(s_key[t] >> 32); };
+  auto slotof = [&](int t) { return (int)(unsigned)(s_key[t] & 0xffffffffu); };
+  for (int i = threadIdx.x; i < nb; i += kTB) {
+    s_lab[i] = i;
+    s_csz[i] = 0;
+    s_cms[i] = 0;
+  }
+  if (threadIdx.x == 0) {
+    s_flag[0] = s_flag[1] = 0;
+    s_ok = nb <= kPackB;
+  }
+  __syncthreads();
+  if (!s_ok) {
+    if (threadIdx.x == 0) a.pfast[cb] = 0;
+    return;
+  }
+  int conv = 0;
+  for (int it = 0; it < 64; it++) {
+    for (int t = 1 + threadIdx.x; t < V; t += kTB) {
+      if (rowkey(t) == rowkey(t - 1)) {
+        const int ra = slotof(t - 1) / R, rb = slotof(t) / R;
+        const int la = lab[ra], lb = lab[rb];
+        if (la != lb) {
+          const int m = min(la, lb);
+          atomicMin(&s_lab[ra], m);
+          atomicMin(&s_lab[rb], m);
+          s_flag[it & 1] = 1;
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_flag[(it + 1) & 1] = 0;
+    for (int i = threadIdx.x; i < nb; i += kTB) {
+      const int l = lab[i];
+      const int ll = lab[l];
+      if (ll < l) atomicMin(&s_lab[i], ll);
+    }
+    __syncthreads();
+    if (!s_flag[it & 1]) {
+      conv = 1;
+      break;
+    }
+  }
+  // component sizes and multi-slot counts
+  for (int i = threadIdx.x; i < nb; i += kTB) atomicAdd(&s_csz[lab[i]], 1);
+  const int per = P / kTB, t0 = threadIdx.x * per;
+  int nm = 0;
+  for (int t = t0; t < t0 + per && t < V; t++) {
+    const bool prev = t > 0 && rowkey(t) == rowkey(t - 1);
+    const bool next = t + 1 < V && rowkey(t + 1) == rowkey(t);
+    if (prev || next) atomicAdd(&s_cms[lab[slotof(t) / R]], 1);
+    if (!prev && next) nm++;
+  }
+  int M = 0;
+  int m0 = block_exclusive_scan(nm, &M, s_ws);
+  if (M <= kPackM) {
+    for (int t = t0; t < t0 + per && t < V; t++) {
+      const bool prev = t > 0 && rowkey(t) == rowkey(t - 1);
+      const bool next = t + 1 < V && rowkey(t + 1) == rowkey(t);
+      if (!prev && next) {
+        int c = 2;
+        while (t + c < V && rowkey(t + c) == rowkey(t)) c++;
+        s_mrun[m0] = t;
+        s_mlen[m0] = c;
+        m0++;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int ok = conv && M <= kPackM && NBF <= kPackNBF;
+    int fill = 0, msf = 0, blk = 0;
+    for (int i = 0; i < nb && ok; i++) {
+      if (lab[i] != i) continue;
+      const int sz = s_csz[i], q = s_cms[i];
+      if (sz > RPB || q > MS) {
+        ok = 0;
+        break;
+      }
+      if (fill + sz > RPB || msf + q > MS) {
+        s_bfill[blk] = fill;
+        blk++;
+        fill = msf = 0;
+      }
+      if (blk >= NBF) {
+        ok = 0;
+        break;
+      }
+      s_cblk[i] = blk;
+      s_cfill[i] = fill;
+      s_cmoff[i] = msf;
+      fill += sz;
+      msf += q;
+    }
+    if (ok) {
+      s_bfill[blk] = fill;
+      for (int j = blk + 1; j < NBF; j++) s_bfill[j] = 0;
+      for (int i = 0; i < nb; i++) {
+        const int r = lab[i];
+        s_grp[i] = s_cblk[r] * RPB + s_cfill[r]++;
+      }
+      for (int k = 0; k < M; k++) {
+        const int r = lab[slotof(s_mrun[k]) / R];
+        s_mbase[k] = s_cmoff[r];
+        s_cmoff[r] += s_mlen[k];
+      }
+    }
+    s_ok = ok;
+    a.pfast[cb] = ok;
+    a.pnblk[cb] = ok ? blk + 1 : 0;
+  }
+  __syncthreads();
+  if (!s_ok) return;
+  const int G = NBF * RPB;
+  int *pidx = a.pidx + (size_t)cb * G * R;
+  unsigned *pcode = reinterpret_cast<unsigned *>(a.pcode) + (size_t)cb * G * R;
+  float *ptgt = a.ptgt + (size_t)cb * G * 3;
+  for (int t = threadIdx.x; t < G * R; t += kTB) {
+    pidx[t] = 0;
+    pcode[t] = 0u;
+  }
+  for (int t = threadIdx.x; t < G * 3; t += kTB) ptgt[t] = 0.f;
+  for (int j = threadIdx.x; j < NBF; j += kTB) a.pnval[(size_t)cb * NBF + j] = s_bfill[j];
+  __syncthreads();  // zero fill before the scattered writes (same workgroup)
+  const int64_t r0 = (int64_t)a.bmeta[cb].y * a.B;
+  for (int t = threadIdx.x; t < nb * R; t += kTB) {
+    const int i = t / R, s = t - i * R;
+    pidx[s_grp[i] * R + s] = a.idx[(int64_t)a.perm[r0 + i] * R + s];
+  }
+  for (int t = threadIdx.x; t < nb * 3; t += kTB) {
+    const int i = t / 3, c = t - i * 3;
+    ptgt[s_grp[i] * 3 + c] = a.tgt[(int64_t)a.perm[r0 + i] * 3 + c];
+  }
+  for (int t = threadIdx.x; t < V; t += kTB) {
+    const bool prev = t > 0 && rowkey(t) == rowkey(t - 1);
+    const bool next = t + 1 < V && rowkey(t + 1) == rowkey(t);
+    if (!prev && !next) {
+      const int sl = slotof(t), i = sl / R;
+      pcode[s_grp[i] * R + (sl - i * R)] = kCodeOwn;
+    }
+  }
+  for (int k = threadIdx.x; k < M; k += kTB) {
+    const int t = s_mrun[k], c = s_mlen[k], base = s_mbase[k];
+    for (int j = 0; j < c; j++) {
+      const int sl = slotof(t + j), i = sl / R;
+      unsigned code = kCodeMulti | (unsigned)(base + j);
+      if (j == 0) code |= kCodeOwn | ((unsigned)c << 12);
+      pcode[s_grp[i] * R + (sl - i * R)] = code;
+    }
+  }
 }
 
 // One workgroup per batch of the chunk: sorted unique (table,row) keys of
@@ -536,6 +1044,7 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
     uoff[U] = V;
     a.ucount[cb] = U;
   }
+  if (a.fused) pack_batch(a, cb, nb, V, P, s_key, s_ws);
 }
 
 // deterministic two-level sum of the chunk's per-block losses:
@@ -671,6 +1180,29 @@ KFn fwd_for(int K, int loss, int act, int tb1) {
   if (K <= 5) return train_fwd_bwd<L, VPL, 5, false, 0, kTB>;
   if (K <= 8) return train_fwd_bwd<L, VPL, 8, false, 0, kTB>;
   return train_fwd_bwd<L, VPL, 16, false, 0, kTB>;
+}
+
+using KFusedFn = void (*)(TrainArgs, int, int, int, int, int, int);
+using KFlushFn = void (*)(TrainArgs, int, int);
+
+// fused one-launch step: d in (64, 256] (one float4 per lane, L = 32 or 64),
+// K = 5 with the FOBE (sigmoid/KLD) or HOBE (relu/MSE) heads
+bool pick_fused(int L, int VPL, int K, int loss, int act, KFusedFn &kf,
+                KFlushFn &kfl, int &tb) {
+  if (VPL != 1 || K != 5 || loss != act) return false;
+  if (L == 32) {
+    tb = 256;
+    kf = loss == 0 ? train_fused<32, 5, 1, 256> : train_fused<32, 5, 2, 256>;
+    kfl = train_row0_flush<32, 256>;
+    return true;
+  }
+  if (L == 64) {
+    tb = 512;
+    kf = loss == 0 ? train_fused<64, 5, 1, 512> : train_fused<64, 5, 2, 512>;
+    kfl = train_row0_flush<64, 512>;
+    return true;
+  }
+  return false;
 }
 
 bool pick_kernels(int L, int VPL, int K, int loss, int act, int &tb1, int tb2,
@@ -915,6 +1447,24 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   }
   const int RPB = tb1 / L;
   const int nblk1 = (batch + RPB - 1) / RPB;
+  // fused step: eligible geometry, batch <= kPackB records, NBF workgroups
+  // (packing leaves holes: nblk1 + 50% + 2, at most kPackNBF)
+  KFusedFn kf = nullptr;
+  KFlushFn kfl = nullptr;
+  int tbf = 0;
+  // HGX_TRAIN_FUSED: 0 off, 1 (default) d in (64, 128] (L = 32), 2 also
+  // d in (128, 256] (L = 64: measured slower than the two-kernel step on the
+  // C4 FOBE stream, 14.8 vs 13.9 us/batch, r01)
+  const int fz = env_int("HGX_TRAIN_FUSED", 1);
+  bool fused = fz != 0 && (L == 32 || fz == 2) &&
+               env_int("HGX_TRAIN_GENERIC", 0) != 1 &&
+               pick_fused(L, VPL, K, loss, act, kf, kfl, tbf) && batch <= kPackB;
+  const int prpb = fused ? tbf / L : 0;
+  const int nbf_need = fused ? (batch + prpb - 1) / prpb : 0;
+  const int NBF = fused ? std::min(kPackNBF, nbf_need + nbf_need / 2 + 2) : 0;
+  if (fused && NBF < nbf_need) fused = false;
+  const int MS = 48;  // LDS rows for multi-slot gradients per workgroup
+  const int lstride = std::max(nblk1, NBF);
   const int GPB2 = tb2 / L;
   // one unique-row task per group, plus the two padding-row workgroups
   const int grid2 = (SB + GPB2 - 1) / GPB2 + 2;
@@ -931,16 +1481,21 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   const size_t bidx_n = (size_t)CB * batch * R + (size_t)RPB * R * 2 + 64;
   const size_t btgt_n = (size_t)CB * batch * 3 + (size_t)RPB * 3 * 2 + 64;
   const size_t inv_n = (size_t)CB * SB + (size_t)RPB * R * 2 + 64;
+  const size_t pg = fused ? (size_t)CB * NBF * prpb : 0;  // packed groups
+  const size_t pack_ints = fused ? pg * R * 2 + pg * 3 + (size_t)CB * NBF + 2 * CB + 64 : 0;
   const size_t prep_ints = bidx_n + btgt_n + inv_n + (size_t)CB * SB +
-                           (size_t)CB * (SB + 1) + CB + 2 * CB + 64;
+                           (size_t)CB * (SB + 1) + CB + 2 * CB + 64 + pack_ints;
   HGX_TRY(hgx_ensure(ctx, ctx->s1, sizeof(int) * (n + 1)));              // perm
   HGX_TRY(hgx_ensure(ctx, ctx->s2, sizeof(float) * (size_t)SB * dp));    // gslot
-  HGX_TRY(hgx_ensure(ctx, ctx->s3, sizeof(float) * (size_t)nblk1 * 2 * dp));
-  HGX_TRY(hgx_ensure(ctx, ctx->s4, sizeof(float) * (size_t)nbatches * nblk1 + 16));
+  // gzero (K1 partials) | r0 [2][2][2][dp] | gp [2][NBF][2][dp]
+  const size_t s3_f = (size_t)nblk1 * 2 * dp + 8 * (size_t)dp + (size_t)2 * NBF * 2 * dp;
+  HGX_TRY(hgx_ensure(ctx, ctx->s3, sizeof(float) * s3_f));
+  HGX_TRY(hgx_ensure(ctx, ctx->s4, sizeof(float) * (size_t)nbatches * lstride + 16));
   HGX_TRY(hgx_ensure(ctx, ctx->s5, sizeof(int) * prep_ints));
   HGX_TRY(hgx_ensure(ctx, ctx->s6, 64 + sizeof(double) * kLossBlocks));  // loss
   int *perm = ctx->s1.as<int>();
   HGX_HIP(ctx, hipMemsetAsync(ctx->s5.p, 0, sizeof(int) * prep_ints, ctx->stream));
+  HGX_HIP(ctx, hipMemsetAsync(ctx->s3.p, 0, sizeof(float) * s3_f, ctx->stream));
   TrainArgs a;
   a.idx = ctx->rec_idx.as<int>();
   a.tgt = ctx->rec_tgt.as<float>();
@@ -959,6 +1514,13 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   a.lossbuf = ctx->s4.as<float>();
   a.SB = SB;
   a.nblk1 = nblk1;
+  a.lstride = lstride;
+  a.fused = fused ? 1 : 0;
+  a.prpb = prpb;
+  a.NBF = NBF;
+  a.MS = MS;
+  a.r0 = a.gzero + (size_t)nblk1 * 2 * dp;
+  a.gp = a.r0 + 8 * (size_t)dp;
   a.lr = lr;
   a.eps = eps;
   a.loss = loss;
@@ -979,6 +1541,18 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     q += CB;
     q += ((uintptr_t)q / sizeof(int)) % 2;  // 8-B align
     a.bmeta = reinterpret_cast<int2 *>(q);
+    q += 2 * CB;
+    a.pidx = q;
+    q += pg * R;
+    a.pcode = q;
+    q += pg * R;
+    a.ptgt = reinterpret_cast<float *>(q);
+    q += pg * 3;
+    a.pnval = q;
+    q += (size_t)CB * NBF;
+    a.pnblk = q;
+    q += CB;
+    a.pfast = q;
   }
   double *dloss = reinterpret_cast<double *>(ctx->s6.as<char>() + 32);
   double *dpart = reinterpret_cast<double *>(ctx->s6.as<char>() + 64);
@@ -1013,7 +1587,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   // same kernels (10.6 us per batch both ways at d=128) with less host time,
   // and rocprofv3 kernel tracing crashes on the replays. HGX_GRAPH=1 replays
   // captured graphs instead.
-  const bool use_graph = env_int("HGX_GRAPH", 0) == 1;
+  const bool use_graph = env_int("HGX_GRAPH", 0) == 1 && !fused;
   auto launch_run = [&](int cb0, int nrun) {
     for (int b = cb0; b < cb0 + nrun; b++) {
       hipLaunchKernelGGL(k1, dim3(nblk1), dim3(tb1), 0, ctx->stream, a, b);
@@ -1043,7 +1617,8 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     res.ev.push_back(e);
   }
 
-  std::vector<int> hperm;
+  std::vector<int> hperm, hfast, hnblk;
+  int64_t nfused = 0, nsplit = 0;
   double batch_ms = 0.0;
   double best = INFINITY;
   int ep = 0;
@@ -1080,14 +1655,54 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
       }
     }
     (void)hipMemsetAsync(dloss, 0, sizeof(double), ctx->stream);
+    (void)hipMemsetAsync(a.lossbuf, 0, sizeof(float) * (size_t)nbatches * lstride,
+                         ctx->stream);
     for (int64_t c = 0; c < nchunks && rc == HGX_OK; c++) {
       const int64_t base = c * CB;
       const int nbc = (int)std::min<int64_t>(CB, nbatches - base);
       hipLaunchKernelGGL(train_prep, dim3(CB), dim3(kTB),
                          (size_t)P * sizeof(unsigned long long), ctx->stream,
                          a, base, nbc, P);
+      if (fused) {
+        // which batches packed: one host read per chunk of up to 1024
+        hfast.resize(nbc);
+        hnblk.resize(nbc);
+        if (hipMemcpyAsync(hfast.data(), a.pfast, sizeof(int) * nbc,
+                           hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipMemcpyAsync(hnblk.data(), a.pnblk, sizeof(int) * nbc,
+                           hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess) {
+          rc = hgx_fail(ctx, HGX_EHIP, "batch preparation failed: %s",
+                        hipGetErrorString(hipGetLastError()));
+          break;
+        }
+      }
       (void)hipEventRecord(bev[2 * c], ctx->stream);
-      if (use_graph) {
+      if (fused) {
+        int qrun = 0;  // position in the current run of fused launches
+        for (int b = 0; b < nbc; b++) {
+          if (hfast[b]) {
+            const int64_t gbat = base + b;
+            const int nrec = (int)std::min<int64_t>(batch, n - gbat * batch);
+            hipLaunchKernelGGL(kf, dim3(NBF), dim3(tbf),
+                               (size_t)MS * L * sizeof(float4), ctx->stream, a,
+                               b, (int)gbat, nrec, qrun > 0 ? hnblk[b - 1] : 0,
+                               qrun, qrun > 0 ? 1 : 0);
+            qrun++;
+            nfused++;
+          } else {
+            if (qrun > 0)
+              hipLaunchKernelGGL(kfl, dim3(1), dim3(tbf), 0, ctx->stream, a,
+                                 b - 1, qrun - 1);
+            qrun = 0;
+            launch_run(b, 1);
+            nsplit++;
+          }
+        }
+        if (qrun > 0)
+          hipLaunchKernelGGL(kfl, dim3(1), dim3(tbf), 0, ctx->stream, a,
+                             nbc - 1, qrun - 1);
+      } else if (use_graph) {
         for (int g = 0; g * GB < nbc; g++) {
           if (hipGraphLaunch(res.gexec[g], ctx->stream) != hipSuccess) {
             rc = hgx_fail(ctx, HGX_EHIP, "graph launch failed");
@@ -1096,12 +1711,13 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
         }
       } else {
         launch_run(0, nbc);
+        nsplit += nbc;
       }
       (void)hipEventRecord(bev[2 * c + 1], ctx->stream);
     }
     if (rc) break;
     hipLaunchKernelGGL(loss_partial, dim3(kLossBlocks), dim3(kTB), 0,
-                       ctx->stream, a.lossbuf, nbatches * nblk1, dpart);
+                       ctx->stream, a.lossbuf, nbatches * lstride, dpart);
     hipLaunchKernelGGL(loss_final, dim3(1), dim3(kLossBlocks), 0, ctx->stream,
                        dpart, dloss);
     double lsum = 0.0;
@@ -1145,6 +1761,8 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   ctx->train_epoch_ms = ms;
   ctx->train_records = (int64_t)ep * n;
   ctx->train_batches = (int64_t)ep * nbatches;
+  ctx->train_fused = nfused;
+  ctx->train_split = nsplit;
   if (epochs_run) *epochs_run = ep;
   return HGX_OK;
 }
@@ -1155,5 +1773,13 @@ extern "C" int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
   if (ms) *ms = ctx->train_ms;
   if (records) *records = ctx->train_records;
   if (batches) *batches = ctx->train_batches;
+  return HGX_OK;
+}
+
+extern "C" int hgx_train_path_stats(hgx_ctx *ctx, int64_t *fused_batches,
+                                    int64_t *split_batches) {
+  if (!ctx) return HGX_EINVAL;
+  if (fused_batches) *fused_batches = ctx->train_fused;
+  if (split_batches) *split_batches = ctx->train_split;
   return HGX_OK;
 }

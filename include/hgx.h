@@ -180,6 +180,15 @@ int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr, float eps,
  * processed. */
 int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
                          int64_t *batches);
+/* Of the last hgx_train: batches run by the fused one-launch step
+ * (train_fused: rows shared inside a batch packed into one workgroup,
+ * padding-row update deferred to the next launch) and batches that took the
+ * two-kernel step (train_fwd_bwd + train_update). HGX_TRAIN_FUSED=0 forces
+ * the two-kernel step. Same Keras semantics either way (embedding.py:269-305,
+ * hg2v_model.py:51-203); the two differ only in the summation order of the
+ * padding row's gradient. */
+int hgx_train_path_stats(hgx_ctx *ctx, int64_t *fused_batches,
+                         int64_t *split_batches);
 
 /* ---- dense MLP engine (combiners + link-prediction classifier) --------- *
  * Replaces the Keras models of

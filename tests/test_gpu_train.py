@@ -133,3 +133,84 @@ def test_train_rejects_out_of_range_rows(ctx):
   ctx.model_init(8, 3, 3, seed=1)  # far too few rows
   with pytest.raises(AssertionError):
     ctx.train(batch=64, max_epochs=1)
+
+
+def _mixed_reuse_records(rs, nb, B, K, hub_batches, wide=20000):
+  """Records in batch order: batches in hub_batches draw every id from a
+  handful of rows (records sharing rows across more than one workgroup: the
+  batch cannot be packed and takes the two-kernel step), the others from a
+  wide range (packable)."""
+  n = nb * B
+  idx = np.zeros((n, 4 + 2 * K), np.int32)
+  kind = rs.randint(0, 3, n)
+  for b in range(nb):
+    lo, hi = (1, 6) if b in hub_batches else (1, wide)
+    sl = slice(b * B, (b + 1) * B)
+    kb = kind[sl]
+    blk = idx[sl]
+    m0, m1, m2 = kb == 0, kb == 1, kb == 2
+    blk[m0, 0] = rs.randint(lo, hi, m0.sum())
+    blk[m0, 2] = rs.randint(lo, hi, m0.sum())
+    blk[m1, 1] = rs.randint(lo, hi, m1.sum())
+    blk[m1, 3] = rs.randint(lo, hi, m1.sum())
+    blk[m2, 0] = rs.randint(lo, hi, m2.sum())
+    blk[m2, 3] = rs.randint(lo, hi, m2.sum())
+    blk[m2, 4:4 + K] = rs.randint(lo, hi, (m2.sum(), K))
+    blk[m2, 4 + K:] = rs.randint(lo, hi, (m2.sum(), K))
+  tgt = np.zeros((n, 3), np.float32)
+  tgt[np.arange(n), kind] = rs.uniform(0, 1, n).astype(np.float32)
+  return idx, tgt
+
+
+@pytest.mark.parametrize("d,loss,act", [(128, O.LOSS_MSE, O.ACT_RELU),
+                                        (256, O.LOSS_KLD, O.ACT_SIGMOID)])
+def test_fused_step_mixed_runs_vs_oracle_and_split(ctx, d, loss, act,
+                                                   monkeypatch):
+  """The fused one-launch step (train_fused) against the oracle and the
+  two-kernel step: runs of fused batches interrupted by unpackable batches
+  (hub rows) exercise the deferred padding-row update, its flush before a
+  two-kernel batch and the restart after it; a ragged last batch too."""
+  rs = np.random.RandomState(11)
+  K, B, nb = 5, 256, 12
+  idx, tgt = _mixed_reuse_records(rs, nb, B, K, hub_batches={3, 4, 8})
+  idx, tgt = idx[:-57], tgt[:-57]  # ragged last batch
+  # in-order batches: the hub batches stay where they were put
+  perms = np.arange(idx.shape[0])[None, :]
+  nrows = int(idx[:, [0, 2] + list(range(4, 4 + K))].max()) + 2
+  erows = int(idx[:, [1, 3] + list(range(4 + K, 4 + 2 * K))].max()) + 2
+  nt = rs.uniform(-0.05, 0.05, (nrows, d)).astype(np.float32)
+  et = rs.uniform(-0.05, 0.05, (erows, d)).astype(np.float32)
+  ont, oet, ol, _, _ = O.train(idx, tgt, K, nt, et, loss, act, batch=B,
+                               max_epochs=1, perms=perms)
+  ctx.records_set(idx, tgt)
+  res = {}
+  for mode in ("2", "0"):
+    monkeypatch.setenv("HGX_TRAIN_FUSED", mode)
+    ctx.model_init(d, nrows, erows, node_tab=nt, edge_tab=et)
+    gl = ctx.train(batch=B, max_epochs=1, loss=loss, act=act, perms=perms)
+    res[mode] = ctx.model_get() + (gl, ctx.train_path_stats())
+  fused, split = res["2"][3], res["0"][3]
+  assert fused == (nb - 3, 3), fused
+  assert split == (0, nb), split
+  for mode in ("2", "0"):
+    gnt, get_, gl, _ = res[mode]
+    assert np.allclose(gl, ol, rtol=1e-4, atol=1e-7), (mode, gl, ol)
+    assert np.abs(gnt - ont).max() < 1e-5 and np.abs(get_ - oet).max() < 1e-5
+  # the two device paths differ only in the padding row's summation order
+  for a, b in zip(res["2"][:2], res["0"][:2]):
+    assert np.abs(a - b).max() < 1e-6
+
+
+def test_fused_step_bitwise_deterministic(ctx):
+  rs = np.random.RandomState(3)
+  idx, tgt = _mixed_reuse_records(rs, 20, 256, 5, hub_batches=set())
+  ctx.records_set(idx, tgt)
+  out = []
+  for _ in range(2):
+    ctx.model_init(128, 20002, 20002, seed=9)
+    ctx.train(batch=256, max_epochs=2, loss=O.LOSS_MSE, act=O.ACT_RELU,
+              shuffle_seed=5, min_delta=-1.0)
+    assert ctx.train_path_stats()[0] >= 36
+    out.append(ctx.model_get())
+  assert np.array_equal(out[0][0], out[1][0])
+  assert np.array_equal(out[0][1], out[1][1])

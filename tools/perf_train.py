@@ -22,3 +22,4 @@ for ep in range(2):
   wall = time.time() - t
   ms, rec, bat = ctx.train_stats()
   print(f"d={d} n={n} epoch wall {wall:.3f}s dev {ms:.1f}ms  {rec/ms*1e3/1e6:.2f} Mrec/s  {ms*1e3/bat:.2f} us/batch  loss {l}")
+  print("  path (fused, split):", ctx.train_path_stats())

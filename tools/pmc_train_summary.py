@@ -15,7 +15,7 @@ def per_kernel(path, counter):
     if r["Counter_Name"] != counter:
       continue
     name = r["Kernel_Name"]
-    for key in ("train_fwd_bwd", "train_update"):
+    for key in ("train_fwd_bwd", "train_update", "train_fused", "train_row0_flush"):
       if key in name:
         vals.setdefault(key, []).append(float(r["Counter_Value"]))
   return {k: float(np.mean(v)) for k, v in vals.items()}, \
@@ -24,15 +24,21 @@ def per_kernel(path, counter):
 
 f, nf = per_kernel(fetch_csv, "FETCH_SIZE")
 w, nw = per_kernel(write_csv, "WRITE_SIZE")
-hbm = 1024 * (2 * sum(f.values()) + sum(w.values()))
+# per batch step: every batch runs train_fused (or K1 + K2); the flush runs
+# once per run of fused batches (per chunk), so it is averaged over batches
+steps = max(nf.get("train_fused", 0) + nf.get("train_fwd_bwd", 0), 1)
+def per_step(vals, counts):
+  return sum(vals[k] * counts[k] for k in vals) / steps
+hbm = 1024 * (2 * per_step(f, nf) + per_step(w, nw))
 alg = 256 * (224 * d + 68)
 res = {
-    "round": 1,
+    "round": int(sys.argv[5]) if len(sys.argv) > 5 else 1,
     "command": ("rocprofv3 --pmc FETCH_SIZE (pass 1) / "
                 "--pmc WRITE_SIZE (pass 2) --output-format csv -- python "
                 f"tools/perf_train.py {d} 400000"),
     "note": ("Per batch of 256 records at d=%d on 100k/50k-row tables, summed over "
-             "the two per-batch kernels, mean over all launches. FETCH_SIZE / "
+             "the per-batch kernels (train_fused, or train_fwd_bwd + train_update, and the "
+             "row-0 flush once per run), per batch step. FETCH_SIZE / "
              "WRITE_SIZE are KB; gfx950 correction: FETCH doubled (wide 16-B-per-"
              "lane reads are tallied at half), WRITE as is. Infinity-Cache hits "
              "are counted by these counters. Collected on the trainer-only script "

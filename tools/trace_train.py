@@ -33,6 +33,29 @@ ctx.train(batch=256, max_epochs=1, loss=1, act=1, min_delta=-1e30)
 ms, rec, bat = ctx.train_stats()
 print(f"{extra} {ms * 1e3 / bat:.2f} us/batch (traced run)")
 t = np.fromfile(path, np.uint64).reshape(256, 2, 1024, 8).astype(np.int64)
+print("path (fused, split):", ctx.train_path_stats())
+if ctx.train_path_stats()[0] > 0:
+  # fused step: kern slot 0 only, stamps start, ids, gathers+row0, compute,
+  # emits, multi rows, end
+  rows = []
+  for b in range(16, 250):
+    a1 = t[b, 0][t[b, 0, :, 0] > 0][:, :7]
+    n1 = t[b + 1, 0][t[b + 1, 0, :, 0] > 0]
+    act = a1[a1[:, 3] > 0]
+    if len(a1) == 0 or len(n1) == 0 or len(act) == 0:
+      continue
+    rows.append([a1[:, 6].max() - a1[:, 0].min(), n1[:, 0].min() - a1[:, 6].max(),
+                 n1[:, 0].min() - a1[:, 0].min(), a1[:, 0].max() - a1[:, 0].min(),
+                 len(a1), len(act)]
+                + list(np.median(np.diff(act, axis=1), axis=0))
+                + list(np.max(np.diff(act, axis=1), axis=0)))
+  r = np.array(rows, np.float64) * 0.01
+  m = np.median(r, axis=0)
+  print(f"fused span {m[0]:.2f} us  gap {m[1]:.2f}  batch {m[2]:.2f}  launch skew {m[3]:.2f}  "
+        f"blocks {m[4]*100:.0f} active {m[5]*100:.0f}")
+  print("per-WG median: ids %.2f gathers+row0 %.2f compute %.2f emits %.2f multi %.2f tail %.2f" % tuple(m[6:12]))
+  print("per-WG max:    ids %.2f gathers+row0 %.2f compute %.2f emits %.2f multi %.2f tail %.2f" % tuple(m[12:18]))
+  sys.exit(0)
 k1 = t[:, 0, :, :6]
 k2 = t[:, 1, :, :4]
 rows = []
