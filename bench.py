@@ -37,6 +37,34 @@ METRIC = ("training samples/sec + alg-dist SpMV GB/s, HOBE dim=128 at "
           "1/2/4/8 MI355X")
 
 
+def gather_roofline(nnz, n_rows, e_rows, ms_per_iter, ks=12):
+  """Alg-dist against the chip's random-row gather rate (the bound of a
+  gather-dominated SpMM whose rows have no locality): each
+  incidence gathers one 4*ks-byte source row per half, edge rows in the node
+  half and node rows in the edge half. Peak per half = the measured random
+  48-B row rate for a table of that size (profiles/r01_gather_tablesize.json,
+  log-interpolated), so the bound is nnz/peak(E table) + nnz/peak(N table)."""
+  path = os.path.join(ROOT, "profiles", "r01_gather_tablesize.json")
+  if not os.path.exists(path):
+    return None
+  with open(path) as f:
+    curve = json.load(f)["curve"]
+  mb = np.log([c["table_mb"] for c in curve])
+  rate = [c["g_rows_per_s"] for c in curve]
+
+  def peak(rows):
+    x = np.log(max(rows * 4.0 * ks / 2**20, 1e-3))
+    return float(np.interp(x, mb, rate)) * 1e9
+
+  t_min = nnz / peak(e_rows) + nnz / peak(n_rows)
+  achieved = 2.0 * nnz / (ms_per_iter * 1e-3)
+  return {"bound": "random-row gather rate", "unit": "G rows/s",
+          "achieved": round(achieved / 1e9, 1),
+          "peak": round(2.0 * nnz / t_min / 1e9, 1),
+          "frac": round(t_min / (ms_per_iter * 1e-3), 3),
+          "source": "profiles/r01_gather_tablesize.json"}
+
+
 def parse():
   p = argparse.ArgumentParser()
   p.add_argument("--gpus", type=int, default=1)
@@ -257,7 +285,10 @@ def main():
           "ms_per_iter": round(ms4 / args.alg_iters, 3),
           "gbps": round(gbps4, 1), "bytes_per_iter": b_iter4,
           "frac_of_hbm_peak": round(gbps4 / HBM_PEAK_GBPS, 4),
-          "sharded": world > 1, "graph_gen_s": round(c4_gen, 1)}
+          "sharded": world > 1, "graph_gen_s": round(c4_gen, 1),
+          "gather_roofline": (gather_roofline(big.nnz, big.N, big.E,
+                                              ms4 / args.alg_iters)
+                              if world == 1 else None)}
     # 128-B line traffic of the same kernels from the committed PMC run
     # (TCC_MISS x 128 B; random gathers move whole lines, tools/
     # gather_granularity.hip), against this run's time
@@ -363,6 +394,9 @@ def main():
                     "gbps": round(alg_gbps, 1),
                     "bytes_per_iter": bytes_iter,
                     "frac_of_hbm_peak": round(alg_gbps / HBM_PEAK_GBPS, 4),
+                    "gather_roofline": (gather_roofline(
+                        inc.nnz, inc.N, inc.E, alg_ms / args.alg_iters)
+                                        if world == 1 else None),
                     "sharded": world > 1},
         "algdist_c4": c4,
         "hobe_sampling_s": round(sample_s, 3),

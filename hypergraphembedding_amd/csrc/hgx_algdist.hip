@@ -37,7 +37,10 @@ using hgx::ord2f;
 
 namespace {
 
-constexpr int kBlock = 256;
+#ifndef HGX_ALG_BLOCK
+#define HGX_ALG_BLOCK 256
+#endif
+constexpr int kBlock = HGX_ALG_BLOCK;
 // min/max words are spread over kRep replicas (workgroup b adds to replica
 // b % kRep): 2048 workgroups on one word serialise at the memory-side
 // atomic unit (~90 us per sweep); 32 per word do not. Readers fold the
@@ -45,7 +48,8 @@ constexpr int kBlock = 256;
 constexpr int kRep = 64;
 enum { MODE_FULL = 0, MODE_PARTIAL = 1 };
 // diagnostic ablation bits (HGX_ALG_ABLATE, timing experiments only):
-// 1 = skip the min/max flush, 2 = skip the source gathers
+// 1 = skip the min/max flush, 2 = skip the source gathers, 4 = flush
+// without its global atomics
 __constant__ int g_ablate = 0;
 
 __device__ __forceinline__ float4 f4fma(float w, float4 v, float4 a) {
@@ -85,11 +89,8 @@ __device__ void load_affine(const int *mm_prev, int KS, int k, float *s_m,
     }
 #pragma unroll
     for (int b = 0; b < B; b++) {
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        mx[b] = max(mx[b], __shfl_xor(mx[b], off));
-        mn[b] = max(mn[b], __shfl_xor(mn[b], off));
-      }
+      mx[b] = hgx::wave_max_i(mx[b]);
+      mn[b] = hgx::wave_max_i(mn[b]);
     }
     if (lane == 0) {
 #pragma unroll
@@ -111,6 +112,11 @@ __device__ void load_affine(const int *mm_prev, int KS, int k, float *s_m,
 }
 
 // Block-wide min/max of per-thread partials -> 2k atomics per workgroup.
+// Whole-wave DPP reductions (hgx::wave_min/max: no LDS traffic; ds_bpermute
+// shuffles queued on the LDS pipe at the tail). Measured on C3 (r01): LDS
+// atomics instead of the wave reductions let every block reach its global
+// atomics at the same moment and the burst on the replica lines cost more
+// (12.5 vs 1.8 us per iteration).
 template <int KS>
 __device__ __forceinline__ void flush_minmax(const float (&lmn)[KS],
                                              const float (&lmx)[KS], int k,
@@ -121,11 +127,8 @@ __device__ __forceinline__ void flush_minmax(const float (&lmn)[KS],
   for (int i = 1; i < KS; i++) {
     float a = lmn[i], b = lmx[i];
     if (i <= k) {  // wave-uniform
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        a = fminf(a, __shfl_xor(a, off));
-        b = fmaxf(b, __shfl_xor(b, off));
-      }
+      a = hgx::wave_min(a);
+      b = hgx::wave_max(b);
     }
     if (lane == 0) {
       s_red[0][wave][i] = a;
@@ -140,13 +143,27 @@ __device__ __forceinline__ void flush_minmax(const float (&lmn)[KS],
       a = fminf(a, s_red[0][w][tid]);
       b = fmaxf(b, s_red[1][w][tid]);
     }
-    if (b >= a) {
+    if (b >= a && !(g_ablate & 4)) {
       const int r = blockIdx.x % kRep;
       atomicMax(&mm_cur[(size_t)tid * kRep + r], f2ord(b));
       atomicMax(&mm_cur[(size_t)(KS + tid) * kRep + r], ~f2ord(a));
     }
   }
 }
+
+// Sampled min/max (hgx_alg_run, every iteration but the last): the k
+// argument carries kSampleFlush and only workgroups < kRep flush. The
+// per-iteration rescale is a per-dimension increasing affine map applied
+// to nodes and edges alike, and both half-updates (a normalised weighted
+// mean averaged with self) commute with such maps, so any intermediate
+// affine gives the same final, exactly normalised, coordinates up to
+// rounding: the intermediate rescale only has to keep the values O(1),
+// which a sample of rows does. The last iteration flushes every workgroup
+// and final_affine applies its exact min/max (algebraic_distance.py:97-123).
+constexpr int kSampleFlush = 1 << 24;
+#define HGX_FLUSH_SEL(k)                                 \
+  const bool fskip_ = ((k) & kSampleFlush) && blockIdx.x >= kRep; \
+  (k) &= kSampleFlush - 1
 
 // One CSR half-sweep over rows [row0, row0+R), narrow rows (KS <= 20):
 // G lanes per destination row; each lane strides the row's incidences with
@@ -160,6 +177,7 @@ __global__ __launch_bounds__(kBlock) void algdist_half_narrow(
     const float *__restrict__ self_in, const float *__restrict__ src,
     float *__restrict__ out, const int *__restrict__ mm_prev, int src_affine,
     int *__restrict__ mm_cur, int k, int long_thresh) {
+  HGX_FLUSH_SEL(k);
   constexpr int NV = KS / 4;
   __shared__ float s_m[KS], s_d[KS];
   load_affine(mm_prev, KS, k, s_m, s_d, true);
@@ -262,7 +280,127 @@ __global__ __launch_bounds__(kBlock) void algdist_half_narrow(
       }
     }
   }
-  if (MODE == MODE_FULL && !(g_ablate & 1)) flush_minmax<KS>(lmn, lmx, k, mm_cur);
+  if (MODE == MODE_FULL && !(g_ablate & 1) && !fskip_)
+    flush_minmax<KS>(lmn, lmx, k, mm_cur);
+}
+
+// Same half-sweep with the source row split over a QUAD of lanes (KS <= 16):
+// lane p of a quad gathers float4 p of the row (p < KS/4), so one load
+// instruction touches 16 source rows as 1-2 whole 64-B sectors each instead
+// of 64 rows x one 16-B piece per instruction (3 instructions per 48-B row in
+// algdist_half_narrow). On an L2-resident source table (C3) the sweep is bound
+// by L2 requests, and this cuts them from 3 to ~1.4 per incidence
+// (tools/gather_tablesize.hip measures the 4-lane pattern). G = 4Q lanes per
+// destination row: quad q of the group strides the row's incidences
+// q, q + Q, ... with M in flight; the weight (vector 0, .x) is broadcast
+// from lane 0 of the quad by DPP; the Q partial sums of each lane position
+// are added by xor shuffles over lane offsets 4 .. G/2.
+template <int G>
+__device__ __forceinline__ float quad_stride_sum(float x) {
+#pragma unroll
+  for (int off = 4; off < G; off <<= 1) x += __shfl_xor(x, off);
+  return x;
+}
+
+template <int KS, int G, int MODE, int M>
+__global__ __launch_bounds__(kBlock) void algdist_half_quad(
+    int row0, int R, const int *__restrict__ rp, const int *__restrict__ col,
+    const float *__restrict__ self_in, const float *__restrict__ src,
+    float *__restrict__ out, const int *__restrict__ mm_prev, int src_affine,
+    int *__restrict__ mm_cur, int k, int long_thresh) {
+  HGX_FLUSH_SEL(k);
+  constexpr int NV = KS / 4, Q = G / 4;
+  static_assert(NV >= 1 && NV <= 4 && G >= 4, "one float4 per lane");
+  __shared__ float s_m[KS], s_d[KS];
+  load_affine(mm_prev, KS, k, s_m, s_d, true);
+  const int tid = threadIdx.x;
+  const int lg = tid % G, p = lg & 3, qi = lg >> 2;
+  const bool vl = p < NV;  // this lane carries vector p of a row
+  constexpr int GPB = kBlock / G;
+  const int ngroups = gridDim.x * GPB;
+  float lmn[4], lmx[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    lmn[c] = INFINITY;
+    lmx[c] = -INFINITY;
+  }
+  const float4 *src4 = reinterpret_cast<const float4 *>(src);
+  for (int rr = blockIdx.x * GPB + tid / G; rr < R; rr += ngroups) {
+    const int r = row0 + rr;
+    const int beg = rp[r], end = rp[r + 1];
+    if (end - beg > long_thresh) continue;  // seg_partial + long_finish
+    float4 self = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (MODE == MODE_FULL && qi == 0 && vl)
+      self = reinterpret_cast<const float4 *>(self_in)[(size_t)r * NV + p];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    float wsum = 0.f;
+    for (int base = beg + qi; base < end; base += Q * M) {
+      int c[M];
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        const int t = base + Q * m;
+        c[m] = t < end ? ((g_ablate & 2) ? -2 : col[t]) : -1;
+      }
+      float4 v[M];
+#pragma unroll
+      for (int m = 0; m < M; m++)
+        v[m] = (c[m] >= 0 && vl) ? src4[(size_t)c[m] * NV + p]
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        // weight = vector 0 .x of the row, held by lane 0 of the quad
+        const float w = hgx::dpp_f<0x00>(v[m].x);  // quad_perm [0,0,0,0]
+        if (c[m] >= 0) {
+          wsum += w;
+          acc = f4fma(w, v[m], acc);
+        }
+      }
+    }
+    wsum = quad_stride_sum<G>(wsum);
+    acc.x = quad_stride_sum<G>(acc.x);
+    acc.y = quad_stride_sum<G>(acc.y);
+    acc.z = quad_stride_sum<G>(acc.z);
+    acc.w = quad_stride_sum<G>(acc.w);
+    if (qi == 0 && vl) {
+      float4 *op = reinterpret_cast<float4 *>(out) + (size_t)r * NV + p;
+      if (MODE == MODE_PARTIAL) {
+        if (p == 0) acc.x = wsum;
+        *op = acc;
+      } else {
+        const float inv_w = 1.0f / wsum;
+        float4 o;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          const int i = 4 * p + c;
+          float v;
+          if (i == 0) {
+            v = 1.0f / (float)(end - beg);
+          } else if (i <= k) {
+            const float sv = (f4get(self, c) - s_m[i]) * s_d[i];
+            float mv = f4get(acc, c) * inv_w;
+            if (src_affine) mv = (mv - s_m[i]) * s_d[i];
+            v = (sv + mv) * 0.5f;
+            lmn[c] = fminf(lmn[c], v);
+            lmx[c] = fmaxf(lmx[c], v);
+          } else {
+            v = 0.f;
+          }
+          f4set(o, c, v);
+        }
+        *op = o;
+      }
+    }
+  }
+  if (MODE == MODE_FULL && !(g_ablate & 1) && !fskip_) {
+    // lane position p holds components 4p .. 4p+3
+    float mn[KS], mx[KS];
+#pragma unroll
+    for (int i = 0; i < KS; i++) {
+      mn[i] = (i / 4 == p) ? lmn[i % 4] : INFINITY;
+      mx[i] = (i / 4 == p) ? lmx[i % 4] : -INFINITY;
+    }
+    flush_minmax<KS>(mn, mx, k, mm_cur);
+  }
 }
 
 // Long rows, step 1: one wave per piece of `T` incidences of a long row
@@ -335,6 +473,7 @@ __global__ __launch_bounds__(kBlock) void algdist_long_finish(
     const float *__restrict__ self_in, float *__restrict__ out,
     const int *__restrict__ mm_prev, int src_affine, int *__restrict__ mm_cur,
     int k) {
+  HGX_FLUSH_SEL(k);
   constexpr int NV = KS / 4;
   __shared__ float s_m[KS], s_d[KS];
   load_affine(mm_prev, KS, k, s_m, s_d, true);
@@ -405,7 +544,7 @@ __global__ __launch_bounds__(kBlock) void algdist_long_finish(
       op[q] = o;
     }
   }
-  if (MODE == MODE_FULL) flush_minmax<KS>(lmn, lmx, k, mm_cur);
+  if (MODE == MODE_FULL && !fskip_) flush_minmax<KS>(lmn, lmx, k, mm_cur);
 }
 
 // Incidence-parallel half-sweep for narrow rows (KS <= 20). Rows are cut
@@ -426,6 +565,7 @@ __global__ __launch_bounds__(kBlock) void algdist_half_flat(
     const float *__restrict__ src, float *__restrict__ out,
     const int *__restrict__ mm_prev, int src_affine, int *__restrict__ mm_cur,
     int k) {
+  HGX_FLUSH_SEL(k);
   constexpr int NV = KS / 4;
   constexpr int W = kBlock / 64;
   constexpr int AS = KS + 1;  // odd stride: conflict-free per-row reads
@@ -559,7 +699,8 @@ __global__ __launch_bounds__(kBlock) void algdist_half_flat(
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  if (MODE == MODE_FULL && !(g_ablate & 1)) flush_minmax<KS>(lmn, lmx, k, mm_cur);
+  if (MODE == MODE_FULL && !(g_ablate & 1) && !fskip_)
+    flush_minmax<KS>(lmn, lmx, k, mm_cur);
 }
 
 // Wide rows (k > 19): one wave per destination row, the row's float4
@@ -571,6 +712,7 @@ __global__ __launch_bounds__(kBlock) void algdist_half_wide(
     const float *__restrict__ src, float *__restrict__ out,
     const int *__restrict__ mm_prev, int src_affine, int *__restrict__ mm_cur,
     int k) {
+  HGX_FLUSH_SEL(k);
   const int NV = KS / 4;
   __shared__ float s_m[2048], s_d[2048];
   load_affine(mm_prev, KS, k, s_m, s_d);
@@ -647,7 +789,7 @@ __global__ __launch_bounds__(kBlock) void algdist_half_wide(
       reinterpret_cast<float4 *>(out)[(size_t)r * NV + j] = o;
     }
   }
-  if (MODE == MODE_PARTIAL) return;
+  if (MODE == MODE_PARTIAL || fskip_) return;
 #pragma unroll
   for (int q = 0; q < MAXV; q++) {
     const int j = lane + 64 * q;
@@ -851,6 +993,53 @@ HalfFn narrow_for_g(int g) {
                          : narrow_for_gm<KS, MODE, 2>(g);
 }
 
+template <int KS, int MODE, int M>
+HalfFn quad_for_gm(int g) {
+  switch (g) {
+    case 4: return algdist_half_quad<KS, 4, MODE, M>;
+    case 8: return algdist_half_quad<KS, 8, MODE, M>;
+    case 16: return algdist_half_quad<KS, 16, MODE, M>;
+    case 32: return algdist_half_quad<KS, 32, MODE, M>;
+    default: return algdist_half_quad<KS, 64, MODE, M>;
+  }
+}
+
+// HGX_ALG_QM: incidences in flight per quad (2 or 4, default 4)
+template <int KS, int MODE>
+HalfFn quad_for_g(int g) {
+  static const int m = [] {
+    const char *e = getenv("HGX_ALG_QM");
+    return e ? atoi(e) : 4;
+  }();
+  return m <= 2 ? quad_for_gm<KS, MODE, 2>(g) : quad_for_gm<KS, MODE, 4>(g);
+}
+
+// quad-split rows (algdist_half_quad) for KS <= 16; HGX_ALG_QUAD=0 selects
+// algdist_half_narrow. G = 4 lanes per quad x Q quads, Q doubling while a
+// quad would stride more than HGX_ALG_QLPI (default 8) incidences.
+template <int MODE>
+HalfFn quad_fn(int ks, double avg, int &g) {
+  static const int on = [] {
+    const char *e = getenv("HGX_ALG_QUAD");
+    return e ? atoi(e) : 1;
+  }();
+  static const int qlpi = [] {
+    const char *e = getenv("HGX_ALG_QLPI");
+    return e ? std::max(1, atoi(e)) : 8;
+  }();
+  if (!on || ks > 16) return nullptr;
+  int q = 1;
+  while (q < 16 && q * qlpi < avg) q *= 2;
+  g = 4 * q;
+  switch (ks) {
+    case 4: return quad_for_g<4, MODE>(g);
+    case 8: return quad_for_g<8, MODE>(g);
+    case 12: return quad_for_g<12, MODE>(g);
+    case 16: return quad_for_g<16, MODE>(g);
+    default: return nullptr;
+  }
+}
+
 template <int MODE>
 HalfFn narrow_fn(int ks, int g) {
   switch (ks) {
@@ -866,8 +1055,9 @@ HalfFn narrow_fn(int ks, int g) {
 int launch_half(hgx_ctx *ctx, int mode, int row0, int R, const int *rp,
                 const int *col, const float *self_in, const float *src,
                 float *out, const int *mm_prev, int src_affine, int *mm_cur,
-                double avg, const int *blk, int nblk, LongRows *lr) {
-  const int k = ctx->k, KS = ctx->ks;
+                double avg, const int *blk, int nblk, LongRows *lr,
+                bool sample_flush = false) {
+  const int k = ctx->k | (sample_flush ? kSampleFlush : 0), KS = ctx->ks;
   if (R <= 0) return HGX_OK;
   static const bool flat_env = [] {
     const char *e = getenv("HGX_ALG_FLAT");
@@ -899,9 +1089,14 @@ int launch_half(hgx_ctx *ctx, int mode, int row0, int R, const int *rp,
                            src_affine, mm_cur, k);
       }
     }
-    const int g = pick_g(avg);
-    HalfFn fn = mode == MODE_FULL ? narrow_fn<MODE_FULL>(KS, g)
-                                  : narrow_fn<MODE_PARTIAL>(KS, g);
+    int g = 0;
+    HalfFn fn = mode == MODE_FULL ? quad_fn<MODE_FULL>(KS, avg, g)
+                                  : quad_fn<MODE_PARTIAL>(KS, avg, g);
+    if (!fn) {
+      g = pick_g(avg);
+      fn = mode == MODE_FULL ? narrow_fn<MODE_FULL>(KS, g)
+                             : narrow_fn<MODE_PARTIAL>(KS, g);
+    }
     hipLaunchKernelGGL(fn, dim3(grid_for(R, kBlock / g, resident_grid(fn))),
                        dim3(kBlock), 0,
                        ctx->stream, row0, R, rp, col, self_in, src, out,
@@ -1021,21 +1216,26 @@ extern "C" int hgx_alg_run(hgx_ctx *ctx, int iters) {
   int *mm = ctx->mm.as<int>();
   HGX_TRY(init_mm(ctx, mm, (int64_t)slot * iters));
   HGX_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  static const bool sample_env = [] {
+    const char *e = getenv("HGX_ALG_SAMPLE_FLUSH");
+    return !e || e[0] != '0';
+  }();
   for (int it = 0; it < iters; it++) {
     const int *prev = it ? mm + slot * (it - 1) : nullptr;
     int *cur = mm + slot * it;
+    const bool sample = sample_env && it + 1 < iters;
     float *xc = ctx->X[ctx->xcur].as<float>(), *xn = ctx->X[ctx->xcur ^ 1].as<float>();
     float *yc = ctx->Y[ctx->ycur].as<float>(), *yn = ctx->Y[ctx->ycur ^ 1].as<float>();
     // node half: self x (scaled), gathered y (scaled)
     HGX_TRY(launch_half(ctx, MODE_FULL, 0, ctx->N, ctx->rp_n.as<int>(),
                         ctx->col_n.as<int>(), xc, yc, xn, prev, prev != nullptr,
                         cur, ctx->avg_deg_n, ctx->blk_n.as<int>(), ctx->nblk_n,
-                        &ctx->long_n));
+                        &ctx->long_n, sample));
     // edge half: self y (scaled), gathered NEW x (raw)
     HGX_TRY(launch_half(ctx, MODE_FULL, 0, ctx->E, ctx->rp_e.as<int>(),
                         ctx->col_e.as<int>(), yc, xn, yn, prev, 0, cur,
                         ctx->avg_deg_e, ctx->blk_e.as<int>(), ctx->nblk_e,
-                        &ctx->long_e));
+                        &ctx->long_e, sample));
     ctx->xcur ^= 1;
     ctx->ycur ^= 1;
   }

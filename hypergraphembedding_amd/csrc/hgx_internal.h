@@ -180,4 +180,39 @@ __device__ __forceinline__ float group_allreduce_sum(float x) {
   return x;
 }
 
+// Whole-wave min / max without LDS traffic: the four in-row DPP steps, then
+// the four row results by v_readlane (wave-uniform result). ds_bpermute
+// shuffles go through the CU's LDS pipe: at a kernel tail where every
+// resident wave reduces ~20 values at once they queued for microseconds.
+// (a lane whose DPP source is disabled keeps its own value: neutral for
+// min / max)
+template <int ctrl>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(x, x, ctrl, 0xF, 0xF, false);
+}
+template <int ctrl>
+__device__ __forceinline__ float dpp_keep_f(float x) {
+  return __builtin_bit_cast(float, dpp_i<ctrl>(__builtin_bit_cast(int, x)));
+}
+__device__ __forceinline__ float wave_max(float x) {
+  x = fmaxf(x, dpp_keep_f<0xB1>(x));
+  x = fmaxf(x, dpp_keep_f<0x4E>(x));
+  x = fmaxf(x, dpp_keep_f<0x141>(x));
+  x = fmaxf(x, dpp_keep_f<0x140>(x));
+  const int b = __builtin_bit_cast(int, x);
+  return fmaxf(fmaxf(__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)),
+                     __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))),
+               fmaxf(__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)),
+                     __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48))));
+}
+__device__ __forceinline__ float wave_min(float x) { return -wave_max(-x); }
+__device__ __forceinline__ int wave_max_i(int x) {
+  x = max(x, dpp_i<0xB1>(x));
+  x = max(x, dpp_i<0x4E>(x));
+  x = max(x, dpp_i<0x141>(x));
+  x = max(x, dpp_i<0x140>(x));
+  return max(max(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
+             max(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
+}
+
 }  // namespace hgx
