@@ -1491,10 +1491,24 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   const size_t s3_f = (size_t)nblk1 * 2 * dp + 8 * (size_t)dp + (size_t)2 * NBF * 2 * dp;
   HGX_TRY(hgx_ensure(ctx, ctx->s3, sizeof(float) * s3_f));
   HGX_TRY(hgx_ensure(ctx, ctx->s4, sizeof(float) * (size_t)nbatches * lstride + 16));
-  HGX_TRY(hgx_ensure(ctx, ctx->s5, sizeof(int) * prep_ints));
+  // chunk buffers in two parities: train_prep of chunk c + 1 runs on a side
+  // stream while chunk c trains (graph replay bakes parity 0: one parity)
+  const bool use_graph = env_int("HGX_GRAPH", 0) == 1 && !fused;
+  // HGX_TRAIN_PIPE: 0 (default) = one parity, prep of chunk c + 1 queued
+  // right after chunk c (the host waits for it with the GPU idle, ~0.1 ms per
+  // 1024 batches); 1 = two parities, prep of chunk c + 1 queued on the same
+  // stream BEFORE chunk c's batches (no host bubble); 2 = two parities, prep
+  // on a side stream beside the batches. Measured r01 at d=128 (4M records):
+  // 8.61 / 8.90 / 9.45 us per batch. The packed records a prep has just
+  // written sit in the Infinity Cache when the batches right behind it read
+  // them; preparing a chunk ahead lets 9 ms of training traffic evict them,
+  // and a second active stream also slows every batch launch.
+  const int pipe = use_graph ? 0 : env_int("HGX_TRAIN_PIPE", 0);
+  const int NPAR = pipe == 0 ? 1 : 2;
+  HGX_TRY(hgx_ensure(ctx, ctx->s5, sizeof(int) * prep_ints * NPAR));
   HGX_TRY(hgx_ensure(ctx, ctx->s6, 64 + sizeof(double) * kLossBlocks));  // loss
   int *perm = ctx->s1.as<int>();
-  HGX_HIP(ctx, hipMemsetAsync(ctx->s5.p, 0, sizeof(int) * prep_ints, ctx->stream));
+  HGX_HIP(ctx, hipMemsetAsync(ctx->s5.p, 0, sizeof(int) * prep_ints * NPAR, ctx->stream));
   HGX_HIP(ctx, hipMemsetAsync(ctx->s3.p, 0, sizeof(float) * s3_f, ctx->stream));
   TrainArgs a;
   a.idx = ctx->rec_idx.as<int>();
@@ -1554,6 +1568,25 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     q += CB;
     a.pfast = q;
   }
+  // parity 1: the same layout shifted by prep_ints
+  TrainArgs ap[2] = {a, a};
+  if (NPAR == 2) {
+    const size_t sh = prep_ints;
+    TrainArgs &b = ap[1];
+    b.bidx += sh;
+    b.btgt += sh;
+    b.inv += sh;
+    b.ukey += sh;
+    b.uoff += sh;
+    b.ucount += sh;
+    b.bmeta = reinterpret_cast<int2 *>(reinterpret_cast<int *>(b.bmeta) + sh);
+    b.pidx += sh;
+    b.pcode += sh;
+    b.ptgt += sh;
+    b.pnval += sh;
+    b.pnblk += sh;
+    b.pfast += sh;
+  }
   double *dloss = reinterpret_cast<double *>(ctx->s6.as<char>() + 32);
   double *dpart = reinterpret_cast<double *>(ctx->s6.as<char>() + 64);
 
@@ -1581,17 +1614,20 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
       for (auto g : gexec) (void)hipGraphExecDestroy(g);
       for (auto g : graph) (void)hipGraphDestroy(g);
       for (auto e : ev) (void)hipEventDestroy(e);
+      if (side) (void)hipStreamDestroy(side);
+      if (hflags) (void)hipHostFree(hflags);
     }
+    hipStream_t side = nullptr;
+    int *hflags = nullptr;  // pinned [NPAR][2][CB]: pfast, pnblk per parity
   } res;
   // Direct launches by default: measured as fast as hipGraph replay of the
   // same kernels (10.6 us per batch both ways at d=128) with less host time,
   // and rocprofv3 kernel tracing crashes on the replays. HGX_GRAPH=1 replays
   // captured graphs instead.
-  const bool use_graph = env_int("HGX_GRAPH", 0) == 1 && !fused;
-  auto launch_run = [&](int cb0, int nrun) {
+  auto launch_run = [&](const TrainArgs &ac, int cb0, int nrun) {
     for (int b = cb0; b < cb0 + nrun; b++) {
-      hipLaunchKernelGGL(k1, dim3(nblk1), dim3(tb1), 0, ctx->stream, a, b);
-      hipLaunchKernelGGL(k2, dim3(grid2), dim3(tb2), 0, ctx->stream, a, b);
+      hipLaunchKernelGGL(k1, dim3(nblk1), dim3(tb1), 0, ctx->stream, ac, b);
+      hipLaunchKernelGGL(k2, dim3(grid2), dim3(tb2), 0, ctx->stream, ac, b);
     }
   };
   if (use_graph) {
@@ -1599,7 +1635,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
       hipGraph_t gr = nullptr;
       hipGraphExec_t ge = nullptr;
       HGX_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
-      launch_run(g * GB, GB);
+      launch_run(a, g * GB, GB);
       hipError_t ce = hipStreamEndCapture(ctx->stream, &gr);
       if (ce != hipSuccess)
         return hgx_fail(ctx, HGX_EHIP, "graph capture failed: %s", hipGetErrorString(ce));
@@ -1617,7 +1653,52 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     res.ev.push_back(e);
   }
 
-  std::vector<int> hperm, hfast, hnblk;
+  // prep pipeline: side stream, per parity "prep done + flags copied" and
+  // "chunk trained" events
+  hipEvent_t ev_prep[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr},
+             ev_perm = nullptr;
+  if (pipe == 2) HGX_HIP(ctx, hipStreamCreateWithFlags(&res.side, hipStreamNonBlocking));
+  hipStream_t ps = pipe == 2 ? res.side : ctx->stream;  // prep stream
+  HGX_HIP(ctx, hipHostMalloc(reinterpret_cast<void **>(&res.hflags),
+                             sizeof(int) * 4 * (size_t)CB));
+  for (int i = 0; i < 2; i++) {
+    HGX_HIP(ctx, hipEventCreateWithFlags(&ev_prep[i], hipEventDisableTiming));
+    res.ev.push_back(ev_prep[i]);
+    HGX_HIP(ctx, hipEventCreateWithFlags(&ev_free[i], hipEventDisableTiming));
+    res.ev.push_back(ev_free[i]);
+  }
+  HGX_HIP(ctx, hipEventCreateWithFlags(&ev_perm, hipEventDisableTiming));
+  res.ev.push_back(ev_perm);
+  // both parities start free
+  for (int i = 0; i < 2; i++) HGX_HIP(ctx, hipEventRecord(ev_free[i], ctx->stream));
+  // train_prep of chunk c into parity c % NPAR on the side stream, after the
+  // epoch's permutation and after the parity's previous chunk trained; then
+  // its packing flags to pinned host memory
+  auto issue_prep = [&](int64_t c) -> int {
+    const int par = (int)(c % NPAR);
+    const TrainArgs &ac = ap[par];
+    const int64_t base = c * CB;
+    const int nbc = (int)std::min<int64_t>(CB, nbatches - base);
+    if (ps != ctx->stream) {
+      HGX_HIP(ctx, hipStreamWaitEvent(ps, ev_perm, 0));
+      HGX_HIP(ctx, hipStreamWaitEvent(ps, ev_free[par], 0));
+    }
+    hipLaunchKernelGGL(train_prep, dim3(CB), dim3(kTB),
+                       (size_t)P * sizeof(unsigned long long), ps, ac,
+                       base, nbc, P);
+    HGX_LAUNCH_CHECK(ctx);
+    if (fused) {
+      int *hf = res.hflags + (size_t)par * 2 * CB;
+      HGX_HIP(ctx, hipMemcpyAsync(hf, ac.pfast, sizeof(int) * nbc,
+                                  hipMemcpyDeviceToHost, ps));
+      HGX_HIP(ctx, hipMemcpyAsync(hf + CB, ac.pnblk, sizeof(int) * nbc,
+                                  hipMemcpyDeviceToHost, ps));
+    }
+    HGX_HIP(ctx, hipEventRecord(ev_prep[par], ps));
+    return HGX_OK;
+  };
+
+  std::vector<int> hperm;
   int64_t nfused = 0, nsplit = 0;
   double batch_ms = 0.0;
   double best = INFINITY;
@@ -1657,25 +1738,31 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     (void)hipMemsetAsync(dloss, 0, sizeof(double), ctx->stream);
     (void)hipMemsetAsync(a.lossbuf, 0, sizeof(float) * (size_t)nbatches * lstride,
                          ctx->stream);
+    if (hipEventRecord(ev_perm, ctx->stream) != hipSuccess ||
+        (rc = issue_prep(0)) != HGX_OK) {
+      if (!rc) rc = hgx_fail(ctx, HGX_EHIP, "prep pipeline failed");
+      break;
+    }
     for (int64_t c = 0; c < nchunks && rc == HGX_OK; c++) {
+      const int par = (int)(c % NPAR);
+      const TrainArgs &ac = ap[par];
       const int64_t base = c * CB;
       const int nbc = (int)std::min<int64_t>(CB, nbatches - base);
-      hipLaunchKernelGGL(train_prep, dim3(CB), dim3(kTB),
-                         (size_t)P * sizeof(unsigned long long), ctx->stream,
-                         a, base, nbc, P);
-      if (fused) {
-        // which batches packed: one host read per chunk of up to 1024
-        hfast.resize(nbc);
-        hnblk.resize(nbc);
-        if (hipMemcpyAsync(hfast.data(), a.pfast, sizeof(int) * nbc,
-                           hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
-            hipMemcpyAsync(hnblk.data(), a.pnblk, sizeof(int) * nbc,
-                           hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
-            hipStreamSynchronize(ctx->stream) != hipSuccess) {
-          rc = hgx_fail(ctx, HGX_EHIP, "batch preparation failed: %s",
-                        hipGetErrorString(hipGetLastError()));
-          break;
-        }
+      const int *hfast = res.hflags + (size_t)par * 2 * CB;
+      const int *hnblk = hfast + CB;
+      // which batches packed: one host wait per chunk, normally long done
+      // (prep c ran beside chunk c - 1)
+      if (hipEventSynchronize(ev_prep[par]) != hipSuccess ||
+          (ps != ctx->stream &&
+           hipStreamWaitEvent(ctx->stream, ev_prep[par], 0) != hipSuccess)) {
+        rc = hgx_fail(ctx, HGX_EHIP, "batch preparation failed: %s",
+                      hipGetErrorString(hipGetLastError()));
+        break;
+      }
+      if (NPAR == 1 && c + 1 < nchunks) {
+        // one parity: chunk c + 1's prep must follow chunk c (queued below)
+      } else if (c + 1 < nchunks && (rc = issue_prep(c + 1)) != HGX_OK) {
+        break;
       }
       (void)hipEventRecord(bev[2 * c], ctx->stream);
       if (fused) {
@@ -1685,22 +1772,22 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
             const int64_t gbat = base + b;
             const int nrec = (int)std::min<int64_t>(batch, n - gbat * batch);
             hipLaunchKernelGGL(kf, dim3(NBF), dim3(tbf),
-                               (size_t)MS * L * sizeof(float4), ctx->stream, a,
+                               (size_t)MS * L * sizeof(float4), ctx->stream, ac,
                                b, (int)gbat, nrec, qrun > 0 ? hnblk[b - 1] : 0,
                                qrun, qrun > 0 ? 1 : 0);
             qrun++;
             nfused++;
           } else {
             if (qrun > 0)
-              hipLaunchKernelGGL(kfl, dim3(1), dim3(tbf), 0, ctx->stream, a,
+              hipLaunchKernelGGL(kfl, dim3(1), dim3(tbf), 0, ctx->stream, ac,
                                  b - 1, qrun - 1);
             qrun = 0;
-            launch_run(b, 1);
+            launch_run(ac, b, 1);
             nsplit++;
           }
         }
         if (qrun > 0)
-          hipLaunchKernelGGL(kfl, dim3(1), dim3(tbf), 0, ctx->stream, a,
+          hipLaunchKernelGGL(kfl, dim3(1), dim3(tbf), 0, ctx->stream, ac,
                              nbc - 1, qrun - 1);
       } else if (use_graph) {
         for (int g = 0; g * GB < nbc; g++) {
@@ -1710,10 +1797,12 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
           }
         }
       } else {
-        launch_run(0, nbc);
+        launch_run(ac, 0, nbc);
         nsplit += nbc;
       }
       (void)hipEventRecord(bev[2 * c + 1], ctx->stream);
+      (void)hipEventRecord(ev_free[par], ctx->stream);
+      if (NPAR == 1 && c + 1 < nchunks && (rc = issue_prep(c + 1)) != HGX_OK) break;
     }
     if (rc) break;
     hipLaunchKernelGGL(loss_partial, dim3(kLossBlocks), dim3(kTB), 0,
