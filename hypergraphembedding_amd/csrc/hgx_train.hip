@@ -475,18 +475,18 @@ __global__ __launch_bounds__(TB) void train_update(TrainArgs a, int cb) {
 // fixed order (thread `sub` of a column: partials sub, sub+TPC, ...; then
 // the TPC sums in order) and returns the column's (p, acc) on sub == 0.
 // col < 2L covers both tables (table = col / L, float4 column col % L).
-template <int L, int TB>
+template <int L, int TB, int NBFM>
 struct Row0Loads {
-  static constexpr int NC = 2 * L, TPC = TB / NC, MAXPER = kPackNBF / TPC;
+  static constexpr int NC = 2 * L, TPC = TB / NC, MAXPER = (NBFM + TPC - 1) / TPC;
   float4 gv[MAXPER];
   float4 rp, ra, tp, ta;
 };
 
-template <int L, int TB>
+template <int L, int TB, int NBFM>
 __device__ __forceinline__ void row0_issue_state(const TrainArgs &a,
                                                  const float4 *r0src,
-                                                 Row0Loads<L, TB> &ld) {
-  using RL = Row0Loads<L, TB>;
+                                                 Row0Loads<L, TB, NBFM> &ld) {
+  using RL = Row0Loads<L, TB, NBFM>;
   static_assert(TB % RL::NC == 0, "workgroup covers whole columns");
   const int col = threadIdx.x % RL::NC;
   const int tab = col / L, c = col % L;
@@ -496,14 +496,15 @@ __device__ __forceinline__ void row0_issue_state(const TrainArgs &a,
   ld.ta = reinterpret_cast<const float4 *>(tab ? a.eacc : a.nacc)[c];
 }
 
-// partials [0, nmax) of gpsrc (nmax <= kPackNBF), issued unconditionally
+// partials [0, nmax) of gpsrc (nmax <= NBFM, the instantiation's workgroup
+// cap: MAXPER = NBFM / TPC loads per thread), issued unconditionally
 // (index clamped: a branch around a load makes the compiler wait for it at
 // the join); row0_stage masks the clamped copies (the gp buffer is zeroed at
 // hgx_train entry, so it only ever holds finite partials).
-template <int L, int TB>
+template <int L, int TB, int NBFM>
 __device__ __forceinline__ void row0_issue_partials(int nmax, const float4 *gpsrc,
-                                                    Row0Loads<L, TB> &ld) {
-  using RL = Row0Loads<L, TB>;
+                                                    Row0Loads<L, TB, NBFM> &ld) {
+  using RL = Row0Loads<L, TB, NBFM>;
   const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
   const int last = max(nmax - 1, 0);
 #pragma unroll
@@ -512,10 +513,10 @@ __device__ __forceinline__ void row0_issue_partials(int nmax, const float4 *gpsr
 }
 
 // this thread's fixed-order partial sum of partials [0, np) -> s_red
-template <int L, int TB>
-__device__ __forceinline__ void row0_stage(int np, const Row0Loads<L, TB> &ld,
+template <int L, int TB, int NBFM>
+__device__ __forceinline__ void row0_stage(int np, const Row0Loads<L, TB, NBFM> &ld,
                                            float4 (*s_red)[2 * L]) {
-  using RL = Row0Loads<L, TB>;
+  using RL = Row0Loads<L, TB, NBFM>;
   const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
   float4 g = f4(0.f);
 #pragma unroll
@@ -529,16 +530,17 @@ __device__ __forceinline__ void row0_stage(int np, const Row0Loads<L, TB> &ld,
 
 // after row0_stage: the workgroup barrier, then the column owners (sub == 0)
 // add the TPC staged sums in order and apply Adagrad (mode 1)
-template <int L, int TB>
+// p0 / a0 arrive holding the selected state (mode ? pending : table),
+// picked right after row0_stage: that forces the state loads' wait BEFORE the
+// gathers are issued (a wait for them after the wave-uniform list-gather
+// branch would be counted conservatively and drain most gathers).
+template <int L, int TB, int NBFM>
 __device__ __forceinline__ void row0_finish(const TrainArgs &a, int mode,
-                                            const Row0Loads<L, TB> &ld,
                                             float4 (*s_red)[2 * L], float4 &p0,
                                             float4 &a0) {
-  using RL = Row0Loads<L, TB>;
+  using RL = Row0Loads<L, TB, NBFM>;
   const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
   __syncthreads();
-  p0 = mode ? ld.rp : ld.tp;
-  a0 = mode ? ld.ra : ld.ta;
   if (sub == 0 && mode) {
     float4 gs = f4(0.f);
 #pragma unroll
@@ -561,7 +563,7 @@ __device__ __forceinline__ void row0_finish(const TrainArgs &a, int mode,
 // One L-lane group per record (dp == 4L), prpb = TB / L records per
 // workgroup, NBF workgroups; q = position in the run of consecutive fused
 // launches, mode = q > 0.
-template <int L, int KMAX, int MODE, int TB>
+template <int L, int KMAX, int MODE, int TB, int NBFM>
 __global__ __launch_bounds__(TB) void train_fused(TrainArgs a, int cb, int gb,
                                                   int nb, int np, int q,
                                                   int mode) {
@@ -595,23 +597,36 @@ __global__ __launch_bounds__(TB) void train_fused(TrainArgs a, int cb, int gb,
   const int nval = a.pnval[(size_t)cb * NBF + blockIdx.x];
   if (!mode) np = 0;
   const size_t par = (size_t)NBF * 2 * L;  // float4 per gp parity
-  Row0Loads<L, TB> r0l;
-  row0_issue_state<L, TB>(a, reinterpret_cast<const float4 *>(a.r0) + (q & 1) * 4 * L,
+  Row0Loads<L, TB, NBFM> r0l;
+  row0_issue_state<L, TB, NBFM>(a, reinterpret_cast<const float4 *>(a.r0) + (q & 1) * 4 * L,
                           r0l);
-  row0_issue_partials<L, TB>(np, reinterpret_cast<const float4 *>(a.gp) + ((q - 1) & 1) * par,
+  row0_issue_partials<L, TB, NBFM>(np, reinterpret_cast<const float4 *>(a.gp) + ((q - 1) & 1) * par,
                              r0l);
   HGX_STAMP(ts[1]);
   if (nval == 0) return;  // unused workgroup of this batch
   const bool has = grp < nval;
   // staged before the gathers: frees the partials' registers
-  row0_stage<L, TB>(np, r0l, s_red);
+  row0_stage<L, TB, NBFM>(np, r0l, s_red);
+  float4 p0 = mode ? r0l.rp : r0l.tp, a0 = mode ? r0l.ra : r0l.ta;
+  // pin the selects here (the compiler would sink them past the gathers)
+  asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(a0.x),
+               "+v"(a0.y), "+v"(a0.z), "+v"(a0.w));
   // round trip 2: every slot's table row and owner slots' accumulator
-  // rows. All unconditional (row 0 /
-  // non-owner slots read row 0, a hot line): a load under a branch is
-  // waited for at the join, which would serialise the gathers.
+  // rows. Per slot unconditional (row 0 / non-owner slots read row 0, a hot
+  // line): a load under a per-lane branch is waited for at the join, which
+  // would serialise the gathers. The neighbour-list slots 4.. are skipped by
+  // a WAVE-uniform branch when no record of the wave has a list (nn / ee
+  // records: all list slots are the padding row, whose value comes from
+  // s_r0 below): they are 20 of a record's 28 row loads, and a CU's load
+  // issue (64 B/clk) is a large part of this phase. HGX_TRAIN_ABLATE & 256
+  // disables the skip.
   float4 Pv[R], Av[R];
+  bool lists = false;
 #pragma unroll
-  for (int s = 0; s < R; s++) {
+  for (int s = 4; s < R; s++) lists |= row[s] != 0;
+  const bool wave_lists = (g_tab & 256) || __any(lists);
+#pragma unroll
+  for (int s = 0; s < 4; s++) {
     const bool edge = slot_is_edge(s, K);
     const float4 *T = reinterpret_cast<const float4 *>(edge ? a.etab : a.ntab);
     const float4 *Ac = reinterpret_cast<const float4 *>(edge ? a.eacc : a.nacc);
@@ -619,9 +634,19 @@ __global__ __launch_bounds__(TB) void train_fused(TrainArgs a, int cb, int gb,
     Pv[s] = T[(size_t)row[s] * L + lane];
     Av[s] = Ac[(size_t)arow * L + lane];
   }
+  if (wave_lists) {
+#pragma unroll
+    for (int s = 4; s < R; s++) {
+      const bool edge = slot_is_edge(s, K);
+      const float4 *T = reinterpret_cast<const float4 *>(edge ? a.etab : a.ntab);
+      const float4 *Ac = reinterpret_cast<const float4 *>(edge ? a.eacc : a.nacc);
+      const int arow = (code[s] & kCodeOwn) ? row[s] : 0;
+      Pv[s] = T[(size_t)row[s] * L + lane];
+      Av[s] = Ac[(size_t)arow * L + lane];
+    }
+  }
   {
-    float4 p0, a0;
-    row0_finish<L, TB>(a, mode, r0l, s_red, p0, a0);
+    row0_finish<L, TB, NBFM>(a, mode, s_red, p0, a0);
     const int col = threadIdx.x % (2 * L), sub = threadIdx.x / (2 * L);
     if (sub == 0) {
       s_r0[col / L][col % L] = p0;
@@ -744,18 +769,18 @@ __global__ __launch_bounds__(TB) void train_fused(TrainArgs a, int cb, int gb,
 
 // After the last launch q of a fused run: the pending padding-row update ->
 // row 0 of both tables and accumulators.
-template <int L, int TB>
+template <int L, int TB, int NBFM>
 __global__ __launch_bounds__(TB) void train_row0_flush(TrainArgs a, int cb, int q) {
   __shared__ float4 s_red[TB / (2 * L)][2 * L];
   const size_t par = (size_t)a.NBF * 2 * L;
-  Row0Loads<L, TB> r0l;
-  row0_issue_state<L, TB>(a, reinterpret_cast<const float4 *>(a.r0) + ((q + 1) & 1) * 4 * L,
+  Row0Loads<L, TB, NBFM> r0l;
+  row0_issue_state<L, TB, NBFM>(a, reinterpret_cast<const float4 *>(a.r0) + ((q + 1) & 1) * 4 * L,
                           r0l);
-  row0_issue_partials<L, TB>(a.NBF, reinterpret_cast<const float4 *>(a.gp) + (q & 1) * par,
+  row0_issue_partials<L, TB, NBFM>(a.NBF, reinterpret_cast<const float4 *>(a.gp) + (q & 1) * par,
                              r0l);
-  row0_stage<L, TB>(a.pnblk[cb], r0l, s_red);
-  float4 p0, a0;
-  row0_finish<L, TB>(a, 1, r0l, s_red, p0, a0);
+  row0_stage<L, TB, NBFM>(a.pnblk[cb], r0l, s_red);
+  float4 p0 = r0l.rp, a0 = r0l.ra;
+  row0_finish<L, TB, NBFM>(a, 1, s_red, p0, a0);
   const int col = threadIdx.x % (2 * L), sub = threadIdx.x / (2 * L);
   if (sub == 0) {
     const int tab = col / L, c = col % L;
@@ -804,9 +829,10 @@ __device__ int block_exclusive_scan(int v, int *total, int *s_ws) {
 __device__ void pack_batch(const TrainArgs &a, int cb, int nb, int V, int P,
                            const unsigned long long *s_key, int *s_ws) {
   __shared__ int s_lab[kPackB], s_csz[kPackB], s_cms[kPackB], s_cblk[kPackB],
-      s_cfill[kPackB], s_cmoff[kPackB], s_grp[kPackB];
+      s_cmoff[kPackB], s_grp[kPackB];
   __shared__ int s_mrun[kPackM], s_mlen[kPackM], s_mbase[kPackM];
-  __shared__ int s_bfill[kPackNBF];
+  __shared__ int s_bfill[kPackNBF], s_bshort[kPackNBF], s_blong[kPackNBF];
+  __shared__ unsigned char s_short[kPackB];
   __shared__ int s_flag[2], s_ok;
   const int R = a.R, RPB = a.prpb, NBF = a.NBF, MS = a.MS;
   volatile int *lab = s_lab;
@@ -878,6 +904,15 @@ __device__ void pack_batch(const TrainArgs &a, int cb, int nb, int V, int P,
       }
     }
   }
+  // records without neighbour lists (nn / ee): placed first in their
+  // workgroup so that whole waves skip the list-slot gathers in train_fused
+  const int64_t rbase = (int64_t)a.bmeta[cb].y * a.B;
+  for (int i = threadIdx.x; i < nb; i += kTB) {
+    const int *ri = a.idx + (int64_t)a.perm[rbase + i] * R;
+    int any = 0;
+    for (int s2 = 4; s2 < R; s2++) any |= ri[s2];
+    s_short[i] = any == 0;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     int ok = conv && M <= kPackM && NBF <= kPackNBF;
@@ -899,7 +934,6 @@ __device__ void pack_batch(const TrainArgs &a, int cb, int nb, int V, int P,
         break;
       }
       s_cblk[i] = blk;
-      s_cfill[i] = fill;
       s_cmoff[i] = msf;
       fill += sz;
       msf += q;
@@ -907,9 +941,18 @@ __device__ void pack_batch(const TrainArgs &a, int cb, int nb, int V, int P,
     if (ok) {
       s_bfill[blk] = fill;
       for (int j = blk + 1; j < NBF; j++) s_bfill[j] = 0;
+      // positions inside a workgroup: records without lists first, then the
+      // others, each in record order (the workgroup of a record, and so the
+      // packing, is unchanged; multi-slot codes index LDS, not positions)
+      for (int j = 0; j <= blk; j++) s_bshort[j] = 0;
+      for (int i = 0; i < nb; i++) s_bshort[s_cblk[lab[i]]] += s_short[i];
+      for (int j = 0; j <= blk; j++) {
+        s_blong[j] = s_bshort[j];
+        s_bshort[j] = 0;
+      }
       for (int i = 0; i < nb; i++) {
-        const int r = lab[i];
-        s_grp[i] = s_cblk[r] * RPB + s_cfill[r]++;
+        const int b = s_cblk[lab[i]];
+        s_grp[i] = b * RPB + (s_short[i] ? s_bshort[b]++ : s_blong[b]++);
       }
       for (int k = 0; k < M; k++) {
         const int r = lab[slotof(s_mrun[k]) / R];
@@ -1186,20 +1229,28 @@ using KFusedFn = void (*)(TrainArgs, int, int, int, int, int, int);
 using KFlushFn = void (*)(TrainArgs, int, int);
 
 // fused one-launch step: d in (64, 256] (one float4 per lane, L = 32 or 64),
-// K = 5 with the FOBE (sigmoid/KLD) or HOBE (relu/MSE) heads
-bool pick_fused(int L, int VPL, int K, int loss, int act, KFusedFn &kf,
+// K = 5 with the FOBE (sigmoid/KLD) or HOBE (relu/MSE) heads. NBFM = the
+// workgroup cap of the instantiation (40 when the batch packs into at most
+// 40 workgroups, else kPackNBF): every workgroup of the next launch loads
+// ceil(NBFM / TPC) padding-row partials per thread.
+template <int L, int TB, int NBFM>
+void fused_fns(int loss, KFusedFn &kf, KFlushFn &kfl) {
+  kf = loss == 0 ? train_fused<L, 5, 1, TB, NBFM> : train_fused<L, 5, 2, TB, NBFM>;
+  kfl = train_row0_flush<L, TB, NBFM>;
+}
+bool pick_fused(int L, int VPL, int K, int loss, int act, int nbfm, KFusedFn &kf,
                 KFlushFn &kfl, int &tb) {
   if (VPL != 1 || K != 5 || loss != act) return false;
   if (L == 32) {
     tb = 256;
-    kf = loss == 0 ? train_fused<32, 5, 1, 256> : train_fused<32, 5, 2, 256>;
-    kfl = train_row0_flush<32, 256>;
+    if (nbfm <= 40) fused_fns<32, 256, 40>(loss, kf, kfl);
+    else fused_fns<32, 256, kPackNBF>(loss, kf, kfl);
     return true;
   }
   if (L == 64) {
     tb = 512;
-    kf = loss == 0 ? train_fused<64, 5, 1, 512> : train_fused<64, 5, 2, 512>;
-    kfl = train_row0_flush<64, 512>;
+    if (nbfm <= 40) fused_fns<64, 512, 40>(loss, kf, kfl);
+    else fused_fns<64, 512, kPackNBF>(loss, kf, kfl);
     return true;
   }
   return false;
@@ -1452,16 +1503,28 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   KFusedFn kf = nullptr;
   KFlushFn kfl = nullptr;
   int tbf = 0;
-  // HGX_TRAIN_FUSED: 0 off, 1 (default) d in (64, 128] (L = 32), 2 also
-  // d in (128, 256] (L = 64: measured slower than the two-kernel step on the
-  // C4 FOBE stream, 14.8 vs 13.9 us/batch, r01)
-  const int fz = env_int("HGX_TRAIN_FUSED", 1);
+  // HGX_TRAIN_FUSED: 0 off, 1 only d in (64, 128] (L = 32), 2 (default)
+  // also d in (128, 256] (L = 64; r01: 12.7 vs 12.7 us/batch with the wide
+  // workgroup cap, 11.3 vs 12.7 with the 40-workgroup cap and the list-gather
+  // skip)
+  const int fz = env_int("HGX_TRAIN_FUSED", 2);
+  // workgroups per fused batch: the records' lane groups plus headroom for
+  // packing holes (components placed whole, first fit): +8 when that stays
+  // within 40 (the NBFM = 40 instantiation, fewer padding-row partial loads
+  // per workgroup; HGX_TRAIN_NBF_WIDE=1 keeps the wide cap), else 50% + 2 up
+  // to kPackNBF. A batch that needs more takes the two-kernel step.
+  const int tb_f = L == 64 ? 512 : 256;
+  const int prpb0 = tb_f / L;
+  const int need0 = (batch + prpb0 - 1) / prpb0;
+  const bool narrow_nbf = need0 + 8 <= 40 && env_int("HGX_TRAIN_NBF_WIDE", 0) != 1;
+  const int nbf_target = narrow_nbf ? need0 + 8 : std::min(kPackNBF, need0 + need0 / 2 + 2);
   bool fused = fz != 0 && (L == 32 || fz == 2) &&
                env_int("HGX_TRAIN_GENERIC", 0) != 1 &&
-               pick_fused(L, VPL, K, loss, act, kf, kfl, tbf) && batch <= kPackB;
+               pick_fused(L, VPL, K, loss, act, nbf_target, kf, kfl, tbf) &&
+               batch <= kPackB;
   const int prpb = fused ? tbf / L : 0;
   const int nbf_need = fused ? (batch + prpb - 1) / prpb : 0;
-  const int NBF = fused ? std::min(kPackNBF, nbf_need + nbf_need / 2 + 2) : 0;
+  const int NBF = fused ? nbf_target : 0;
   if (fused && NBF < nbf_need) fused = false;
   const int MS = 48;  // LDS rows for multi-slot gradients per workgroup
   const int lstride = std::max(nblk1, NBF);
