@@ -831,7 +831,7 @@ __device__ void pack_batch(const TrainArgs &a, int cb, int nb, int V, int P,
   __shared__ int s_lab[kPackB], s_csz[kPackB], s_cms[kPackB], s_cblk[kPackB],
       s_cmoff[kPackB], s_grp[kPackB];
   __shared__ int s_mrun[kPackM], s_mlen[kPackM], s_mbase[kPackM];
-  __shared__ int s_bfill[kPackNBF], s_bshort[kPackNBF], s_blong[kPackNBF];
+  __shared__ int s_bfill[kPackNBF], s_bshort[kPackNBF];
   __shared__ unsigned char s_short[kPackB];
   __shared__ int s_flag[2], s_ok;
   const int R = a.R, RPB = a.prpb, NBF = a.NBF, MS = a.MS;
@@ -914,58 +914,105 @@ __device__ void pack_batch(const TrainArgs &a, int cb, int nb, int V, int P,
     s_short[i] = any == 0;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  // Component placement, first fit in record order. The scan is sequential,
+  // so wave 0 runs it in scalar registers: every record's packed
+  // (size | multi-slot count << 10, 0 for a non-root) sits in a VGPR of its
+  // lane and is read by a wave-uniform readlane; the results go back into
+  // the root's lane by a lane-select. No LDS round trip sits on the chain (one
+  // thread walking LDS arrays took most of train_prep's time).
+  if (threadIdx.x < 64) {
+    constexpr int U = kPackB / 64;
+    const int lane = threadIdx.x;
+    int pk[U], rb[U], ro[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int i = u * 64 + lane;
+      pk[u] = (i < nb && lab[i] == i) ? (s_csz[i] | (s_cms[i] << 10)) : 0;
+      rb[u] = ro[u] = 0;
+    }
     int ok = conv && M <= kPackM && NBF <= kPackNBF;
     int fill = 0, msf = 0, blk = 0;
-    for (int i = 0; i < nb && ok; i++) {
-      if (lab[i] != i) continue;
-      const int sz = s_csz[i], q = s_cms[i];
-      if (sz > RPB || q > MS) {
-        ok = 0;
-        break;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (u * 64 >= nb) break;
+      for (int l = 0; l < 64 && ok; l++) {
+        const int v = __builtin_amdgcn_readlane(pk[u], l);
+        if (v == 0) continue;
+        const int sz = v & 1023, q = v >> 10;
+        if (sz > RPB || q > MS) {
+          ok = 0;
+          break;
+        }
+        if (fill + sz > RPB || msf + q > MS) {
+          if (lane == 0) s_bfill[blk] = fill;
+          blk++;
+          fill = msf = 0;
+        }
+        if (blk >= NBF) {
+          ok = 0;
+          break;
+        }
+        if (lane == l) {
+          rb[u] = blk;
+          ro[u] = msf;
+        }
+        fill += sz;
+        msf += q;
       }
-      if (fill + sz > RPB || msf + q > MS) {
-        s_bfill[blk] = fill;
-        blk++;
-        fill = msf = 0;
-      }
-      if (blk >= NBF) {
-        ok = 0;
-        break;
-      }
-      s_cblk[i] = blk;
-      s_cmoff[i] = msf;
-      fill += sz;
-      msf += q;
     }
     if (ok) {
-      s_bfill[blk] = fill;
-      for (int j = blk + 1; j < NBF; j++) s_bfill[j] = 0;
-      // positions inside a workgroup: records without lists first, then the
-      // others, each in record order (the workgroup of a record, and so the
-      // packing, is unchanged; multi-slot codes index LDS, not positions)
-      for (int j = 0; j <= blk; j++) s_bshort[j] = 0;
-      for (int i = 0; i < nb; i++) s_bshort[s_cblk[lab[i]]] += s_short[i];
-      for (int j = 0; j <= blk; j++) {
-        s_blong[j] = s_bshort[j];
-        s_bshort[j] = 0;
-      }
-      for (int i = 0; i < nb; i++) {
-        const int b = s_cblk[lab[i]];
-        s_grp[i] = b * RPB + (s_short[i] ? s_bshort[b]++ : s_blong[b]++);
-      }
-      for (int k = 0; k < M; k++) {
-        const int r = lab[slotof(s_mrun[k]) / R];
-        s_mbase[k] = s_cmoff[r];
-        s_cmoff[r] += s_mlen[k];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        if (pk[u] != 0) {
+          s_cblk[u * 64 + lane] = rb[u];
+          s_cmoff[u * 64 + lane] = ro[u];
+        }
       }
     }
-    s_ok = ok;
-    a.pfast[cb] = ok;
-    a.pnblk[cb] = ok ? blk + 1 : 0;
+    if (lane == 0) {
+      if (ok) s_bfill[blk] = fill;
+      s_ok = ok;
+      s_flag[0] = blk + 1;
+      a.pfast[cb] = ok;
+      a.pnblk[cb] = ok ? blk + 1 : 0;
+    }
   }
   __syncthreads();
   if (!s_ok) return;
+  {
+    // positions inside a workgroup: records without lists first, then the
+    // others, each in record order (the workgroup of a record, and so the
+    // packing, is unchanged; multi-slot codes index LDS, not positions).
+    // s_csz now holds each record's key = block * 2 + no-list flag; s_mlen
+    // gets its run's component in the upper half.
+    const int nblk = s_flag[0];
+    for (int j = threadIdx.x; j < NBF; j += kTB) {
+      if (j < nblk) s_bshort[j] = 0;
+      else s_bfill[j] = 0;
+    }
+    for (int i = threadIdx.x; i < nb; i += kTB) s_csz[i] = s_cblk[lab[i]] * 2 + s_short[i];
+    for (int k = threadIdx.x; k < M; k += kTB)
+      s_mlen[k] |= lab[slotof(s_mrun[k]) / R] << 16;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nb; i += kTB)
+      if (s_short[i]) atomicAdd(&s_bshort[s_csz[i] >> 1], 1);
+    __syncthreads();
+    // rank among the earlier records of the same key; a multi-slot run's
+    // base = its component's offset + the runs of that component before it
+    for (int i = threadIdx.x; i < nb; i += kTB) {
+      const int key = s_csz[i], b = key >> 1;
+      int r = 0;
+      for (int j = 0; j < i; j++) r += s_csz[j] == key;
+      s_grp[i] = b * RPB + ((key & 1) ? r : s_bshort[b] + r);
+    }
+    for (int k = threadIdx.x; k < M; k += kTB) {
+      const int comp = s_mlen[k] >> 16;
+      int base = s_cmoff[comp];
+      for (int j = 0; j < k; j++)
+        if ((s_mlen[j] >> 16) == comp) base += s_mlen[j] & 0xffff;
+      s_mbase[k] = base;
+    }
+  }
   const int G = NBF * RPB;
   int *pidx = a.pidx + (size_t)cb * G * R;
   unsigned *pcode = reinterpret_cast<unsigned *>(a.pcode) + (size_t)cb * G * R;
@@ -995,7 +1042,7 @@ __device__ void pack_batch(const TrainArgs &a, int cb, int nb, int V, int P,
     }
   }
   for (int k = threadIdx.x; k < M; k += kTB) {
-    const int t = s_mrun[k], c = s_mlen[k], base = s_mbase[k];
+    const int t = s_mrun[k], c = s_mlen[k] & 0xffff, base = s_mbase[k];
     for (int j = 0; j < c; j++) {
       const int sl = slotof(t + j), i = sl / R;
       unsigned code = kCodeMulti | (unsigned)(base + j);
