@@ -1,12 +1,12 @@
 #!/bin/bash
-# One GPU session: trainer tests, trainer perf, bench line, rocprofv3 kernel
+# One GPU session: the GPU test suite, trainer perf, bench line, rocprofv3 kernel
 # stats of the bench, FETCH/WRITE PMC passes of the trainer (separate runs).
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_train.py -x -q --timeout 120 --timeout-method thread > $O/t_train.log 2>&1 || exit 11
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread --durations=25 > $O/gpu_tests.log 2>&1 || exit 11
 timeout -k 10 120 python tools/perf_train.py 128 > $O/perf_train.log 2>&1 || exit 12
 timeout -k 10 120 python tools/perf_train.py 256 >> $O/perf_train.log 2>&1 || exit 13
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || exit 14
