@@ -161,8 +161,13 @@ __device__ __forceinline__ uint32_t bounded(uint64_t r, uint32_t n) {
 // Sum over aligned groups of G lanes (G a power of two <= 64); every lane of
 // the group gets the sum. Steps inside a 16-lane DPP row are single VALU ops
 // (quad_perm xor1 / xor2, row_half_mirror, row_mirror pair lanes whose
-// partial sums are disjoint); only the 16- and 32-lane steps go through
-// ds_bpermute.
+// partial sums are disjoint). The 16- and 32-lane steps are gfx950's
+// v_permlane16_swap / v_permlane32_swap (VALU half exchanges, no LDS pipe):
+// with x in two registers, the swap leaves x_i in one and x_{i^16} (x_{i^32})
+// in the other on every lane, so their sum is the xor-shuffle step's value
+// bit for bit (float addition commutes). Inline asm with two "+v" operands
+// keeps them in distinct registers (the builtin with one value for both
+// operands gave wrong sums); s_nop 1 covers the VALU-write -> permlane hazard.
 template <int ctrl>
 __device__ __forceinline__ float dpp_f(float x) {
   return __builtin_bit_cast(
@@ -175,8 +180,16 @@ __device__ __forceinline__ float group_allreduce_sum(float x) {
   if (G >= 4) x += dpp_f<0x4E>(x);   // quad_perm [2,3,0,1]
   if (G >= 8) x += dpp_f<0x141>(x);  // row_half_mirror
   if (G >= 16) x += dpp_f<0x140>(x); // row_mirror
-  if (G >= 32) x += __shfl_xor(x, 16);
-  if (G >= 64) x += __shfl_xor(x, 32);
+  if (G >= 32) {
+    float a = x, b = x;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    x = a + b;
+  }
+  if (G >= 64) {
+    float a = x, b = x;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    x = a + b;
+  }
   return x;
 }
 
