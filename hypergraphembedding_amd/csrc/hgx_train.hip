@@ -588,10 +588,28 @@ __global__ __launch_bounds__(TB) void train_fused(TrainArgs a, int cb, int gb,
   const float *yt = a.ptgt + gi * 3;
   int row[R];
   unsigned code[R];
+  {
+    // one id and one code load per lane (lane s of the group loads slot s),
+    // then readlanes broadcast the group's slots: 2 load instructions
+    // instead of 2R on the first round trip. L = 64: one record per wave,
+    // the ids land in scalar registers; L = 32: two records per wave.
+    static_assert(L == 32 || L == 64, "fused step geometry");
+    const int sl = lane < R ? lane : 0;
+    const int rv = ri[sl];
+    const int cv = (int)rc[sl];
 #pragma unroll
-  for (int s = 0; s < R; s++) {
-    row[s] = ri[s];
-    code[s] = rc[s];
+    for (int s = 0; s < R; s++) {
+      if (L == 64) {
+        row[s] = __builtin_amdgcn_readlane(rv, s);
+        code[s] = (unsigned)__builtin_amdgcn_readlane(cv, s);
+      } else {
+        const bool hi = threadIdx.x & 32;
+        const int r0 = __builtin_amdgcn_readlane(rv, s), r1 = __builtin_amdgcn_readlane(rv, 32 + s);
+        const int c0 = __builtin_amdgcn_readlane(cv, s), c1 = __builtin_amdgcn_readlane(cv, 32 + s);
+        row[s] = hi ? r1 : r0;
+        code[s] = (unsigned)(hi ? c1 : c0);
+      }
+    }
   }
   const float yt0 = yt[0], yt1 = yt[1], yt2 = yt[2];
   const int nval = a.pnval[(size_t)cb * NBF + blockIdx.x];
