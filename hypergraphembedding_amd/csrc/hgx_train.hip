@@ -611,7 +611,20 @@ __global__ __launch_bounds__(TB) void train_fused(TrainArgs a, int cb, int gb,
       }
     }
   }
-  const float yt0 = yt[0], yt1 = yt[1], yt2 = yt[2];
+  // targets: at L = 64 (one record per wave) lane c < 3 loads target c and
+  // readlanes broadcast them (scalar); at L = 32 three broadcast loads
+  // measured faster than the two-record select
+  float yt0, yt1, yt2;
+  if (L == 64) {
+    const int tv = __float_as_int(yt[lane < 3 ? lane : 0]);
+    yt0 = __int_as_float(__builtin_amdgcn_readlane(tv, 0));
+    yt1 = __int_as_float(__builtin_amdgcn_readlane(tv, 1));
+    yt2 = __int_as_float(__builtin_amdgcn_readlane(tv, 2));
+  } else {
+    yt0 = yt[0];
+    yt1 = yt[1];
+    yt2 = yt[2];
+  }
   const int nval = a.pnval[(size_t)cb * NBF + blockIdx.x];
   if (!mode) np = 0;
   const size_t par = (size_t)NBF * 2 * L;  // float4 per gp parity
