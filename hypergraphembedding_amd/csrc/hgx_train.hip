@@ -105,6 +105,7 @@ constexpr unsigned kCodeOwn = 0x40000000u;    // this slot applies the update
 constexpr int kPackB = 512;                   // max records per fused batch
 constexpr int kPackM = 1024;                  // max multi-slot rows per batch
 constexpr int kPackNBF = 64;                  // max fused workgroups per batch
+constexpr int kPrepB = 1366;  // max records per prepared batch: 8192 slots / R >= 6
 
 __device__ __forceinline__ bool slot_is_edge(int s, int K) {
   return s == 1 || s == 3 || s >= 4 + K;
@@ -937,9 +938,12 @@ __device__ void pack_batch(const TrainArgs &a, int cb, int nb, int V, int P,
   }
   // records without neighbour lists (nn / ee): placed first in their
   // workgroup so that whole waves skip the list-slot gathers in train_fused
-  const int64_t rbase = (int64_t)a.bmeta[cb].y * a.B;
+  // (from the batch-ordered copies train_prep wrote: contiguous, no
+  // dependent record-id load)
+  const int *bidx = a.bidx + (size_t)cb * a.B * R;
+  const float *btgt = a.btgt + (size_t)cb * a.B * 3;
   for (int i = threadIdx.x; i < nb; i += kTB) {
-    const int *ri = a.idx + (int64_t)a.perm[rbase + i] * R;
+    const int *ri = bidx + i * R;
     int any = 0;
     for (int s2 = 4; s2 < R; s2++) any |= ri[s2];
     s_short[i] = any == 0;
@@ -1055,14 +1059,27 @@ __device__ void pack_batch(const TrainArgs &a, int cb, int nb, int V, int P,
   for (int t = threadIdx.x; t < G * 3; t += kTB) ptgt[t] = 0.f;
   for (int j = threadIdx.x; j < NBF; j += kTB) a.pnval[(size_t)cb * NBF + j] = s_bfill[j];
   __syncthreads();  // zero fill before the scattered writes (same workgroup)
-  const int64_t r0 = (int64_t)a.bmeta[cb].y * a.B;
-  for (int t = threadIdx.x; t < nb * R; t += kTB) {
-    const int i = t / R, s = t - i * R;
-    pidx[s_grp[i] * R + s] = a.idx[(int64_t)a.perm[r0 + i] * R + s];
+  // 8 loads per thread in flight before the stores (a global store between
+  // two loads would make each load wait for the previous one)
+  for (int t0 = threadIdx.x; t0 < nb * R; t0 += 8 * kTB) {
+    int v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int t = t0 + u * kTB;
+      v[u] = t < nb * R ? bidx[t] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int t = t0 + u * kTB;
+      if (t < nb * R) {
+        const int i = t / R;
+        pidx[s_grp[i] * R + (t - i * R)] = v[u];
+      }
+    }
   }
   for (int t = threadIdx.x; t < nb * 3; t += kTB) {
     const int i = t / 3, c = t - i * 3;
-    ptgt[s_grp[i] * 3 + c] = a.tgt[(int64_t)a.perm[r0 + i] * 3 + c];
+    ptgt[s_grp[i] * 3 + c] = btgt[t];
   }
   for (int t = threadIdx.x; t < V; t += kTB) {
     const bool prev = t > 0 && rowkey(t) == rowkey(t - 1);
@@ -1101,23 +1118,37 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
   const int S = nb * R;
   int *bidx = a.bidx + (size_t)cb * a.B * R;
   float *btgt = a.btgt + (size_t)cb * a.B * 3;
+  // the batch's record ids once into LDS, then every gather below has one
+  // round trip; slot rows 8 per thread in flight before the stores
+  __shared__ int s_perm[kPrepB];
+  for (int i = threadIdx.x; i < nb; i += kTB) s_perm[i] = a.perm[r0 + i];
+  __syncthreads();
   for (int t = threadIdx.x; t < nb * 3; t += kTB) {
     const int i = t / 3;
-    btgt[t] = a.tgt[(int64_t)a.perm[r0 + i] * 3 + (t - 3 * i)];
+    btgt[t] = a.tgt[(int64_t)s_perm[i] * 3 + (t - 3 * i)];
   }
-  for (int t = threadIdx.x; t < P; t += kTB) {
-    unsigned long long key = ~0ull;
-    if (t < S) {
-      const int i = t / R, s = t % R;
-      const int rec = a.perm[r0 + i];
-      const int row = a.idx[(int64_t)rec * R + s];
-      bidx[t] = row;
-      if (row != 0) {
-        const unsigned k32 = ((unsigned)slot_is_edge(s, K) << 30) | (unsigned)row;
-        key = ((unsigned long long)k32 << 32) | (unsigned)t;
-      }
+  for (int t0 = threadIdx.x; t0 < P; t0 += 8 * kTB) {
+    int rv[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int t = t0 + u * kTB, i = t / R;
+      rv[u] = t < S ? a.idx[(int64_t)s_perm[i] * R + (t - i * R)] : 0;
     }
-    s_key[t] = key;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int t = t0 + u * kTB;
+      if (t >= P) break;
+      unsigned long long key = ~0ull;
+      if (t < S) {
+        const int s = t % R, row = rv[u];
+        bidx[t] = row;
+        if (row != 0) {
+          const unsigned k32 = ((unsigned)slot_is_edge(s, K) << 30) | (unsigned)row;
+          key = ((unsigned long long)k32 << 32) | (unsigned)t;
+        }
+      }
+      s_key[t] = key;
+    }
   }
   __syncthreads();
   for (int size = 2; size <= P; size <<= 1) {
