@@ -480,21 +480,25 @@ template <int L, int TB, int NBFM>
 struct Row0Loads {
   static constexpr int NC = 2 * L, TPC = TB / NC, MAXPER = (NBFM + TPC - 1) / TPC;
   float4 gv[MAXPER];
-  float4 rp, ra, tp, ta;
+  float4 rp, ra;  // the selected row-0 state (pending or table)
 };
 
 template <int L, int TB, int NBFM>
 __device__ __forceinline__ void row0_issue_state(const TrainArgs &a,
-                                                 const float4 *r0src,
+                                                 const float4 *r0src, int mode,
                                                  Row0Loads<L, TB, NBFM> &ld) {
   using RL = Row0Loads<L, TB, NBFM>;
   static_assert(TB % RL::NC == 0, "workgroup covers whole columns");
   const int col = threadIdx.x % RL::NC;
   const int tab = col / L, c = col % L;
-  ld.rp = r0src[(tab * 2) * L + c];
-  ld.ra = r0src[(tab * 2 + 1) * L + c];
-  ld.tp = reinterpret_cast<const float4 *>(tab ? a.etab : a.ntab)[c];
-  ld.ta = reinterpret_cast<const float4 *>(tab ? a.eacc : a.nacc)[c];
+  // the address is selected (mode is wave-uniform), not the loaded value:
+  // two loads instead of four on the first round trip
+  const float4 *sp = mode ? r0src + (tab * 2) * L
+                          : reinterpret_cast<const float4 *>(tab ? a.etab : a.ntab);
+  const float4 *sa = mode ? r0src + (tab * 2 + 1) * L
+                          : reinterpret_cast<const float4 *>(tab ? a.eacc : a.nacc);
+  ld.rp = sp[c];
+  ld.ra = sa[c];
 }
 
 // partials [0, nmax) of gpsrc (nmax <= NBFM, the instantiation's workgroup
@@ -631,7 +635,7 @@ __global__ __launch_bounds__(TB) void train_fused(TrainArgs a, int cb, int gb,
   const size_t par = (size_t)NBF * 2 * L;  // float4 per gp parity
   Row0Loads<L, TB, NBFM> r0l;
   row0_issue_state<L, TB, NBFM>(a, reinterpret_cast<const float4 *>(a.r0) + (q & 1) * 4 * L,
-                          r0l);
+                                mode, r0l);
   row0_issue_partials<L, TB, NBFM>(np, reinterpret_cast<const float4 *>(a.gp) + ((q - 1) & 1) * par,
                              r0l);
   HGX_STAMP(ts[1]);
@@ -639,7 +643,7 @@ __global__ __launch_bounds__(TB) void train_fused(TrainArgs a, int cb, int gb,
   const bool has = grp < nval;
   // staged before the gathers: frees the partials' registers
   row0_stage<L, TB, NBFM>(np, r0l, s_red);
-  float4 p0 = mode ? r0l.rp : r0l.tp, a0 = mode ? r0l.ra : r0l.ta;
+  float4 p0 = r0l.rp, a0 = r0l.ra;
   // pin the selects here (the compiler would sink them past the gathers)
   asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(a0.x),
                "+v"(a0.y), "+v"(a0.z), "+v"(a0.w));
@@ -807,7 +811,7 @@ __global__ __launch_bounds__(TB) void train_row0_flush(TrainArgs a, int cb, int 
   const size_t par = (size_t)a.NBF * 2 * L;
   Row0Loads<L, TB, NBFM> r0l;
   row0_issue_state<L, TB, NBFM>(a, reinterpret_cast<const float4 *>(a.r0) + ((q + 1) & 1) * 4 * L,
-                          r0l);
+                                1, r0l);
   row0_issue_partials<L, TB, NBFM>(a.NBF, reinterpret_cast<const float4 *>(a.gp) + (q & 1) * par,
                              r0l);
   row0_stage<L, TB, NBFM>(a.pnblk[cb], r0l, s_red);
