@@ -663,6 +663,15 @@ __global__ __launch_bounds__(TB) void train_fused(TrainArgs a, int cb, int gb,
   const bool wave_lists = (g_tab & 256) || __any(lists);
 #pragma unroll
   for (int s = 0; s < 4; s++) {
+    // every record kind has two padding slots among the first four (ne:
+    // le, rn; nn: le, re; ee: ln, rn). At L = 64 (one record per wave, the
+    // ids are scalar) they are skipped: their value comes from s_r0 below.
+    // At L = 32 the two records of a wave may differ in kind, and the
+    // per-slot branch measured slower (7.80 -> 7.90 us per batch).
+    if (L == 64 && !(g_tab & 512) && row[s] == 0) {
+      Pv[s] = Av[s] = f4(0.f);
+      continue;
+    }
     const bool edge = slot_is_edge(s, K);
     const float4 *T = reinterpret_cast<const float4 *>(edge ? a.etab : a.ntab);
     const float4 *Ac = reinterpret_cast<const float4 *>(edge ? a.eacc : a.nacc);
