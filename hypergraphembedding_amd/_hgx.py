@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(HERE, "libhgx.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "hgx.h")
 
 HGX_OK, HGX_EINVAL, HGX_EHIP, HGX_ENOMEM = 0, -1, -2, -3
-HGX_EZERODIV, HGX_ESTATE, HGX_EUNSUP = -4, -5, -6
+HGX_EZERODIV, HGX_ESTATE, HGX_EUNSUP, HGX_EVALUE = -4, -5, -6, -7
 LOSS_KLD, LOSS_MSE = 0, 1
 ACT_SIGMOID, ACT_RELU = 0, 1
 HOBE_NN, HOBE_EE, HOBE_NE = 0, 1, 2
@@ -42,6 +42,7 @@ SIGNATURES = {
     "hgx_version": (_int, []),
     "hgx_set_stream": (_int, [_vp, _vp]),
     "hgx_synchronize": (_int, [_vp]),
+    "hgx_set_tuning": (_int, [_vp, ctypes.c_char_p, _i64]),
     "hgx_upload_incidence": (_int, [_vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]),
     "hgx_alg_dist": (_int, [_vp, _int, _int, _vp, _vp]),
     "hgx_alg_set": (_int, [_vp, _int, _vp, _vp]),
@@ -57,7 +58,9 @@ SIGNATURES = {
     "hgx_incidence_weights": (_int, [_vp, _int, ctypes.c_double, _vp, _vp]),
     "hgx_sample_fobe": (_int, [_vp, _u64, _int, _vp, _vp, _vp, _vp, _pi64]),
     "hgx_sample_hobe": (_int, [_vp, _u64, _int, _int, _pi64]),
+    "hgx_sample_hobe_rows": (_int, [_vp, _u64, _int, _vp, _vp, _int, _pi64]),
     "hgx_sample_last_stats": (_int, [_vp, _pi64, _pi64]),
+    "hgx_sample_uniform_rows": (_int, [_vp, _pi64]),
     "hgx_features_set": (_int, [_vp, _vp, _vp]),
     "hgx_sample_jaccard": (_int, [_vp, _u64, _int, _vp, _vp, _pi64]),
     "hgx_jaccard_probs": (_int, [_vp, _int, _i64, _vp, _vp, _vp]),
@@ -140,6 +143,8 @@ def _raise(rc, msg):
     raise AssertionError(msg)
   if rc == HGX_EZERODIV:
     raise ZeroDivisionError(msg)
+  if rc == HGX_EVALUE:
+    raise ValueError(msg)
   raise HgxError(f"libhgx error {rc}: {msg}")
 
 
@@ -186,6 +191,11 @@ class Context:
 
   def synchronize(self):
     self._chk(lib().hgx_synchronize(self.h))
+
+  def set_tuning(self, key, value):
+    """Pick between exact implementations (hgx_set_tuning): sample_reject_w,
+    sample_mode3, train_fused, alg_long, alg_ks."""
+    self._chk(lib().hgx_set_tuning(self.h, key.encode(), int(value)))
 
   # ---- incidence ----
   def upload(self, inc):
@@ -270,10 +280,19 @@ class Context:
                                     ctypes.byref(n)))
     return n.value
 
-  def sample_hobe(self, seed, K, S):
+  def sample_hobe(self, seed, K, S, node_q=None, edge_q=None):
+    """AlgebraicDistanceSamples on the device; with node_q / edge_q only
+    those rows (quota per row instead of S)."""
     n = ctypes.c_int64()
-    self._chk(lib().hgx_sample_hobe(self.h, seed & (2**64 - 1), K, S,
-                                    ctypes.byref(n)))
+    if node_q is None and edge_q is None:
+      self._chk(lib().hgx_sample_hobe(self.h, seed & (2**64 - 1), K, S,
+                                      ctypes.byref(n)))
+    else:
+      nq, eq = _c(node_q, np.int32), _c(edge_q, np.int32)
+      assert nq.size == self.inc.N and eq.size == self.inc.E
+      self._chk(lib().hgx_sample_hobe_rows(self.h, seed & (2**64 - 1), K,
+                                           _ptr(nq), _ptr(eq), S,
+                                           ctypes.byref(n)))
     return n.value
 
   # weighted-Jaccard samplers
@@ -310,11 +329,17 @@ class Context:
     return p, j, v
 
   def sample_stats(self):
-    """(union-sampled 2-hop rows, fallbacks to expansion) of the last call."""
+    """(rows sampled by rejection, fallbacks to expansion) of the last call."""
     u, f = ctypes.c_int64(), ctypes.c_int64()
     self._chk(lib().hgx_sample_last_stats(self.h, ctypes.byref(u),
                                           ctypes.byref(f)))
     return u.value, f.value
+
+  def sample_uniform_rows(self):
+    """3-hop rows of the last call sampled by uniform-column rejection."""
+    u = ctypes.c_int64()
+    self._chk(lib().hgx_sample_uniform_rows(self.h, ctypes.byref(u)))
+    return u.value
 
   def records_set(self, idx, tgt):
     idx = _c(idx, np.int32)

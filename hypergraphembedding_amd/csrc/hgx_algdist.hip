@@ -50,7 +50,11 @@ enum { MODE_FULL = 0, MODE_PARTIAL = 1 };
 // diagnostic ablation bits (HGX_ALG_ABLATE, timing experiments only):
 // 1 = skip the min/max flush, 2 = skip the source gathers, 4 = flush
 // without its global atomics
-__constant__ int g_ablate = 0;
+#ifdef HGX_DEBUG_KNOBS
+__constant__ int g_ablate = 0;  // ablation bits (diagnostic builds only)
+#else
+static constexpr int g_ablate = 0;
+#endif
 
 __device__ __forceinline__ float4 f4fma(float w, float4 v, float4 a) {
   return make_float4(fmaf(w, v.x, a.x), fmaf(w, v.y, a.y), fmaf(w, v.z, a.z),
@@ -921,8 +925,7 @@ int resident_grid(F fn) {
 
 int pick_g(double avg) {
   static const int lpi = [] {  // incidences per lane targeted
-    const char *e = getenv("HGX_ALG_LPI");
-    return e ? atoi(e) : 4;
+    return hgx_debug_env("HGX_ALG_LPI", 4);
   }();
   int g = 1;
   while (g < 64 && g * lpi < avg) g *= 2;
@@ -985,8 +988,7 @@ HalfFn narrow_for_gm(int g) {
 template <int KS, int MODE>
 HalfFn narrow_for_g(int g) {
   static const int m = [] {
-    const char *e = getenv("HGX_ALG_M");
-    return e ? atoi(e) : 2;
+    return hgx_debug_env("HGX_ALG_M", 2);
   }();
   return m >= 4 ? narrow_for_gm<KS, MODE, 4>(g)
                 : m == 1 ? narrow_for_gm<KS, MODE, 1>(g)
@@ -1008,8 +1010,7 @@ HalfFn quad_for_gm(int g) {
 template <int KS, int MODE>
 HalfFn quad_for_g(int g) {
   static const int m = [] {
-    const char *e = getenv("HGX_ALG_QM");
-    return e ? atoi(e) : 4;
+    return hgx_debug_env("HGX_ALG_QM", 4);
   }();
   return m <= 2 ? quad_for_gm<KS, MODE, 2>(g) : quad_for_gm<KS, MODE, 4>(g);
 }
@@ -1020,12 +1021,10 @@ HalfFn quad_for_g(int g) {
 template <int MODE>
 HalfFn quad_fn(int ks, double avg, int &g) {
   static const int on = [] {
-    const char *e = getenv("HGX_ALG_QUAD");
-    return e ? atoi(e) : 1;
+    return hgx_debug_env("HGX_ALG_QUAD", 1);
   }();
   static const int qlpi = [] {
-    const char *e = getenv("HGX_ALG_QLPI");
-    return e ? std::max(1, atoi(e)) : 8;
+    return std::max(1, hgx_debug_env("HGX_ALG_QLPI", 8));
   }();
   if (!on || ks > 16) return nullptr;
   int q = 1;
@@ -1060,8 +1059,7 @@ int launch_half(hgx_ctx *ctx, int mode, int row0, int R, const int *rp,
   const int k = ctx->k | (sample_flush ? kSampleFlush : 0), KS = ctx->ks;
   if (R <= 0) return HGX_OK;
   static const bool flat_env = [] {
-    const char *e = getenv("HGX_ALG_FLAT");
-    return e && e[0] == '1';
+    return hgx_debug_env("HGX_ALG_FLAT", 0) == 1;
   }();
   if (KS <= 20 && flat_env) {
     FlatFn fn = mode == MODE_FULL ? flat_fn<MODE_FULL>(KS) : flat_fn<MODE_PARTIAL>(KS);
@@ -1165,10 +1163,9 @@ extern "C" int hgx_alg_set(hgx_ctx *ctx, int k, const float *node_xy,
   HGX_TRY(check_nonempty(ctx));
   int KS = ((k + 1) + 3) / 4 * 4;
   {
-    // rows of 12 floats straddle 64-byte sectors; HGX_ALG_KS forces a wider
-    // row stride (diagnostic / tuning)
-    const char *e = getenv("HGX_ALG_KS");
-    const int want = e ? atoi(e) : 0;
+    // rows of 12 floats straddle 64-byte sectors; the alg_ks tuning forces
+    // a wider row stride
+    const int want = ctx->tune.alg_ks;
     if (want > KS && want % 4 == 0 && want <= 20) KS = want;
   }
   ctx->k = k;
@@ -1205,11 +1202,12 @@ extern "C" int hgx_alg_run(hgx_ctx *ctx, int iters) {
   HGX_CHECK(ctx, iters >= 0, HGX_EINVAL, "iterations must be >= 0");
   HGX_HIP(ctx, hipSetDevice(ctx->device));
   if (iters == 0) return HGX_OK;
+#ifdef HGX_DEBUG_KNOBS
   {
-    const char *ab = getenv("HGX_ALG_ABLATE");
-    int v = ab ? atoi(ab) : 0;
+    const int v = hgx_debug_env("HGX_ALG_ABLATE", 0);
     HGX_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_ablate), &v, sizeof(int)));
   }
+#endif
   const int KS = ctx->ks;
   const size_t slot = 2 * (size_t)KS * kRep;
   HGX_TRY(hgx_ensure(ctx, ctx->mm, sizeof(int) * slot * iters));
@@ -1217,8 +1215,7 @@ extern "C" int hgx_alg_run(hgx_ctx *ctx, int iters) {
   HGX_TRY(init_mm(ctx, mm, (int64_t)slot * iters));
   HGX_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
   static const bool sample_env = [] {
-    const char *e = getenv("HGX_ALG_SAMPLE_FLUSH");
-    return !e || e[0] != '0';
+    return hgx_debug_env("HGX_ALG_SAMPLE_FLUSH", 1) != 0;
   }();
   for (int it = 0; it < iters; it++) {
     const int *prev = it ? mm + slot * (it - 1) : nullptr;

@@ -80,7 +80,8 @@ extern "C" int hgx_destroy(hgx_ctx *ctx) {
                     &ctx->nacc, &ctx->eacc, &ctx->s0, &ctx->s1, &ctx->s2,
                     &ctx->s3, &ctx->s4, &ctx->s5, &ctx->s6, &ctx->s7,
                     &ctx->feat_n, &ctx->feat_e, &ctx->cn_p, &ctx->cn_j,
-                    &ctx->cn_v, &ctx->ce_p, &ctx->ce_j, &ctx->ce_v};
+                    &ctx->cn_v, &ctx->ce_p, &ctx->ce_j, &ctx->ce_v,
+                    &ctx->hw_n, &ctx->hw_e, &ctx->hw_self};
   for (DevBuf *b : bufs) hgx_release(*b);
   for (LongRows *l : {&ctx->long_n, &ctx->long_e, &ctx->long_sn, &ctx->long_el})
     for (DevBuf *b : {&l->seg, &l->off, &l->rows, &l->part}) hgx_release(*b);
@@ -98,6 +99,34 @@ extern "C" const char *hgx_last_error(const hgx_ctx *ctx) {
 extern "C" int hgx_set_stream(hgx_ctx *ctx, void *hip_stream) {
   if (!ctx) return HGX_EINVAL;
   ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+  return HGX_OK;
+}
+
+extern "C" int hgx_set_tuning(hgx_ctx *ctx, const char *key, int64_t value) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, key, HGX_EINVAL, "null tuning key");
+  const std::string k(key);
+  Tuning &t = ctx->tune;
+  if (k == "sample_reject_w") {
+    HGX_CHECK(ctx, value >= 0, HGX_EINVAL, "sample_reject_w must be >= 0");
+    t.sample_reject_w = value;
+  } else if (k == "sample_mode3") {
+    HGX_CHECK(ctx, value >= 0 && value <= 2, HGX_EINVAL, "sample_mode3 must be 0, 1 or 2");
+    t.sample_mode3 = (int)value;
+  } else if (k == "train_fused") {
+    HGX_CHECK(ctx, value == 0 || value == 1, HGX_EINVAL, "train_fused must be 0 or 1");
+    t.train_fused = (int)value;
+  } else if (k == "alg_long") {
+    HGX_CHECK(ctx, value == 0 || (value >= 64 && value <= (1 << 20)), HGX_EINVAL,
+              "alg_long must be 0 or in [64, 2^20]");
+    t.alg_long = (int)value;
+  } else if (k == "alg_ks") {
+    HGX_CHECK(ctx, value == 0 || (value % 4 == 0 && value <= 20), HGX_EINVAL,
+              "alg_ks must be 0 or a multiple of 4 <= 20");
+    t.alg_ks = (int)value;
+  } else {
+    return hgx_fail(ctx, HGX_EINVAL, "unknown tuning key '%s'", key);
+  }
   return HGX_OK;
 }
 
@@ -204,11 +233,7 @@ int hgx_make_row_blocks(hgx_ctx *ctx, const int32_t *rp, int32_t r0, int32_t r1,
 
 int hgx_make_long_rows(hgx_ctx *ctx, const int32_t *rp, int32_t r0, int32_t r1,
                        LongRows &out) {
-  static const int thresh = [] {
-    const char *e = getenv("HGX_ALG_LONG");  // diagnostic / tuning
-    const int v = e ? atoi(e) : 0;
-    return v >= 64 ? v : kLongRow;
-  }();
+  const int thresh = ctx->tune.alg_long >= 64 ? ctx->tune.alg_long : kLongRow;
   std::vector<int32_t> rows, off(1, 0);
   std::vector<int32_t> seg;  // pairs {row, piece}
   for (int32_t r = r0; r < r1; r++) {

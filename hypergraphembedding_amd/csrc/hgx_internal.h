@@ -6,6 +6,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "hgx.h"
@@ -30,6 +31,23 @@ struct LongRows {
   int nlong = 0, nseg = 0, thresh = 0;
 };
 constexpr int kLongRow = 512;
+
+// Per-context tuning (hgx_set_tuning). None of these changes the math or
+// the distribution of a result; they pick between exact implementations.
+struct Tuning {
+  // 2/3-hop sample rows with more expansion paths than this are sampled by
+  // rejection (0: always expand)
+  int64_t sample_reject_w = 1 << 15;
+  // 3-hop rejection proposal: 0 auto, 1 paths (Karp-Luby), 2 uniform columns
+  int sample_mode3 = 0;
+  // trainer: 1 fused one-launch batch step where a batch packs, 0 the
+  // two-kernel step for every batch
+  int train_fused = 1;
+  // alg-dist: long-row threshold (0: kLongRow) and coordinate row width
+  // (0: round_up(k + 1, 4))
+  int alg_long = 0;
+  int alg_ks = 0;
+};
 
 struct hgx_ctx {
   int device = 0;
@@ -74,6 +92,12 @@ struct hgx_ctx {
 
   // sampler diagnostics of the last hgx_sample_* call
   int64_t sample_union_rows = 0, sample_fallback_rows = 0;
+  int64_t sample_uniform_rows = 0;
+  Tuning tune;
+
+  // HOBE per-incidence distance weights (node-major, edge-major) and each
+  // edge's largest weight, built from the current alg coords
+  DevBuf hw_n, hw_e, hw_self;
 
   // ---- records (SamplesToModelInput layout) ----
   int64_t n_rec = 0;
@@ -91,6 +115,28 @@ struct hgx_ctx {
   // ---- scratch ----
   DevBuf s0, s1, s2, s3, s4, s5, s6, s7;
 };
+
+// Diagnostic knobs of the A/B experiments under tools/ (ablations, kernel
+// geometry): the environment is read only in a build with -DHGX_DEBUG_KNOBS
+// (tools/build_variant.sh); the release library always takes the default,
+// so no environment variable changes what it computes.
+inline int hgx_debug_env(const char *name, int dflt) {
+#ifdef HGX_DEBUG_KNOBS
+  const char *e = getenv(name);
+  return e && e[0] ? atoi(e) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
+}
+inline const char *hgx_debug_env_str(const char *name) {
+#ifdef HGX_DEBUG_KNOBS
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 int hgx_fail(hgx_ctx *ctx, int code, const char *fmt, ...);
 // alg-dist row-block partition of rows [r0, r1) of a CSR (host side)

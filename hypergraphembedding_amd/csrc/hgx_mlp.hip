@@ -1202,7 +1202,7 @@ int hgx_mlp_fit(hgx_mlp *m, int batch, int max_epochs, float lr, float eps,
   std::vector<double> bl(nb);
   std::vector<int> hperm;
   // debug: from batch HGX_MLP_GRAD_AT on, weights receive the raw gradient
-  const char *ga = getenv("HGX_MLP_GRAD_AT");
+  const char *ga = hgx_debug_env_str("HGX_MLP_GRAD_AT");
   const int64_t grad_at = ga ? atoll(ga) : -1;
   double best = INFINITY;
   int ran = 0;

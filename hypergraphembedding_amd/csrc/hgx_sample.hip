@@ -8,34 +8,45 @@
 //
 // The reference samples rows of explicit sparse products (A*A^T, A^T*A,
 // A*A^T*A, A^T*A*A^T built with scipy SpGEMM). Here no product is
-// materialised: one workgroup per row walks the 1/2/3-hop CSR expansion
-// with LDS block scans + binary search (one path endpoint per thread),
-// de-duplicates endpoints with a test-and-set bitmap (LDS when the column
-// space fits, else a per-workgroup slice in HBM) into a distinct list, and
-// picks an exactly uniform m-subset (m = min(q, distinct)) as the m smallest
-// 64-bit keys (hash(seed,row,col) << 32 | col) by an 8-pass LDS radix
-// select. The chosen columns are written sorted (deterministic for a seed).
-// The uniform draws come from a counter-based hash, so the sampled SET has
-// the reference's distribution but not numpy's MT19937 stream.
+// materialised. Rows with a quota are listed, then sampled in two passes:
 //
-// Large 2-hop rows (A*A^T, A^T*A with more than `reject_w` expansion paths,
-// e.g. every node of a power-law edge with 1e6 members) are not expanded.
-// They are sampled from the union U = U_m S_m (S_m = row m of the second
-// factor, m over row r of the first) by Karp-Luby rejection:
-//   1. draw a path uniformly: m with probability |S_m| / W, c uniform in S_m;
-//   2. accept iff m is the FIRST set holding c, i.e.
-//      m == min(row r of l1 ∩ row c of l1) (for both patterns the second
-//      factor is the transpose of the first);
-//   3. distinct accepted columns are kept in draw order until q are held.
-// Step 2 makes every c in U equally likely per draw; step 3 (sequential
-// draws, repeats rejected) yields a uniform q-subset, which is the
-// distribution of np.random.choice(U, q, replace=False). Draws are processed
-// in rounds of 256 in thread order, so the result is deterministic for a
-// seed. A row whose union turns out smaller than q (no progress for 32
-// rounds) falls back to expansion.
+// 1. `reject_rows` (2- and 3-hop patterns): rows whose expansion has more
+//    than `reject_w` paths are sampled from the union of the pattern row by
+//    rejection, never expanded. A workgroup draws 256 candidates per round
+//    and keeps the distinct accepted ones in draw order until q are held
+//    (an LDS hash set de-duplicates); sequential draws with repeats
+//    rejected give a uniform q-subset, the distribution of
+//    np.random.choice(row, q, replace=False). Rounds are processed in
+//    thread order, so the result is deterministic for a seed. Proposals:
+//      * 2-hop (Karp-Luby over paths r -> m -> c): m with probability
+//        |S_m| / W, c uniform in S_m; accept iff m is the FIRST set holding
+//        c, m == min(row_r(l1) ∩ row_c(l1)) (the second factor is the
+//        transpose of the first);
+//      * 3-hop, paths (Karp-Luby over r -> m1 -> m2 -> c): a uniform path
+//        (m1 weighted by its path count, m2 by |row m2 of l3| through a
+//        scan of l2's incidences), accepted iff (m1, m2) is the
+//        lexicographically first path to c;
+//      * 3-hop, uniform columns: c uniform over all columns, accepted iff
+//        (v, e) is in A A^T A, i.e. some e' in E(v) shares a node with e,
+//        probed from the smaller edge against each member's sorted edge
+//        list. Used when the path count exceeds the column count, where
+//        its acceptance rate |row| / ncols beats |row| / W.
+//    Rows with at most `reject_w` paths, rows with q > 2048 and rows whose
+//    rejection stalls (a union smaller than q) are deferred to pass 2.
+// 2. `expand_rows`: one workgroup per row walks the 1/2/3-hop CSR expansion
+//    with LDS block scans + binary search (one path endpoint per thread),
+//    de-duplicates endpoints with a test-and-set bitmap (LDS when the column
+//    space fits, else a per-workgroup slice in HBM) into a distinct list,
+//    and picks an exactly uniform m-subset (m = min(q, distinct)) as the m
+//    smallest 64-bit keys (hash(seed,row,col) << 32 | col) by an 8-pass LDS
+//    radix select. 1-hop rows are their own distinct list.
+// Chosen columns are written sorted (the reference's row order). The
+// uniform draws come from a counter-based hash, so the sampled SET has the
+// reference's distribution but not numpy's MT19937 stream.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <climits>
 #include <vector>
 
 #include "hgx_internal.h"
@@ -43,32 +54,14 @@
 namespace {
 
 constexpr int kSB = 256;      // sampler workgroup
-constexpr int kSelCap = 2048; // LDS sort capacity for the chosen columns
+constexpr int kSelCap = 2048; // LDS capacity for the chosen columns
+constexpr int kHashBits = 12; // LDS hash set of the chosen columns
+constexpr int kHash = 1 << kHashBits;
 
 enum Pattern { PAT_A = 0, PAT_AT, PAT_NN, PAT_EE, PAT_NNE, PAT_EEN };
 
 struct Csr {
   const int *rp, *col;
-};
-
-struct SampleArgs {
-  int pattern;
-  int nrows, ncols;
-  Csr l1, l2, l3;            // CSR used at each expansion level
-  int levels;
-  const int *quota;          // per row (nullptr -> quota_all)
-  int quota_all;
-  const int64_t *cap_off;    // exclusive scan of quotas
-  int *out_cols;             // capacity buffer
-  int *out_cnt;              // chosen per row
-  unsigned *bitmap_g;        // per-WG bitmap slices (global mode)
-  int *list_g;               // per-WG distinct lists
-  int64_t list_cap;          // per-WG list capacity
-  int *row_ctr;              // dynamic row queue
-  uint64_t seed;
-  int lds_bitmap;            // 1 -> bitmap in dynamic LDS
-  int64_t reject_w;          // 2-hop rows with more paths: rejection sampling
-  int *stats;                // [0] rows sampled by rejection, [1] fallbacks
 };
 
 __device__ int block_scan_excl(int v, int *total, int *s_ws) {
@@ -93,8 +86,32 @@ __device__ int block_scan_excl(int v, int *total, int *s_ws) {
   return base + inc - v;
 }
 
+__device__ long long block_scan_excl64(long long v, long long *total,
+                                       long long *s_ws) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  long long inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const long long o = __shfl_up(inc, off);
+    if (lane >= off) inc += o;
+  }
+  if (lane == 63) s_ws[wave] = inc;
+  __syncthreads();
+  long long base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kSB / 64; w++) {
+    const long long x = s_ws[w];
+    if (w < wave) base += x;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + inc - v;
+}
+
 // index i of the last entry with off[i] <= w (off ascending, n entries)
-__device__ __forceinline__ int upper_find(const int *off, int n, int w) {
+template <class T>
+__device__ __forceinline__ int upper_find(const T *off, int n, T w) {
   int lo = 0, hi = n - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -104,6 +121,17 @@ __device__ __forceinline__ int upper_find(const int *off, int n, int w) {
   return lo;
 }
 
+// position of x in sorted col[b, e), or -1
+__device__ __forceinline__ int find_sorted(const int *col, int b, int e, int x) {
+  int lo = b, hi = e;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (col[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return (lo < e && col[lo] == x) ? lo : -1;
+}
+
 __device__ __forceinline__ unsigned long long composite(uint64_t seed, int pat,
                                                         int row, int col) {
   const uint32_t h = (uint32_t)(hgx::rand64(seed, 0x100 + pat,
@@ -111,6 +139,100 @@ __device__ __forceinline__ unsigned long long composite(uint64_t seed, int pat,
                                                 (uint32_t)col) >> 32);
   return ((unsigned long long)h << 32) | (unsigned)col;
 }
+
+__device__ void bitonic_sort_int(int *a, int n) {
+  int P = 1;
+  while (P < n) P <<= 1;
+  for (int t = n + threadIdx.x; t < P; t += kSB) a[t] = 0x7fffffff;
+  __syncthreads();
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < P / 2; t += kSB) {
+        const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const int x = a[lo], y = a[hi];
+        if ((x > y) == up) {
+          a[lo] = y;
+          a[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// smallest element of sorted a[0..na) that is also in sorted b[0..nb)
+// (INT_MAX if none): walk the shorter list, binary-search the longer one
+__device__ int first_common(const int *a, int na, const int *b, int nb) {
+  if (na > nb) {
+    const int *t = a;
+    a = b;
+    b = t;
+    const int tn = na;
+    na = nb;
+    nb = tn;
+  }
+  int lo = 0;
+  for (int i = 0; i < na; i++) {
+    const int x = a[i];
+    int hi = nb;
+    while (lo < hi) {  // first b[j] >= x, from the previous position on
+      const int mid = (lo + hi) >> 1;
+      if (b[mid] < x) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo == nb) return INT_MAX;
+    if (b[lo] == x) return x;
+  }
+  return INT_MAX;
+}
+
+// ---- 3-hop membership (A: node -> edges, AT: edge -> nodes) --------------
+// Smallest node in members(x) ∩ members(y) (INT_MAX if none): the smaller
+// edge's members in ascending order, each probed for the other edge in its
+// own sorted edge list; the first hit is the minimum.
+__device__ int edges_min_common(const Csr &A, const Csr &AT, int x, int y) {
+  if (x == y) return AT.rp[x + 1] > AT.rp[x] ? AT.col[AT.rp[x]] : INT_MAX;
+  if (AT.rp[x + 1] - AT.rp[x] > AT.rp[y + 1] - AT.rp[y]) {
+    const int t = x;
+    x = y;
+    y = t;
+  }
+  for (int t = AT.rp[x]; t < AT.rp[x + 1]; t++) {
+    const int u = AT.col[t];
+    if (find_sorted(A.col, A.rp[u], A.rp[u + 1], y) >= 0) return u;
+  }
+  return INT_MAX;
+}
+
+// (v, e) in A A^T A (equivalently (e, v) in A^T A A^T): some edge of v
+// shares a node with e. E(v) is walked in ascending id order.
+__device__ bool ne3_member(const Csr &A, const Csr &AT, int v, int e) {
+  for (int t = A.rp[v]; t < A.rp[v + 1]; t++)
+    if (edges_min_common(A, AT, A.col[t], e) != INT_MAX) return true;
+  return false;
+}
+
+// ---- pass 2: expansion ----------------------------------------------------
+struct ExpandArgs {
+  int pattern;
+  int nrows, ncols;
+  Csr l1, l2, l3;            // CSR used at each expansion level
+  int levels;
+  const int *quota;          // per row
+  const int64_t *cap_off;    // exclusive scan of quotas
+  int *out_cols;             // capacity buffer
+  int *out_cnt;              // chosen per row
+  const int *rows;           // rows to expand
+  int nlist;
+  unsigned *bitmap_g;        // per-WG bitmap slices (global mode)
+  int *list_g;               // per-WG distinct lists
+  int64_t list_cap;          // per-WG list capacity
+  int *row_ctr;              // dynamic queue over `rows`
+  uint64_t seed;
+  int lds_bitmap;            // 1 -> bitmap in dynamic LDS
+  int *overflow;             // set when a row has more than list_cap columns
+};
 
 struct SharedState {
   int cnt;
@@ -135,16 +257,11 @@ __device__ __forceinline__ void insert_col(int c, unsigned *bm, int *list,
   }
 }
 
-// Walk every endpoint of row r's expansion and insert it.
-__device__ void expand_row(const SampleArgs &A, int r, unsigned *bm, int *list,
+// Walk every endpoint of row r's 2- or 3-hop expansion and insert it.
+__device__ void expand_row(const ExpandArgs &A, int r, unsigned *bm, int *list,
                            SharedState &S) {
   const int tid = threadIdx.x;
   const int b1 = A.l1.rp[r], e1 = A.l1.rp[r + 1];
-  if (A.levels == 1) {
-    for (int t = b1 + tid; t < e1; t += kSB)
-      insert_col(A.l1.col[t], bm, list, A.list_cap, &S.cnt);
-    return;
-  }
   for (int c1 = b1; c1 < e1; c1 += kSB) {
     // level-1 chunk: ids and level-2 row sizes
     const int i1 = c1 + tid;
@@ -195,234 +312,48 @@ __device__ void expand_row(const SampleArgs &A, int r, unsigned *bm, int *list,
   }
 }
 
-__device__ void bitonic_sort_int(int *a, int n) {
-  int P = 1;
-  while (P < n) P <<= 1;
-  for (int t = n + threadIdx.x; t < P; t += kSB) a[t] = 0x7fffffff;
-  __syncthreads();
-  for (int size = 2; size <= P; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = threadIdx.x; t < P / 2; t += kSB) {
-        const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
-        const bool up = (lo & size) == 0;
-        const int x = a[lo], y = a[hi];
-        if ((x > y) == up) {
-          a[lo] = y;
-          a[hi] = x;
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
-// smallest element of sorted a[0..na) that is also in sorted b[0..nb)
-// (INT_MAX if none): walk the shorter list, binary-search the longer one
-__device__ int first_common(const int *a, int na, const int *b, int nb) {
-  if (na > nb) {
-    const int *t = a;
-    a = b;
-    b = t;
-    const int tn = na;
-    na = nb;
-    nb = tn;
-  }
-  int lo = 0;
-  for (int i = 0; i < na; i++) {
-    const int x = a[i];
-    int hi = nb;
-    while (lo < hi) {  // first b[j] >= x, from the previous position on
-      const int mid = (lo + hi) >> 1;
-      if (b[mid] < x) lo = mid + 1;
-      else hi = mid;
-    }
-    if (lo == nb) return INT_MAX;
-    if (b[lo] == x) return x;
-  }
-  return INT_MAX;
-}
-
-struct RejState {
-  unsigned long long key[kSB];
-  int flag[kSB];
-  int cand[kSB];
-  int wsum_ws[kSB / 64];
-  long long wtot;
-  int wmax;
-};
-
-// Karp-Luby union sampling of row r (see the header). Fills S.sel[0..q) and
-// sets their bitmap bits; returns false if the union looks smaller than q.
-__device__ bool reject_row(const SampleArgs &A, int r, int q, unsigned *bm,
-                           SharedState &S, RejState &J, long long W, int wmax) {
-  const int tid = threadIdx.x;
-  const int b1 = A.l1.rp[r], e1 = A.l1.rp[r + 1], n1 = e1 - b1;
-  const bool small = n1 <= kSB;
-  if (small) {  // exact path draws: prefix of |S_m| over row r in LDS
-    const int i1 = b1 + tid;
-    int id1 = -1, sz = 0;
-    if (tid < n1) {
-      id1 = A.l1.col[i1];
-      sz = A.l2.rp[id1 + 1] - A.l2.rp[id1];
-    }
-    int tot;
-    const int o1 = block_scan_excl(sz, &tot, S.ws);
-    S.a_id[tid] = id1;
-    S.a_off[tid] = o1;
-  }
-  if (tid == 0) S.nsel = 0;
-  __syncthreads();
-  int stall = 0;
-  for (int round = 0; round < 4096; round++) {
-    const uint64_t base = ((uint64_t)(uint32_t)r << 32) ^ ((uint64_t)round << 12);
-    const uint64_t h = hgx::rand64(A.seed, 0x300 + A.pattern, base + tid);
-    const uint64_t h2 = hgx::mix64(h ^ 0x51ed27ull);
-    int m = -1, c = -1;
-    if (small) {
-      const int w = (int)hgx::bounded(h, (uint32_t)W);
-      const int j = upper_find(S.a_off, n1, w);
-      m = S.a_id[j];
-      c = A.l2.col[A.l2.rp[m] + (w - S.a_off[j])];
-    } else {  // m uniform, accepted with |S_m| / max |S_m|
-      m = A.l1.col[b1 + (int)hgx::bounded(h, (uint32_t)n1)];
-      const int sz = A.l2.rp[m + 1] - A.l2.rp[m];
-      if ((uint32_t)(h2 >> 32) % (uint32_t)wmax < (uint32_t)sz)
-        c = A.l2.col[A.l2.rp[m] + (int)hgx::bounded(h2, (uint32_t)sz)];
-    }
-    int cand = INT_MAX;
-    if (c >= 0 && !(bm[c >> 5] & (1u << (c & 31)))) {
-      const int f = first_common(A.l1.col + b1, n1, A.l1.col + A.l1.rp[c],
-                                 A.l1.rp[c + 1] - A.l1.rp[c]);
-      if (f == m) cand = c;
-    }
-    // repeats inside the round: keep the lowest thread (sort (col, tid))
-    J.key[tid] = ((unsigned long long)(unsigned)cand << 32) | (unsigned)tid;
-    __syncthreads();
-    for (int size = 2; size <= kSB; size <<= 1) {
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        const int t = tid;
-        if (t < kSB / 2) {
-          const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
-          const bool up = (lo & size) == 0;
-          const unsigned long long x = J.key[lo], y = J.key[hi];
-          if ((x > y) == up) {
-            J.key[lo] = y;
-            J.key[hi] = x;
-          }
-        }
-        __syncthreads();
-      }
-    }
-    {
-      const unsigned long long k = J.key[tid];
-      const int col = (int)(k >> 32);
-      const bool fresh = col != INT_MAX &&
-                         (tid == 0 || (int)(J.key[tid - 1] >> 32) != col);
-      J.flag[(int)(k & 0xffffffffu)] = fresh ? 1 : 0;
-    }
-    __syncthreads();
-    int total;
-    const int rank = block_scan_excl(J.flag[tid], &total, S.ws);
-    const int need = q - S.nsel;
-    if (J.flag[tid] && rank < need) {
-      S.sel[S.nsel + rank] = cand;
-      atomicOr(&bm[cand >> 5], 1u << (cand & 31));
-    }
-    __syncthreads();
-    const int got = min(total, need);
-    if (tid == 0) S.nsel += got;
-    __syncthreads();
-    if (S.nsel >= q) return true;
-    stall = got ? 0 : stall + 1;
-    if (stall >= 32) break;
-  }
-  // give back the bits and let expansion handle the row
-  for (int i = tid; i < S.nsel; i += kSB) {
-    const int c = S.sel[i];
-    bm[c >> 5] = 0u;
-  }
-  __syncthreads();
-  return false;
-}
-
-__global__ __launch_bounds__(kSB) void sample_rows(SampleArgs A) {
+__global__ __launch_bounds__(kSB) void expand_rows(ExpandArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned s_dyn[];
   __shared__ SharedState S;
-  __shared__ RejState J;
-  __shared__ long long s_rw[kSB / 64];
-  __shared__ int s_rm[kSB / 64];
-  __shared__ int s_row;
+  __shared__ int s_idx;
   const int tid = threadIdx.x;
   const int nwords = (A.ncols + 31) >> 5;
-  unsigned *bm = A.lds_bitmap ? s_dyn : A.bitmap_g + (size_t)blockIdx.x * nwords;
-  int *list = A.list_g + (size_t)blockIdx.x * A.list_cap;
-  for (int w = tid; w < nwords; w += kSB) bm[w] = 0u;
+  unsigned *bm = nullptr;
+  int *list = nullptr;
+  if (A.levels > 1) {
+    bm = A.lds_bitmap ? s_dyn : A.bitmap_g + (size_t)blockIdx.x * nwords;
+    list = A.list_g + (size_t)blockIdx.x * A.list_cap;
+    for (int w = tid; w < nwords; w += kSB) bm[w] = 0u;
+  }
   __syncthreads();
   while (true) {
     if (tid == 0) {
-      s_row = atomicAdd(A.row_ctr, 1);
+      s_idx = atomicAdd(A.row_ctr, 1);
       S.cnt = 0;
       S.nsel = 0;
     }
     __syncthreads();
-    const int r = s_row;
-    if (r >= A.nrows) break;
-    const int q = A.quota ? A.quota[r] : A.quota_all;
+    if (s_idx >= A.nlist) break;
+    const int r = A.rows[s_idx];
+    const int q = A.quota[r];
     int *out = A.out_cols + A.cap_off[r];
     if (q <= 0) {
       if (tid == 0) A.out_cnt[r] = 0;
       __syncthreads();
       continue;
     }
-    if (A.levels == 2 && q <= kSelCap && A.reject_w > 0) {
-      // path count W and max |S_m| of the row (block reductions)
-      const int b1 = A.l1.rp[r], e1 = A.l1.rp[r + 1];
-      long long w = 0;
-      int wm = 0;
-      for (int t = b1 + tid; t < e1; t += kSB) {
-        const int id = A.l1.col[t];
-        const int sz = A.l2.rp[id + 1] - A.l2.rp[id];
-        w += sz;
-        wm = max(wm, sz);
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        w += __shfl_xor(w, off);
-        wm = max(wm, __shfl_xor(wm, off));
-      }
-      if ((tid & 63) == 0) {
-        s_rw[tid >> 6] = w;
-        s_rm[tid >> 6] = wm;
-      }
+    const int *lst;
+    int cnt;
+    if (A.levels == 1) {  // the CSR row is already a distinct list
+      lst = A.l1.col + A.l1.rp[r];
+      cnt = A.l1.rp[r + 1] - A.l1.rp[r];
+    } else {
+      expand_row(A, r, bm, list, S);
       __syncthreads();
-      long long W = 0;
-      int wmax = 0;
-#pragma unroll
-      for (int i = 0; i < kSB / 64; i++) {
-        W += s_rw[i];
-        wmax = max(wmax, s_rm[i]);
-      }
-      __syncthreads();
-      if (W > A.reject_w && W < (1ll << 31) && reject_row(A, r, q, bm, S, J, W, wmax)) {
-        if (tid == 0) atomicAdd(&A.stats[0], 1);
-        bitonic_sort_int(S.sel, q);
-        for (int i = tid; i < q; i += kSB) out[i] = S.sel[i];
-        if (tid == 0) A.out_cnt[r] = q;
-        for (int i = tid; i < q; i += kSB) {
-          const int c = S.sel[i];
-          bm[c >> 5] = 0u;
-        }
-        __syncthreads();
-        continue;
-      }
-      if (W > A.reject_w && tid == 0) atomicAdd(&A.stats[1], 1);
-      if (tid == 0) S.nsel = 0;
-      __syncthreads();
+      if (tid == 0 && S.cnt > A.list_cap) atomicOr(A.overflow, 1);
+      lst = list;
+      cnt = (int)min((int64_t)S.cnt, A.list_cap);
     }
-    expand_row(A, r, bm, list, S);
-    __syncthreads();
-    if (tid == 0 && S.cnt > A.list_cap) atomicOr(&A.stats[2], 1);
-    const int cnt = (int)min((int64_t)S.cnt, A.list_cap);
     const int m = min(q, cnt);
     if (m < cnt) {
       // m smallest composite keys: 8-pass radix select -> exact threshold
@@ -436,7 +367,7 @@ __global__ __launch_bounds__(kSB) void sample_rows(SampleArgs A) {
         const unsigned long long hm = p == 7 ? 0ull : ~((1ull << (8 * (p + 1))) - 1);
         const unsigned long long pre = S.prefix;
         for (int i = tid; i < cnt; i += kSB) {
-          const unsigned long long c = composite(A.seed, A.pattern, r, list[i]);
+          const unsigned long long c = composite(A.seed, A.pattern, r, lst[i]);
           if ((c & hm) == (pre & hm)) atomicAdd(&S.hist[(c >> (8 * p)) & 255], 1);
         }
         __syncthreads();
@@ -472,7 +403,7 @@ __global__ __launch_bounds__(kSB) void sample_rows(SampleArgs A) {
       }
       const unsigned long long T = S.prefix;
       for (int i = tid; i < cnt; i += kSB) {
-        const int c = list[i];
+        const int c = lst[i];
         if (composite(A.seed, A.pattern, r, c) <= T) {
           const int pos = atomicAdd(&S.nsel, 1);
           if (m <= kSelCap) S.sel[pos] = c;
@@ -481,23 +412,336 @@ __global__ __launch_bounds__(kSB) void sample_rows(SampleArgs A) {
       }
     } else {
       for (int i = tid; i < cnt; i += kSB) {
-        if (m <= kSelCap) S.sel[i] = list[i];
-        else out[i] = list[i];
+        if (m <= kSelCap) S.sel[i] = lst[i];
+        else out[i] = lst[i];
       }
     }
     __syncthreads();
     if (m <= kSelCap) {
       bitonic_sort_int(S.sel, m);
       for (int i = tid; i < m; i += kSB) out[i] = S.sel[i];
+    } else if (A.levels > 1 || m < cnt) {
+      // more than kSelCap chosen in arbitrary order: sort them in place
+      // (odd-even transposition over global memory; rare, big quotas only)
+      for (int ph = 0; ph < m; ph++) {
+        for (int i = 2 * tid + (ph & 1); i + 1 < m; i += 2 * kSB) {
+          const int x = out[i], y = out[i + 1];
+          if (x > y) {
+            out[i] = y;
+            out[i + 1] = x;
+          }
+        }
+        __syncthreads();
+      }
     }
     if (tid == 0) A.out_cnt[r] = m;
     // clear exactly the bits that were set
-    for (int i = tid; i < cnt; i += kSB) {
-      const int c = list[i];
-      bm[c >> 5] = 0u;
-    }
+    if (A.levels > 1)
+      for (int i = tid; i < cnt; i += kSB) {
+        const int c = list[i];
+        bm[c >> 5] = 0u;
+      }
     __syncthreads();
   }
+}
+
+// ---- pass 1: rejection sampling of large 2/3-hop rows --------------------
+struct RejectArgs {
+  int pattern;
+  int nrows, ncols;
+  Csr l1, l2, l3;
+  int levels;
+  Csr A, AT;                 // node -> edges, edge -> nodes
+  const int *quota;
+  const int64_t *cap_off;
+  int *out_cols, *out_cnt;
+  const int *rows;
+  int nlist;
+  int *row_ctr;
+  int *defer_small, *defer_big, *ndefer;  // ndefer[0] small, [1] big
+  uint64_t seed;
+  int64_t reject_w;
+  const int64_t *ps;         // 3-hop: exclusive scan over l2's incidences of
+                             // |l3 row of the incidence's column| (nnz + 1)
+  int mode3;                 // 0 auto, 1 paths, 2 uniform columns
+  int *stats;                // [0] rejection rows, [1] stalled, [3] uniform-mode rows
+};
+
+struct RejShared {
+  int sel[kSelCap];
+  int hash[kHash];
+  unsigned long long key[kSB];
+  int flag[kSB];
+  int a_id[kSB];
+  long long a_off[kSB];
+  long long wsl[kSB / 64];
+  long long wml[kSB / 64];
+  int ws[kSB / 64];
+  int nsel;
+  int idx;
+};
+
+__device__ __forceinline__ unsigned hslot(int c) {
+  return ((unsigned)c * 2654435761u) >> (32 - kHashBits);
+}
+__device__ bool hash_has(const int *h, int c) {
+  unsigned s = hslot(c);
+  while (true) {
+    const int k = h[s];
+    if (k == c) return true;
+    if (k < 0) return false;
+    s = (s + 1) & (kHash - 1);
+  }
+}
+__device__ void hash_put(int *h, int c) {
+  unsigned s = hslot(c);
+  while (true) {
+    const int old = atomicCAS(&h[s], -1, c);
+    if (old == -1 || old == c) return;
+    s = (s + 1) & (kHash - 1);
+  }
+}
+
+// path count of level-1 entity m of row r
+__device__ __forceinline__ long long level1_weight(const RejectArgs &A, int m) {
+  if (A.levels == 2) return A.l2.rp[m + 1] - A.l2.rp[m];
+  return A.ps[A.l2.rp[m + 1]] - A.ps[A.l2.rp[m]];
+}
+
+__device__ __forceinline__ uint64_t umulhi64(uint64_t h, uint64_t n) {
+  return __umul64hi(h, n);
+}
+
+// One candidate draw for row r (INT_MAX = rejected). mode: 0 2-hop paths,
+// 1 3-hop paths, 2 3-hop uniform columns.
+__device__ int draw_candidate(const RejectArgs &A, int r, int mode, bool small,
+                              int n1, long long W, long long wmax,
+                              const RejShared &S, uint64_t h) {
+  const int b1 = A.l1.rp[r];
+  const uint64_t h2 = hgx::mix64(h ^ 0x51ed27ull);
+  const uint64_t h3 = hgx::mix64(h2 ^ 0xa5a5a5a5ull);
+  if (mode == 2) {
+    const int c = (int)hgx::bounded(h, (uint32_t)A.ncols);
+    if (hash_has(S.hash, c)) return INT_MAX;
+    const bool in = A.pattern == PAT_NNE ? ne3_member(A.A, A.AT, r, c)
+                                         : ne3_member(A.A, A.AT, c, r);
+    return in ? c : INT_MAX;
+  }
+  // uniform path: level-1 entity m1 and the path offset w1 inside it
+  int m1;
+  long long w1;
+  if (small) {
+    const long long w = (long long)umulhi64(h, (uint64_t)W);
+    const int j = upper_find(S.a_off, n1, w);
+    m1 = S.a_id[j];
+    w1 = w - S.a_off[j];
+  } else {  // m1 uniform, accepted with weight / max weight
+    m1 = A.l1.col[b1 + (int)hgx::bounded(h, (uint32_t)n1)];
+    const long long wt = level1_weight(A, m1);
+    if ((long long)umulhi64(h2, (uint64_t)wmax) >= wt) return INT_MAX;
+    w1 = (long long)umulhi64(h3, (uint64_t)wt);
+  }
+  if (mode == 0) {
+    const int c = A.l2.col[A.l2.rp[m1] + (int)w1];
+    if (hash_has(S.hash, c)) return INT_MAX;
+    const int f = first_common(A.l1.col + b1, A.l1.rp[r + 1] - b1,
+                               A.l1.col + A.l1.rp[c], A.l1.rp[c + 1] - A.l1.rp[c]);
+    return f == m1 ? c : INT_MAX;
+  }
+  // 3-hop: m2 = the l2 incidence t of m1 whose prefix interval holds w1
+  const int tb = A.l2.rp[m1], te = A.l2.rp[m1 + 1];
+  const long long target = A.ps[tb] + w1;
+  int lo = tb, hi = te - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (A.ps[mid] <= target) lo = mid;
+    else hi = mid - 1;
+  }
+  const int m2 = A.l2.col[lo];
+  const int c = A.l3.col[A.l3.rp[m2] + (int)(target - A.ps[lo])];
+  if (hash_has(S.hash, c)) return INT_MAX;
+  // canonical (first) path to c, lexicographic in (m1, m2)
+  if (A.pattern == PAT_NNE) {
+    // r = v, m1 = e1 in E(v), m2 = u in e1, c = e: the first e1 of E(v)
+    // meeting e, then the smallest common member
+    for (int t = b1; t < A.l1.rp[r + 1]; t++) {
+      const int e1 = A.l1.col[t];
+      if (e1 > m1) break;
+      const int u = edges_min_common(A.A, A.AT, e1, c);
+      if (u != INT_MAX) return (e1 == m1 && u == m2) ? c : INT_MAX;
+    }
+    return INT_MAX;
+  }
+  // PAT_EEN: r = e, m1 = u in e, m2 = e2 in E(u), c = v: the first member u
+  // of e with E(u) ∩ E(v) non-empty, then its smallest common edge
+  const int *ev = A.A.col + A.A.rp[c];
+  const int nev = A.A.rp[c + 1] - A.A.rp[c];
+  for (int t = b1; t < A.l1.rp[r + 1]; t++) {
+    const int u = A.l1.col[t];
+    if (u > m1) break;
+    const int f = first_common(A.A.col + A.A.rp[u], A.A.rp[u + 1] - A.A.rp[u], ev, nev);
+    if (f != INT_MAX) return (u == m1 && f == m2) ? c : INT_MAX;
+  }
+  return INT_MAX;
+}
+
+__global__ __launch_bounds__(kSB) void reject_rows(RejectArgs A) {
+  __shared__ RejShared S;
+  const int tid = threadIdx.x;
+  while (true) {
+    if (tid == 0) S.idx = atomicAdd(A.row_ctr, 1);
+    __syncthreads();
+    const int i = S.idx;
+    if (i >= A.nlist) break;
+    const int r = A.rows[i];
+    const int q = A.quota[r];
+    if (q <= 0) {
+      if (tid == 0) A.out_cnt[r] = 0;
+      __syncthreads();
+      continue;
+    }
+    if (q > kSelCap) {
+      if (tid == 0) A.defer_big[atomicAdd(&A.ndefer[1], 1)] = r;
+      __syncthreads();
+      continue;
+    }
+    // path count W and max level-1 weight of the row
+    const int b1 = A.l1.rp[r], e1 = A.l1.rp[r + 1], n1 = e1 - b1;
+    long long w = 0, wm = 0;
+    for (int t = b1 + tid; t < e1; t += kSB) {
+      const long long x = level1_weight(A, A.l1.col[t]);
+      w += x;
+      wm = max(wm, x);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      w += __shfl_xor(w, off);
+      wm = max(wm, (long long)__shfl_xor(wm, off));
+    }
+    if ((tid & 63) == 0) {
+      S.wsl[tid >> 6] = w;
+      S.wml[tid >> 6] = wm;
+    }
+    __syncthreads();
+    long long W = 0, wmax = 0;
+#pragma unroll
+    for (int k = 0; k < kSB / 64; k++) {
+      W += S.wsl[k];
+      wmax = max(wmax, S.wml[k]);
+    }
+    __syncthreads();
+    if (W <= A.reject_w) {
+      if (tid == 0) A.defer_small[atomicAdd(&A.ndefer[0], 1)] = r;
+      __syncthreads();
+      continue;
+    }
+    int mode = 0;
+    if (A.levels == 3)
+      mode = (A.mode3 == 2 || (A.mode3 == 0 && W >= (long long)A.ncols)) ? 2 : 1;
+    const bool small = n1 <= kSB;
+    if (mode != 2 && small) {  // exact path draws: prefix of weights in LDS
+      long long x = 0;
+      int id1 = -1;
+      if (tid < n1) {
+        id1 = A.l1.col[b1 + tid];
+        x = level1_weight(A, id1);
+      }
+      long long tot;
+      const long long o1 = block_scan_excl64(x, &tot, S.wsl);
+      S.a_id[tid] = id1;
+      S.a_off[tid] = o1;
+    }
+    for (int k = tid; k < kHash; k += kSB) S.hash[k] = -1;
+    if (tid == 0) S.nsel = 0;
+    __syncthreads();
+    int stall = 0;
+    bool done = false;
+    for (int round = 0; round < 4096; round++) {
+      const uint64_t base = ((uint64_t)(uint32_t)r << 32) ^ ((uint64_t)round << 12);
+      const uint64_t h = hgx::rand64(A.seed, 0x300 + A.pattern, base + tid);
+      const int cand = draw_candidate(A, r, mode, small, n1, W, wmax, S, h);
+      // repeats inside the round: keep the lowest thread (sort (col, tid))
+      S.key[tid] = ((unsigned long long)(unsigned)cand << 32) | (unsigned)tid;
+      __syncthreads();
+      for (int size = 2; size <= kSB; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          if (tid < kSB / 2) {
+            const int lo = 2 * tid - (tid & (stride - 1)), hi = lo + stride;
+            const bool up = (lo & size) == 0;
+            const unsigned long long x = S.key[lo], y = S.key[hi];
+            if ((x > y) == up) {
+              S.key[lo] = y;
+              S.key[hi] = x;
+            }
+          }
+          __syncthreads();
+        }
+      }
+      {
+        const unsigned long long k = S.key[tid];
+        const int col = (int)(k >> 32);
+        const bool fresh = col != INT_MAX &&
+                           (tid == 0 || (int)(S.key[tid - 1] >> 32) != col);
+        S.flag[(int)(k & 0xffffffffu)] = fresh ? 1 : 0;
+      }
+      __syncthreads();
+      int total;
+      const int rank = block_scan_excl(S.flag[tid], &total, S.ws);
+      const int need = q - S.nsel;
+      if (S.flag[tid] && rank < need) {
+        S.sel[S.nsel + rank] = cand;
+        hash_put(S.hash, cand);
+      }
+      __syncthreads();
+      const int got = min(total, need);
+      if (tid == 0) S.nsel += got;
+      __syncthreads();
+      if (S.nsel >= q) {
+        done = true;
+        break;
+      }
+      stall = got ? 0 : stall + 1;
+      if (stall >= 32) break;
+    }
+    if (!done) {  // the union looks smaller than q: expand it (pass 2)
+      if (tid == 0) {
+        A.defer_big[atomicAdd(&A.ndefer[1], 1)] = r;
+        atomicAdd(&A.stats[1], 1);
+      }
+      __syncthreads();
+      continue;
+    }
+    if (tid == 0) {
+      atomicAdd(&A.stats[0], 1);
+      if (mode == 2) atomicAdd(&A.stats[3], 1);
+    }
+    bitonic_sort_int(S.sel, q);
+    int *out = A.out_cols + A.cap_off[r];
+    for (int k = tid; k < q; k += kSB) out[k] = S.sel[k];
+    if (tid == 0) A.out_cnt[r] = q;
+    __syncthreads();
+  }
+}
+
+// rows with a positive quota (order irrelevant: every draw is keyed by row)
+__global__ void list_rows(const int *q, int n, int *rows, int *cnt) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += gridDim.x * blockDim.x) {
+    if (q[i] > 0) rows[atomicAdd(cnt, 1)] = i;
+  }
+}
+
+// |row of l3| summed over l2's incidences: val[t] = |l3 row l2.col[t]|
+struct L3Len {
+  const int *col2, *rp3;
+  __host__ __device__ int64_t operator()(int t) const {
+    const int c = col2[t];
+    return (int64_t)(rp3[c + 1] - rp3[c]);
+  }
+};
+__global__ void ps_finish(int64_t *p, int64_t n, L3Len g) {
+  if (threadIdx.x == 0 && blockIdx.x == 0)
+    p[n] = n ? p[n - 1] + g((int)(n - 1)) : 0;
 }
 
 // ---- record materialisation ----------------------------------------------
@@ -552,24 +796,29 @@ __global__ void emit_negatives(int kind, int nrows, int ncols, const int *q,
 }
 
 // _sample_neighbors for node-edge records [b, e): nn_k from N(re-1),
-// ne_k from E(ln-1), K draws with replacement each.
+// ne_k from E(ln-1), K draws with replacement each. An endpoint with no
+// neighbours (possible for negatives of a graph with an isolated node or an
+// empty edge) is an error, as np.random.choice on an empty row raises
+// ValueError in the reference (hg2v_sample.py:49-51).
 __global__ void draw_neighbors(int64_t b, int64_t e, int K, int R, int *idx,
                                const int *rp_n, const int *col_n,
                                const int *rp_e, const int *col_e,
-                               uint64_t seed, uint64_t stream) {
+                               uint64_t seed, uint64_t stream, int *err) {
   for (int64_t rec = b + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; rec < e;
        rec += (int64_t)gridDim.x * blockDim.x) {
     int *ri = idx + rec * R;
     const int v = ri[0] - 1, ed = ri[3] - 1;
     const int nb = rp_e[ed], nl = rp_e[ed + 1] - nb;
     const int eb = rp_n[v], el = rp_n[v + 1] - eb;
+    if (nl == 0 || el == 0) {
+      atomicOr(err, 1);
+      continue;
+    }
     for (int k = 0; k < K; k++) {
       const uint64_t h = hgx::rand64(seed, stream, (uint64_t)rec * 64 + k);
       const uint64_t h2 = hgx::rand64(seed, stream + 1, (uint64_t)rec * 64 + k);
-      // an isolated endpoint (possible only for negatives) keeps padding 0;
-      // the reference raises there (np.random.choice on an empty row)
-      ri[4 + k] = nl ? col_e[nb + hgx::bounded(h, (uint32_t)nl)] + 1 : 0;
-      ri[4 + K + k] = el ? col_n[eb + hgx::bounded(h2, (uint32_t)el)] + 1 : 0;
+      ri[4 + k] = col_e[nb + hgx::bounded(h, (uint32_t)nl)] + 1;
+      ri[4 + K + k] = col_n[eb + hgx::bounded(h2, (uint32_t)el)] + 1;
     }
   }
 }
@@ -622,12 +871,54 @@ __global__ void fill_quota(int *q, int n, int v) {
     q[i] = i < n ? v : 0;
 }
 
+// pass 2 over `rows` (device list of n rows) with lists of list_cap columns
+int expand_pass(hgx_ctx *ctx, const ExpandArgs &base, const int *rows, int n,
+                int64_t list_cap) {
+  if (n == 0) return HGX_OK;
+  ExpandArgs a = base;
+  const int nwords = (a.ncols + 31) / 32;
+  const bool lds = a.levels > 1 && (size_t)nwords * 4 <= 48 * 1024;
+  int nwg = 1024;
+  if (a.levels > 1)
+    while (nwg > 64 && (double)nwg * (list_cap * 4 + (lds ? 0 : nwords * 4)) > 4e9)
+      nwg /= 2;
+  nwg = std::min(nwg, std::max(n, 1));
+  DevBuf list, bmap;
+  if (a.levels > 1) {
+    HGX_TRY(hgx_ensure(ctx, list, sizeof(int) * (size_t)nwg * list_cap + 16));
+    if (!lds) {
+      int rc = hgx_ensure(ctx, bmap, sizeof(unsigned) * (size_t)nwg * nwords);
+      if (rc != HGX_OK) {
+        hgx_release(list);
+        return rc;
+      }
+    }
+  }
+  a.rows = rows;
+  a.nlist = n;
+  a.list_g = list.as<int>();
+  a.bitmap_g = lds ? nullptr : bmap.as<unsigned>();
+  a.list_cap = list_cap;
+  a.lds_bitmap = lds;
+  int rc = HGX_OK;
+  hipMemsetAsync(a.row_ctr, 0, sizeof(int), ctx->stream);
+  hipLaunchKernelGGL(expand_rows, dim3(nwg), dim3(kSB), lds ? (size_t)nwords * 4 : 0,
+                     ctx->stream, a);
+  if (hipGetLastError() != hipSuccess)
+    rc = hgx_fail(ctx, HGX_EHIP, "expand_rows launch failed");
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess && rc == HGX_OK)
+    rc = hgx_fail(ctx, HGX_EHIP, "expand_rows failed");
+  hgx_release(list);
+  hgx_release(bmap);
+  return rc;
+}
+
 int run_pattern(hgx_ctx *ctx, int pattern, const int32_t *host_quota,
                 int quota_all, uint64_t seed, PatOut &po) {
   const int N = ctx->N, E = ctx->E;
   const Csr A{ctx->rp_n.as<int>(), ctx->col_n.as<int>()};
   const Csr AT{ctx->rp_e.as<int>(), ctx->col_e.as<int>()};
-  SampleArgs a{};
+  ExpandArgs a{};
   a.pattern = pattern;
   switch (pattern) {
     case PAT_A: a.nrows = N; a.ncols = E; a.l1 = A; a.levels = 1; break;
@@ -655,56 +946,112 @@ int run_pattern(hgx_ctx *ctx, int pattern, const int32_t *host_quota,
   HGX_TRY(hgx_ensure(ctx, po.cols, sizeof(int) * (cap_total + 1)));
   HGX_TRY(hgx_ensure(ctx, po.cnt, sizeof(int) * (R + 1)));
   HGX_HIP(ctx, hipMemsetAsync(po.cnt.p, 0, sizeof(int) * (R + 1), ctx->stream));
-  // workgroups and their scratch
-  const int nwords = (a.ncols + 31) / 32;
-  const bool lds = (size_t)nwords * 4 <= 48 * 1024;
-  int nwg = 1024;
-  {
-    // 2-hop rows with more expansion paths than this are union-sampled
-    // (HGX_SAMPLE_REJECT_W overrides; 0 disables)
-    const char *e = getenv("HGX_SAMPLE_REJECT_W");
-    a.reject_w = e ? atoll(e) : (int64_t)1 << 15;
-  }
-  // the distinct list only serves expanded rows: with union sampling on,
-  // 2-hop rows expand at most reject_w paths (a fallback row that does not
-  // fit is reported, never truncated)
-  const int64_t list_cap =
-      (a.levels == 2 && a.reject_w > 0)
-          ? std::min<int64_t>(a.ncols, std::max<int64_t>(2 * a.reject_w, 65536))
-          : a.ncols;
-  while (nwg > 64 && (double)nwg * (list_cap * 4 + (lds ? 0 : nwords * 4)) > 4e9)
-    nwg /= 2;
-  HGX_TRY(hgx_ensure(ctx, ctx->s3, sizeof(int) * (size_t)nwg * list_cap + 16));
-  if (!lds) HGX_TRY(hgx_ensure(ctx, ctx->s4, sizeof(unsigned) * (size_t)nwg * nwords));
-  HGX_TRY(hgx_ensure(ctx, ctx->s0, 16));
-  HGX_HIP(ctx, hipMemsetAsync(ctx->s0.p, 0, 16, ctx->stream));
+  // counters: [0] row queue, [1] listed rows, [2] deferred small, [3]
+  // deferred big, [4] overflow, [5..8] rejection stats
+  HGX_TRY(hgx_ensure(ctx, ctx->s0, 64));
+  int *ctr = ctx->s0.as<int>();
+  HGX_HIP(ctx, hipMemsetAsync(ctr, 0, 64, ctx->stream));
+  // rows with a quota; two deferral lists
+  DevBuf rows, dsmall, dbig;
+  HGX_TRY(hgx_ensure(ctx, rows, sizeof(int) * (R + 1)));
+  hipLaunchKernelGGL(list_rows, dim3(grid_for(R, 256)), dim3(256), 0,
+                     ctx->stream, po.q.as<int>(), R, rows.as<int>(), ctr + 1);
+  HGX_LAUNCH_CHECK(ctx);
+  int nlist = 0;
+  HGX_HIP(ctx, hipMemcpyAsync(&nlist, ctr + 1, sizeof(int), hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   a.quota = po.q.as<int>();
-  a.quota_all = quota_all;
   a.cap_off = po.cap_off.as<int64_t>();
   a.out_cols = po.cols.as<int>();
   a.out_cnt = po.cnt.as<int>();
-  a.bitmap_g = lds ? nullptr : ctx->s4.as<unsigned>();
-  a.list_g = ctx->s3.as<int>();
-  a.list_cap = list_cap;
-  a.row_ctr = ctx->s0.as<int>();
+  a.row_ctr = ctr;
   a.seed = seed;
-  a.lds_bitmap = lds;
-  a.stats = ctx->s0.as<int>() + 1;  // [0] union-sampled rows, [1] fallbacks, [2] overflow
-  hipLaunchKernelGGL(sample_rows, dim3(nwg), dim3(kSB),
-                     lds ? (size_t)nwords * 4 : 0, ctx->stream, a);
-  HGX_LAUNCH_CHECK(ctx);
-  {
-    int st[3] = {0, 0, 0};
-    HGX_HIP(ctx, hipMemcpyAsync(st, a.stats, sizeof(st), hipMemcpyDeviceToHost,
+  a.overflow = ctr + 4;
+  const int64_t reject_w = ctx->tune.sample_reject_w;
+  const bool reject = a.levels > 1 && reject_w > 0;
+  int st[4] = {0, 0, 0, 0};
+  if (!reject) {
+    HGX_TRY(expand_pass(ctx, a, rows.as<int>(), nlist,
+                        a.levels == 1 ? 0 : (int64_t)a.ncols));
+  } else {
+    HGX_TRY(hgx_ensure(ctx, dsmall, sizeof(int) * (nlist + 1)));
+    HGX_TRY(hgx_ensure(ctx, dbig, sizeof(int) * (nlist + 1)));
+    DevBuf ps;
+    if (a.levels == 3) {  // path counts through l2's incidences
+      const int64_t nnz = ctx->nnz;
+      HGX_TRY(hgx_ensure(ctx, ps, sizeof(int64_t) * (nnz + 1)));
+      L3Len f{a.l2.col, a.l3.rp};
+      hipcub::CountingInputIterator<int> ci(0);
+      hipcub::TransformInputIterator<int64_t, L3Len, hipcub::CountingInputIterator<int>>
+          it(ci, f);
+      size_t tmp = 0;
+      // the value at t == nnz is never used: scan nnz values, then the total
+      hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, ps.as<int64_t>(), nnz,
+                                       ctx->stream);
+      HGX_TRY(hgx_ensure(ctx, ctx->s7, tmp + 256));
+      HGX_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(ctx->s7.p, tmp, it,
+                                                    ps.as<int64_t>(), nnz,
+                                                    ctx->stream));
+      // ps[nnz] = ps[nnz-1] + val[nnz-1]
+      hipLaunchKernelGGL(ps_finish, dim3(1), dim3(64), 0, ctx->stream,
+                         ps.as<int64_t>(), nnz, f);
+      HGX_LAUNCH_CHECK(ctx);
+    }
+    RejectArgs r{};
+    r.pattern = pattern;
+    r.nrows = a.nrows;
+    r.ncols = a.ncols;
+    r.l1 = a.l1;
+    r.l2 = a.l2;
+    r.l3 = a.l3;
+    r.levels = a.levels;
+    r.A = A;
+    r.AT = AT;
+    r.quota = a.quota;
+    r.cap_off = a.cap_off;
+    r.out_cols = a.out_cols;
+    r.out_cnt = a.out_cnt;
+    r.rows = rows.as<int>();
+    r.nlist = nlist;
+    r.row_ctr = ctr;
+    r.defer_small = dsmall.as<int>();
+    r.defer_big = dbig.as<int>();
+    r.ndefer = ctr + 2;
+    r.seed = seed;
+    r.reject_w = reject_w;
+    r.ps = ps.as<int64_t>();
+    r.mode3 = ctx->tune.sample_mode3;
+    r.stats = ctr + 5;
+    if (nlist > 0) {
+      int dev = 0, ncu = 256;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      const int nwg = std::min(nlist, 4 * ncu);
+      hipLaunchKernelGGL(reject_rows, dim3(nwg), dim3(kSB), 0, ctx->stream, r);
+      HGX_LAUNCH_CHECK(ctx);
+    }
+    int nd[2] = {0, 0};
+    HGX_HIP(ctx, hipMemcpyAsync(nd, ctr + 2, sizeof(nd), hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HGX_HIP(ctx, hipMemcpyAsync(st, ctr + 5, sizeof(st), hipMemcpyDeviceToHost,
                                 ctx->stream));
     HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    ctx->sample_union_rows += st[0];
-    ctx->sample_fallback_rows += st[1];
-    HGX_CHECK(ctx, st[2] == 0, HGX_EUNSUP,
-              "a sampled row has more than %lld distinct columns "
-              "(raise HGX_SAMPLE_REJECT_W or disable union sampling)",
-              (long long)list_cap);
+    hgx_release(ps);
+    // deferred rows: small ones have at most reject_w distinct columns
+    HGX_TRY(expand_pass(ctx, a, dsmall.as<int>(), nd[0],
+                        std::min<int64_t>(a.ncols, std::max<int64_t>(2 * reject_w, 65536))));
+    HGX_TRY(expand_pass(ctx, a, dbig.as<int>(), nd[1], (int64_t)a.ncols));
   }
+  int ovf = 0;
+  HGX_HIP(ctx, hipMemcpyAsync(&ovf, ctr + 4, sizeof(int), hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->sample_union_rows += st[0];
+  ctx->sample_fallback_rows += st[1];
+  ctx->sample_uniform_rows += st[3];
+  HGX_CHECK(ctx, ovf == 0, HGX_EUNSUP,
+            "a sampled row has more distinct columns than its expansion list");
   HGX_TRY(hgx_ensure(ctx, po.rec_off, sizeof(int64_t) * (R + 1)));
   HGX_TRY(excl_scan_i32_to_i64(ctx, po.cnt.as<int>(), po.rec_off.as<int64_t>(),
                                R, &po.total));
@@ -736,12 +1083,22 @@ int emit(hgx_ctx *ctx, int kind, const PatOut &po, int64_t base, float prob) {
 int neighbors(hgx_ctx *ctx, int64_t b, int64_t e, uint64_t seed,
               uint64_t stream) {
   if (e <= b) return HGX_OK;
+  HGX_TRY(hgx_ensure(ctx, ctx->s1, 16));
+  HGX_HIP(ctx, hipMemsetAsync(ctx->s1.p, 0, sizeof(int), ctx->stream));
   hipLaunchKernelGGL(draw_neighbors, dim3(grid_for(e - b, 256)), dim3(256), 0,
                      ctx->stream, b, e, ctx->K, 4 + 2 * ctx->K,
                      ctx->rec_idx.as<int>(), ctx->rp_n.as<int>(),
                      ctx->col_n.as<int>(), ctx->rp_e.as<int>(),
-                     ctx->col_e.as<int>(), seed, stream);
+                     ctx->col_e.as<int>(), seed, stream, ctx->s1.as<int>());
   HGX_LAUNCH_CHECK(ctx);
+  int err = 0;
+  HGX_HIP(ctx, hipMemcpyAsync(&err, ctx->s1.p, sizeof(int), hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  HGX_CHECK(ctx, err == 0, HGX_EVALUE,
+            "a cannot be empty unless no samples are taken (_sample_neighbors "
+            "on a node without edges or an edge without nodes, "
+            "hg2v_sample.py:49-51)");
   return HGX_OK;
 }
 
@@ -785,9 +1142,15 @@ int check_quota(hgx_ctx *ctx, const int32_t *q, int n, const char *what) {
   return HGX_OK;
 }
 
+void reset_stats(hgx_ctx *ctx) {
+  ctx->sample_union_rows = ctx->sample_fallback_rows = 0;
+  ctx->sample_uniform_rows = 0;
+}
+
 }  // namespace
 
 // HOBE probability kernels live in hgx_hobe.hip
+int hgx_hobe_prepare(hgx_ctx *ctx);
 int hgx_hobe_fill_probs(hgx_ctx *ctx, int kind, int64_t b, int64_t e);
 
 extern "C" int hgx_sample_fobe(hgx_ctx *ctx, uint64_t seed, int K,
@@ -804,7 +1167,7 @@ extern "C" int hgx_sample_fobe(hgx_ctx *ctx, uint64_t seed, int K,
   HGX_TRY(check_quota(ctx, node_quota, ctx->N, "node"));
   HGX_TRY(check_quota(ctx, edge_quota, ctx->E, "edge"));
   HGX_HIP(ctx, hipSetDevice(ctx->device));
-  ctx->sample_union_rows = ctx->sample_fallback_rows = 0;
+  reset_stats(ctx);
   // BooleanSamples order (hg2v_sample.py:156-194): nn, ee, ne(node rows),
   // ne(edge rows, swapped); then negatives (:198-240).
   PatOut nn, ee, ne_n, ne_e;
@@ -847,22 +1210,30 @@ extern "C" int hgx_sample_fobe(hgx_ctx *ctx, uint64_t seed, int K,
   return HGX_OK;
 }
 
-extern "C" int hgx_sample_hobe(hgx_ctx *ctx, uint64_t seed, int K, int S,
-                               int64_t *n_records) {
+extern "C" int hgx_sample_hobe_rows(hgx_ctx *ctx, uint64_t seed, int K,
+                                    const int32_t *node_quota,
+                                    const int32_t *edge_quota, int S,
+                                    int64_t *n_records) {
   if (!ctx) return HGX_EINVAL;
   HGX_CHECK(ctx, ctx->N > 0, HGX_ESTATE, "no incidence uploaded");
   HGX_CHECK(ctx, ctx->k > 0, HGX_ESTATE,
             "HOBE needs the algebraic-distance coords on device");
   HGX_CHECK(ctx, K >= 1 && K <= 16, HGX_EUNSUP, "num_neighbors %d outside [1,16]", K);
   HGX_CHECK(ctx, S >= 0, HGX_EINVAL, "num_samples must be >= 0 (hg2v_sample.py:647)");
+  HGX_CHECK(ctx, (node_quota == nullptr) == (edge_quota == nullptr), HGX_EINVAL,
+            "give both row quotas or neither");
+  if (node_quota) {
+    HGX_TRY(check_quota(ctx, node_quota, ctx->N, "node"));
+    HGX_TRY(check_quota(ctx, edge_quota, ctx->E, "edge"));
+  }
   HGX_HIP(ctx, hipSetDevice(ctx->device));
-  ctx->sample_union_rows = ctx->sample_fallback_rows = 0;
+  reset_stats(ctx);
   // AlgebraicDistanceSamples order (hg2v_sample.py:658-715)
   PatOut nn, ee, ne_n, ne_e;
-  HGX_TRY(run_pattern(ctx, PAT_NN, nullptr, S, seed, nn));
-  HGX_TRY(run_pattern(ctx, PAT_EE, nullptr, S, seed, ee));
-  HGX_TRY(run_pattern(ctx, PAT_NNE, nullptr, S, seed, ne_n));
-  HGX_TRY(run_pattern(ctx, PAT_EEN, nullptr, S, seed, ne_e));
+  HGX_TRY(run_pattern(ctx, PAT_NN, node_quota, S, seed, nn));
+  HGX_TRY(run_pattern(ctx, PAT_EE, edge_quota, S, seed, ee));
+  HGX_TRY(run_pattern(ctx, PAT_NNE, node_quota, S, seed, ne_n));
+  HGX_TRY(run_pattern(ctx, PAT_EEN, edge_quota, S, seed, ne_e));
   const int64_t o_ee = nn.total, o_ne = o_ee + ee.total;
   const int64_t o_en = o_ne + ne_n.total, total = o_en + ne_e.total;
   HGX_TRY(alloc_records(ctx, total, K));
@@ -871,12 +1242,18 @@ extern "C" int hgx_sample_hobe(hgx_ctx *ctx, uint64_t seed, int K, int S,
   HGX_TRY(emit(ctx, REC_NE_NODE, ne_n, o_ne, 0.f));
   HGX_TRY(emit(ctx, REC_NE_EDGE, ne_e, o_en, 0.f));
   HGX_TRY(neighbors(ctx, o_ne, total, seed, 0x500));
+  HGX_TRY(hgx_hobe_prepare(ctx));
   HGX_TRY(hgx_hobe_fill_probs(ctx, 0, 0, o_ee));
   HGX_TRY(hgx_hobe_fill_probs(ctx, 1, o_ee, o_ne));
   HGX_TRY(hgx_hobe_fill_probs(ctx, 2, o_ne, total));
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (n_records) *n_records = total;
   return HGX_OK;
+}
+
+extern "C" int hgx_sample_hobe(hgx_ctx *ctx, uint64_t seed, int K, int S,
+                               int64_t *n_records) {
+  return hgx_sample_hobe_rows(ctx, seed, K, nullptr, nullptr, S, n_records);
 }
 
 // WeightedJaccardSamples pair blocks (hg2v_sample.py:436-505): nn (node
@@ -888,7 +1265,7 @@ int hgx_sample_pairs4(hgx_ctx *ctx, uint64_t seed, int K, const int32_t *node_q,
                       int64_t *o_ne_out, int64_t *total_out) {
   HGX_TRY(check_quota(ctx, node_q, ctx->N, "node"));
   HGX_TRY(check_quota(ctx, edge_q, ctx->E, "edge"));
-  ctx->sample_union_rows = ctx->sample_fallback_rows = 0;
+  reset_stats(ctx);
   PatOut nn, ee, ne_n, ne_e;
   HGX_TRY(run_pattern(ctx, PAT_NN, node_q, 0, seed, nn));
   HGX_TRY(run_pattern(ctx, PAT_EE, edge_q, 0, seed, ee));
@@ -913,5 +1290,11 @@ extern "C" int hgx_sample_last_stats(hgx_ctx *ctx, int64_t *union_rows,
   if (!ctx) return HGX_EINVAL;
   if (union_rows) *union_rows = ctx->sample_union_rows;
   if (fallback_rows) *fallback_rows = ctx->sample_fallback_rows;
+  return HGX_OK;
+}
+
+extern "C" int hgx_sample_uniform_rows(hgx_ctx *ctx, int64_t *rows) {
+  if (!ctx) return HGX_EINVAL;
+  if (rows) *rows = ctx->sample_uniform_rows;
   return HGX_OK;
 }

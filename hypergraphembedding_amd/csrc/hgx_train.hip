@@ -48,7 +48,11 @@ constexpr int kGraphBatches = 64;  // batches per chunk buffer and per graph
 // results are wrong when set): 1 empty K1, 2 empty K2, 4 K1 gathers hit
 // row 0, 8 K1 skips gradient stores, 16 K2 skips slot sums, 32 K2 skips
 // the table read-modify-write.
-__constant__ int g_tab = 0;
+#ifdef HGX_DEBUG_KNOBS
+__constant__ int g_tab = 0;  // ablation bits (diagnostic builds only)
+#else
+static constexpr int g_tab = 0;
+#endif
 
 // diagnostic phase trace (HGX_TRAIN_TRACE=<file>, timing experiments only):
 // wave 0 of every workgroup stamps s_memrealtime (100 MHz) at phase ends
@@ -1324,10 +1328,7 @@ void geometry(int d, int &L, int &VPL) {
 
 using KFn = void (*)(TrainArgs, int);
 
-int env_int(const char *name, int dflt) {
-  const char *v = getenv(name);
-  return v && v[0] ? atoi(v) : dflt;
-}
+int env_int(const char *name, int dflt) { return hgx_debug_env(name, dflt); }
 
 template <int L, int VPL, int TB>
 KFn fwd_spec(int K, int loss, int act) {
@@ -1589,11 +1590,13 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   KFn k1 = nullptr, k2 = nullptr;
   HGX_CHECK(ctx, pick_kernels(L, VPL, K, loss, act, tb1, tb2, k1, k2), HGX_EUNSUP,
             "no kernel for d=%d", ctx->d);
+#ifdef HGX_DEBUG_KNOBS
   {
     const int ab = env_int("HGX_TRAIN_ABLATE", 0);
     HGX_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_tab), &ab, sizeof(int)));
   }
-  const char *trace_path = getenv("HGX_TRAIN_TRACE");
+#endif
+  const char *trace_path = hgx_debug_env_str("HGX_TRAIN_TRACE");
   const int trace_nb = 256;
   struct TraceBuf {
     void *p = nullptr;
@@ -1625,11 +1628,12 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   KFusedFn kf = nullptr;
   KFlushFn kfl = nullptr;
   int tbf = 0;
-  // HGX_TRAIN_FUSED: 0 off, 1 only d in (64, 128] (L = 32), 2 (default)
+  // train_fused tuning 0: off; else HGX_TRAIN_FUSED (debug builds): 0 off,
+  // 1 only d in (64, 128] (L = 32), 2 (default)
   // also d in (128, 256] (L = 64; r01: 12.7 vs 12.7 us/batch with the wide
   // workgroup cap, 11.3 vs 12.7 with the 40-workgroup cap and the list-gather
   // skip)
-  const int fz = env_int("HGX_TRAIN_FUSED", 2);
+  const int fz = ctx->tune.train_fused ? env_int("HGX_TRAIN_FUSED", 2) : 0;
   // workgroups per fused batch: the records' lane groups plus headroom for
   // packing holes (components placed whole, first fit): +8 when that stays
   // within 40 (the NBFM = 40 instantiation, fewer padding-row partial loads

@@ -31,6 +31,8 @@ extern "C" {
 #define HGX_EZERODIV -4  /* isolated node/edge in algebraic distance        */
 #define HGX_ESTATE -5    /* call out of order (e.g. no incidence uploaded)  */
 #define HGX_EUNSUP -6    /* shape outside what this build supports          */
+#define HGX_EVALUE -7    /* ValueError in the reference (np.random.choice on
+                            an empty row, hg2v_sample.py:49-51)             */
 
 #define HGX_LOSS_KLD 0   /* BooleanModel: kullback_leibler_divergence       */
 #define HGX_LOSS_MSE 1   /* UnweightedFloatModel: mean_squared_error        */
@@ -48,6 +50,18 @@ int hgx_version(void);
  * the context's own stream. */
 int hgx_set_stream(hgx_ctx *ctx, void *hip_stream);
 int hgx_synchronize(hgx_ctx *ctx);
+/* Implementation choices of this context (none changes a result's math or
+ * distribution; not a reference interface). key:
+ *   "sample_reject_w"  2/3-hop sample rows with more expansion paths are
+ *                      sampled by rejection (default 32768; 0 = expand all)
+ *   "sample_mode3"     3-hop rejection proposal: 0 auto, 1 paths
+ *                      (Karp-Luby), 2 uniform columns
+ *   "train_fused"      1 fused one-launch batch step (default), 0 the
+ *                      two-kernel step for every batch
+ *   "alg_long"         alg-dist long-row threshold (0 = 512, else >= 64)
+ *   "alg_ks"           alg-dist coordinate row width in floats (0 = auto)
+ * Unknown keys and out-of-range values -> HGX_EINVAL. */
+int hgx_set_tuning(hgx_ctx *ctx, const char *key, int64_t value);
 
 /* ---- incidence --------------------------------------------------------- *
  * Replaces ToCsrMatrix / ToEdgeCsrMatrix(CompressRange(hg))
@@ -129,6 +143,12 @@ int hgx_sample_fobe(hgx_ctx *ctx, uint64_t seed, int K,
  * coords: quota S for every row, nn/ee/ne probabilities as above. */
 int hgx_sample_hobe(hgx_ctx *ctx, uint64_t seed, int K, int S,
                     int64_t *n_records);
+/* The same on a subset of rows: quota per node row / edge row instead of S
+ * (both NULL -> S everywhere, i.e. hgx_sample_hobe). Used to sample the
+ * rows one rank owns and for bounded slices of large graphs. */
+int hgx_sample_hobe_rows(hgx_ctx *ctx, uint64_t seed, int K,
+                         const int32_t *node_quota, const int32_t *edge_quota,
+                         int S, int64_t *n_records);
 /* ---- weighted-Jaccard samples (HG2V_ADJ_JAC / HG2V_NEIGH_JAC) --------- *
  * Replaces WeightedJaccardSamples (hg2v_sample.py:395-510) with
  * SparseWeightedJaccard (:250-273) and GetAllCentroids (:276-326).
@@ -149,10 +169,13 @@ int hgx_jaccard_probs(hgx_ctx *ctx, int kind, int64_t n, const int32_t *a,
 int hgx_jaccard_centroids(hgx_ctx *ctx, int which, int64_t *nnz,
                           int64_t *rowptr, int32_t *col, float *val);
 /* Of the last hgx_sample_* call: 2-hop rows sampled from the union by
- * rejection (rows whose expansion exceeds HGX_SAMPLE_REJECT_W paths,
+ * rejection (rows whose expansion exceeds the sample_reject_w tuning,
  * default 32768) and rows that fell back to expansion. */
 int hgx_sample_last_stats(hgx_ctx *ctx, int64_t *union_rows,
                           int64_t *fallback_rows);
+/* Of the last hgx_sample_* call: 3-hop rows sampled by uniform-column
+ * rejection (a subset of union_rows). */
+int hgx_sample_uniform_rows(hgx_ctx *ctx, int64_t *rows);
 int hgx_records_set(hgx_ctx *ctx, int64_t n, int K, const int32_t *idx,
                     const float *tgt);
 int hgx_records_info(hgx_ctx *ctx, int64_t *n, int *K);

@@ -184,11 +184,14 @@ def test_fused_step_mixed_runs_vs_oracle_and_split(ctx, d, loss, act,
                                max_epochs=1, perms=perms)
   ctx.records_set(idx, tgt)
   res = {}
-  for mode in ("2", "0"):
-    monkeypatch.setenv("HGX_TRAIN_FUSED", mode)
-    ctx.model_init(d, nrows, erows, node_tab=nt, edge_tab=et)
-    gl = ctx.train(batch=B, max_epochs=1, loss=loss, act=act, perms=perms)
-    res[mode] = ctx.model_get() + (gl, ctx.train_path_stats())
+  try:
+    for mode in ("2", "0"):
+      ctx.set_tuning("train_fused", 1 if mode == "2" else 0)
+      ctx.model_init(d, nrows, erows, node_tab=nt, edge_tab=et)
+      gl = ctx.train(batch=B, max_epochs=1, loss=loss, act=act, perms=perms)
+      res[mode] = ctx.model_get() + (gl, ctx.train_path_stats())
+  finally:
+    ctx.set_tuning("train_fused", 1)
   fused, split = res["2"][3], res["0"][3]
   assert fused == (nb - 3, 3), fused
   assert split == (0, nb), split
