@@ -49,13 +49,18 @@ def EmbedAlgebraicDistance(hypergraph, dimension, iterations=20,
 
 
 def coords_to_embedding(inc, x, y, dimension, method_name):
+  """HypergraphEmbedding keyed by the original ids (KerasModelToEmbedding,
+  hg2v_model.py:31-48 / algebraic_distance.py:166-174): serialized by the
+  native writer and parsed once, instead of filling the maps field by field
+  in Python (same message; map entries in ascending id order)."""
+  from . import _hgx
+  x = np.ascontiguousarray(x, np.float32).reshape(inc.N, dimension)
+  y = np.ascontiguousarray(y, np.float32).reshape(inc.E, dimension)
   emb = HypergraphEmbedding()
+  emb.ParseFromString(_hgx.write_embedding_bytes(inc.node_ids, x, inc.edge_ids,
+                                                 y, method_name).tobytes())
   emb.dim = dimension
   emb.method_name = method_name
-  for i, orig in enumerate(inc.node_ids.tolist()):
-    emb.node[orig].values.extend(x[i].tolist())
-  for i, orig in enumerate(inc.edge_ids.tolist()):
-    emb.edge[orig].values.extend(y[i].tolist())
   return emb
 
 

@@ -109,10 +109,15 @@ def _plot_distributions(path, records):
 def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
                              loss, act, fit_batch_size, fit_epochs,
                              debug_summary_path, disable_pbar, ctx=None):
-  """embedding.py:269-305, device-resident end to end."""
+  """embedding.py:269-305, device-resident end to end. `hypergraph` is the
+  reference's Hypergraph message or an already compressed Incidence (e.g.
+  proto_native.read_incidence of a file too large for Python protobuf)."""
   del disable_pbar
   ctx = ctx or get_context()
-  inc = Incidence.from_hypergraph(hypergraph)  # CompressRange + CSR
+  if isinstance(hypergraph, Incidence):
+    inc = hypergraph
+  else:
+    inc = Incidence.from_hypergraph(hypergraph)  # CompressRange + CSR
   records = sampler_fn(inc, ctx)
   if debug_summary_path is not None:
     _plot_distributions(debug_summary_path, records)

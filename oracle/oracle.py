@@ -272,9 +272,10 @@ _mt = None
 
 
 def train_mt(idx, tgt, K, node_tab, edge_tab, loss, act, batch=256, lr=0.01,
-             eps=1e-7, epochs=1, threads=0):
+             eps=1e-7, epochs=1, threads=0, copy=True):
   """Multi-threaded CPU baseline trainer (cpu_train_mt.c; records in the
-  given order). Updates copies of the tables; returns (nt, et, mean loss)."""
+  given order). Updates copies of the tables (copy=False: the given float32
+  tables in place); returns (nt, et, mean loss)."""
   global _mt
   if _mt is None:
     build()
@@ -289,8 +290,10 @@ def train_mt(idx, tgt, K, node_tab, edge_tab, loss, act, batch=256, lr=0.01,
                                  ctypes.POINTER(ctypes.c_double)]
   idx = np.ascontiguousarray(idx, np.int32)
   tgt = np.ascontiguousarray(tgt, np.float32)
-  nt = np.ascontiguousarray(node_tab, np.float32).copy()
-  et = np.ascontiguousarray(edge_tab, np.float32).copy()
+  nt = np.ascontiguousarray(node_tab, np.float32)
+  et = np.ascontiguousarray(edge_tab, np.float32)
+  if copy:
+    nt, et = nt.copy(), et.copy()
   na, ea = np.zeros_like(nt), np.zeros_like(et)
   lo = ctypes.c_double()
   _mt.cpu_train_mt(idx.shape[0], K, idx, tgt, nt.shape[1], nt.shape[0],

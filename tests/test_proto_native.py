@@ -100,7 +100,15 @@ def test_write_embedding_matches_protobuf(tmp_path):
   d = 5
   x = rnd.standard_normal((inc.N, d)).astype(np.float32)
   y = rnd.standard_normal((inc.E, d)).astype(np.float32)
-  want = coords_to_embedding(inc, x, y, d, "HG2V_ALG_DIST")
+  # the message filled field by field through Python protobuf
+  want = HypergraphEmbedding()
+  want.dim = d
+  want.method_name = "HG2V_ALG_DIST"
+  for i, orig in enumerate(inc.node_ids.tolist()):
+    want.node[orig].values.extend(x[i].tolist())
+  for i, orig in enumerate(inc.edge_ids.tolist()):
+    want.edge[orig].values.extend(y[i].tolist())
+  assert coords_to_embedding(inc, x, y, d, "HG2V_ALG_DIST") == want
   got = HypergraphEmbedding()
   got.ParseFromString(embedding_bytes(inc, x, y, "HG2V_ALG_DIST").tobytes())
   assert got == want

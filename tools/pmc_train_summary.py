@@ -1,8 +1,8 @@
-"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
-tools/perf_train.py into profiles/<round>_pmc_train.json: HBM bytes per
-batch step (train_fwd_bwd + train_update), gfx950 FETCH correction x2
-(MI355X_MICROARCH.md, HBM section). Usage:
-  python tools/pmc_train_summary.py FETCH_CSV WRITE_CSV OUT_JSON d"""
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (of bench.py, or
+tools/perf_train.py) into profiles/<round>_pmc_train.json: HBM bytes per
+batch step (train_fused, or train_fwd_bwd + train_update), gfx950 FETCH
+correction x2 (MI355X_MICROARCH.md, HBM section). Usage:
+  python tools/pmc_train_summary.py FETCH_CSV WRITE_CSV OUT_JSON d ROUND [CMD]"""
 import csv, json, sys
 import numpy as np
 
@@ -34,16 +34,15 @@ alg = 256 * (224 * d + 68)
 res = {
     "round": int(sys.argv[5]) if len(sys.argv) > 5 else 1,
     "command": ("rocprofv3 --pmc FETCH_SIZE (pass 1) / "
-                "--pmc WRITE_SIZE (pass 2) --output-format csv -- python "
-                f"tools/perf_train.py {d} 400000"),
+                "--pmc WRITE_SIZE (pass 2) --output-format csv -- python3 "
+                + (sys.argv[6] if len(sys.argv) > 6 else
+                   "bench.py --steps 1 --warmup 0 --no-cpu --no-c4 --no-extra")),
     "note": ("Per batch of 256 records at d=%d on 100k/50k-row tables, summed over "
              "the per-batch kernels (train_fused, or train_fwd_bwd + train_update, and the "
              "row-0 flush once per run), per batch step. FETCH_SIZE / "
              "WRITE_SIZE are KB; gfx950 correction: FETCH doubled (wide 16-B-per-"
              "lane reads are tallied at half), WRITE as is. Infinity-Cache hits "
-             "are counted by these counters. Collected on the trainer-only script "
-             "(same kernels and shapes as bench.py; --pmc on the full bench.py "
-             "crashed inside the profiler in round 1)." % d),
+             "are counted by these counters." % d),
     "launches": {"fetch": nf, "write": nw},
     "fetch_kb_per_batch": f,
     "write_kb_per_batch": w,
