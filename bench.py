@@ -136,9 +136,10 @@ def main():
   bytes_iter = 8.0 * inc.nnz + (8.0 + 12.0 * k) * (inc.N + inc.E)
 
   # ---- algebraic distance (SpMV relaxation) ----
+  exch = {}
   if world > 1:
     alg_dist_sharded(ctx, inc, x0, y0, args.alg_iters)  # warm
-    runs = [alg_dist_sharded(ctx, inc, x0, y0, args.alg_iters)[2]
+    runs = [alg_dist_sharded(ctx, inc, x0, y0, args.alg_iters, stats=exch)[2]
             for _ in range(3)]
     alg_ms = max_over_ranks(float(np.median(runs)))
   else:
@@ -156,9 +157,18 @@ def main():
   ctx.upload(inc)
   ctx.alg_set(x0, y0)
   ctx.alg_run(args.alg_iters)
+  barrier()
   t = time.time()
-  n = ctx.sample_hobe(1000 + rank, args.num_neighbors, args.num_samples)
-  sample_s = time.time() - t
+  if world > 1:
+    # row-sharded sampling: each rank samples its rows, then an
+    # all-gather gives every training replica the whole stream
+    from hypergraphembedding_amd.hg2v_sample import sample_sharded
+    n, _ = sample_sharded(inc, args.num_neighbors, args.num_samples, ctx=ctx,
+                          seed=1000, kind="hobe",
+                          device=None if args.dist_backend == "nccl" else "cpu")
+  else:
+    n = ctx.sample_hobe(1000, args.num_neighbors, args.num_samples)
+  sample_s = max_over_ranks(time.time() - t)
 
   # ---- training: the timed steps ----
   ctx.model_init(args.dim, inc.N + 1, inc.E + 1, seed=7 + rank)
@@ -333,8 +343,10 @@ def main():
                     "frac_of_hbm_peak": round(alg_gbps / HBM_PEAK_GBPS, 4),
                     "note": "C3's 35 MB working set is cache-resident; the "
                             "HBM fraction is judged on algdist_c4",
-                    "sharded": world > 1},
+                    "sharded": world > 1, "exchange": exch or None},
         "hobe_sampling_s": round(sample_s, 3),
+        "sampling": ("row-sharded over ranks + record all-gather" if world > 1
+                     else "single GPU"),
         "c2_fobe_d128": c2,
         "end_to_end": e2e,
         "algdist_c4": c4,
@@ -357,9 +369,11 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
   bx0 = rs4.random_sample((big.N, k)).astype(np.float32)
   by0 = rs4.random_sample((big.E, k)).astype(np.float32)
   b_iter4 = 8.0 * big.nnz + (8.0 + 12.0 * k) * (big.N + big.E)
+  exch4 = {}
   if world > 1:
     alg_dist_sharded(ctx, big, bx0, by0, 2)  # warm
-    ms4 = max_over_ranks(alg_dist_sharded(ctx, big, bx0, by0, args.alg_iters)[2])
+    ms4 = max_over_ranks(alg_dist_sharded(ctx, big, bx0, by0, args.alg_iters,
+                                          stats=exch4)[2])
     ctx.upload(big)  # HOBE below runs on the whole graph of this rank
   else:
     ctx.alg_set(bx0, by0)
@@ -376,7 +390,8 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
         "ms_per_iter": round(ms4 / args.alg_iters, 3),
         "gbps": round(gbps4, 1), "bytes_per_iter": b_iter4,
         "frac_of_hbm_peak": round(gbps4 / HBM_PEAK_GBPS, 4),
-        "sharded": world > 1, "graph_gen_s": round(c4_gen, 1)}
+        "sharded": world > 1, "exchange": exch4 or None,
+        "graph_gen_s": round(c4_gen, 1)}
   # ---- HOBE d=256 on the same graph: the north star's 10M/5M workload ----
   # AlgebraicDistanceSamples with quota S on a seeded 2% of node rows and of
   # edge rows (0 elsewhere; the reference samples S per row everywhere, a
@@ -390,9 +405,15 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
   eq4 = np.where(rsq.random_sample(big.E) < args.c4_frac, S4, 0).astype(np.int32)
   sync()
   t = time.perf_counter()
-  n4 = ctx.sample_hobe(4000 + rank, K4, S4, node_q=nq4, edge_q=eq4)
+  if world > 1:
+    from hypergraphembedding_amd.hg2v_sample import sample_sharded
+    n4, _ = sample_sharded(big, K4, S4, ctx=ctx, seed=4000, kind="hobe",
+                           node_quota=nq4, edge_quota=eq4,
+                           device=None if args.dist_backend == "nccl" else "cpu")
+  else:
+    n4 = ctx.sample_hobe(4000, K4, S4, node_q=nq4, edge_q=eq4)
   sync()
-  hobe_sample_s = time.perf_counter() - t
+  hobe_sample_s = max_over_ranks(time.perf_counter() - t)
   rej_rows, fb_rows = ctx.sample_stats()
   ctx.model_init(d4, big.N + 1, big.E + 1, seed=11 + rank)
   sync()

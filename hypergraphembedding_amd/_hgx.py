@@ -54,6 +54,7 @@ SIGNATURES = {
     "hgx_alg_shard_edge_partial": (_int, [_vp, _int]),
     "hgx_alg_shard_edge_final": (_int, [_vp, _int]),
     "hgx_alg_shard_end": (_int, [_vp]),
+    "hgx_alg_shard_wire": (_int, [_vp, _vp, _i64, _vp]),
     "hgx_hobe_probs": (_int, [_vp, _int, _i64, _vp, _vp, _vp]),
     "hgx_incidence_weights": (_int, [_vp, _int, ctypes.c_double, _vp, _vp]),
     "hgx_sample_fobe": (_int, [_vp, _u64, _int, _vp, _vp, _vp, _vp, _pi64]),
@@ -68,6 +69,9 @@ SIGNATURES = {
     "hgx_records_set": (_int, [_vp, _i64, _int, _vp, _vp]),
     "hgx_records_info": (_int, [_vp, _pi64, _pint]),
     "hgx_records_get": (_int, [_vp, _vp, _vp]),
+    "hgx_records_blocks": (_int, [_vp, _pint, _vp]),
+    "hgx_records_export": (_int, [_vp, _vp, _vp]),
+    "hgx_records_import": (_int, [_vp, _i64, _int, _vp, _vp, _int, _vp]),
     "hgx_model_init": (_int, [_vp, _int, _i64, _i64, _u64, _vp, _vp]),
     "hgx_model_get": (_int, [_vp, _vp, _vp]),
     "hgx_train": (_int, [_vp, _int, _int, _f32, _f32, _int, _int, _f32, _u64,
@@ -253,6 +257,11 @@ class Context:
   def alg_shard_end(self):
     self._chk(lib().hgx_alg_shard_end(self.h))
 
+  def alg_shard_wire(self, d_wire, n_shared, edge_slot):
+    es = _c(edge_slot, np.int32)
+    self._keep_slot = es
+    self._chk(lib().hgx_alg_shard_wire(self.h, d_wire, n_shared, _ptr(es)))
+
   # ---- HOBE probabilities / incidence weights ----
   def hobe_probs(self, kind, a, b):
     a = _c(a, np.int32)
@@ -353,6 +362,23 @@ class Context:
     n, K = ctypes.c_int64(), ctypes.c_int()
     self._chk(lib().hgx_records_info(self.h, ctypes.byref(n), ctypes.byref(K)))
     return n.value, K.value
+
+  def records_blocks(self):
+    """Kind-block bounds of the record stream (nblocks + 1 int64)."""
+    nb = ctypes.c_int()
+    b = np.zeros(17, np.int64)
+    self._chk(lib().hgx_records_blocks(self.h, ctypes.byref(nb), _ptr(b)))
+    return b[:nb.value + 1].copy()
+
+  def records_export(self, d_idx, d_tgt):
+    """Copy the records into caller device buffers (data pointers)."""
+    self._chk(lib().hgx_records_export(self.h, d_idx, d_tgt))
+
+  def records_import(self, n, K, d_idx, d_tgt, bounds=None):
+    """Set the records from caller device buffers (data pointers)."""
+    b = None if bounds is None else _c(bounds, np.int64)
+    nb = 0 if b is None else b.size - 1
+    self._chk(lib().hgx_records_import(self.h, n, K, d_idx, d_tgt, nb, _ptr(b)))
 
   def records_get(self):
     n, K = self.records_info()

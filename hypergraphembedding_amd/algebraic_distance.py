@@ -74,11 +74,21 @@ def shard_rows(rp, world, rank):
   return min(lo, len(rp) - 1), min(hi, len(rp) - 1)
 
 
-def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None):
+def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None,
+                     compact=True, stats=None):
   """Node-row-sharded relaxation; the caller's process group does the
   exchange. Every rank must call it with the same inputs. Returns the node
   rows this rank owns (row0, row1, x_own) and all edge coords, already
   rescaled, plus the time in ms of the iteration loop.
+
+  Per iteration (algebraic_distance.py:54-123 split by node rows): the node
+  half of the own rows, the edge partial sums [sum w, sum w x] over the own
+  rows, a SUM all-reduce of those partials, the edge finish, a MAX
+  all-reduce of the min/max words. With `compact` only the edges whose
+  incidences sit on two or more ranks are exchanged, as k + 1 floats
+  (hgx_alg_shard_wire); an edge private to one rank is finished there and
+  gathered once after the last iteration. `stats` (a dict) receives the
+  exchanged bytes per iteration.
 
   `ctx` is a libhgx Context (exchange buffers on its GPU, RCCL) or any
   object with the same alg_shard_* protocol; with device=cpu the exchange
@@ -101,6 +111,23 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None):
   M = 2 * ks * 64  # HGX_MM_REPLICAS
   part = torch.zeros(inc.E * ks, dtype=torch.float32, device=dev)
   mm = torch.zeros(iterations * M, dtype=torch.int32, device=dev)
+  slot = None
+  if compact:
+    # ranks holding incidences of each edge (one int32 all-reduce, once)
+    touched = np.zeros(inc.E, np.int32)
+    touched[inc.col_n[inc.rp_n[r0]:inc.rp_n[r1]]] = 1
+    cnt = torch.from_numpy(touched.copy()).to(dev)  # never alias `touched`
+    dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
+    cnt = cnt.cpu().numpy()
+    shared = cnt >= 2
+    n_shared = int(shared.sum())
+    slot = np.where(shared, np.cumsum(shared) - 1,
+                    np.where(touched == 1, -1, -2)).astype(np.int32)
+    wire = torch.zeros(max(n_shared, 1) * (k + 1), dtype=torch.float32,
+                       device=dev)[:n_shared * (k + 1)]
+    exch = wire
+  else:
+    exch = part
   stream = None
   if on_gpu:
     # kernels and collectives share one (non-default) torch stream: stream
@@ -112,6 +139,8 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None):
     ks_lib = ctx.alg_shard_begin(r0, r1, part.data_ptr(), mm.data_ptr(),
                                  iterations)
     assert ks_lib == ks
+    if compact:
+      ctx.alg_shard_wire(wire.data_ptr() if n_shared else None, n_shared, slot)
     if on_gpu:
       start = torch.cuda.Event(enable_timing=True)
       end = torch.cuda.Event(enable_timing=True)
@@ -121,7 +150,8 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None):
       for it in range(iterations):
         ctx.alg_shard_node(it)
         ctx.alg_shard_edge_partial(it)
-        dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group)
+        if exch.numel():
+          dist.all_reduce(exch, op=dist.ReduceOp.SUM, group=group)
         ctx.alg_shard_edge_final(it)
         dist.all_reduce(mm[it * M:(it + 1) * M], op=dist.ReduceOp.MAX,
                         group=group)
@@ -135,6 +165,23 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None):
       ctx.set_stream(None)
   ms = start.elapsed_time(end) if on_gpu else (time.perf_counter() - t0) * 1e3
   x, y = ctx.alg_get()
+  if compact and (slot == -2).any():
+    # other ranks' private edges: each has exactly one owner
+    priv = torch.from_numpy(np.where((slot == -1)[:, None], y, 0).astype(np.float32))
+    priv = priv.to(dev)
+    dist.all_reduce(priv, op=dist.ReduceOp.SUM, group=group)
+    y = np.where((slot == -2)[:, None], priv.cpu().numpy(), y).astype(np.float32)
+  if stats is not None:
+    mm_bytes = M * 4
+    stats.update(
+        exchange="compact" if compact else "dense",
+        shared_edges=int(n_shared) if compact else inc.E,
+        partial_bytes_per_iter=int(exch.numel()) * 4,
+        dense_partial_bytes_per_iter=inc.E * ks * 4,
+        minmax_bytes_per_iter=mm_bytes,
+        # ring all-reduce: each rank sends and receives 2 (G-1)/G of a buffer
+        ring_bytes_per_rank_per_iter=int(2 * (world - 1) / world *
+                                         (int(exch.numel()) * 4 + mm_bytes)))
   return (r0, r1, x[r0:r1].copy()), y, ms
 
 

@@ -845,6 +845,62 @@ __global__ __launch_bounds__(kBlock) void algdist_edge_final(
   }
 }
 
+// Compact exchange: the shared edges' partial rows [sum w, sum w x_1..k]
+// (k + 1 floats, no padding slot) gathered onto the wire.
+__global__ void algdist_wire_pack(int E, int KS, int k,
+                                  const int *__restrict__ slot,
+                                  const float *__restrict__ part,
+                                  float *__restrict__ wire) {
+  const int64_t total = (int64_t)E * (k + 1);
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < total;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int e = (int)(q / (k + 1)), i = (int)(q % (k + 1));
+    const int s = slot[e];
+    if (s >= 0) wire[(int64_t)s * (k + 1) + i] = part[(int64_t)e * KS + i];
+  }
+}
+
+// algdist_edge_final over the compact exchange: shared edges read their
+// reduced row from the wire, this rank's private edges their local partial,
+// other ranks' private edges are skipped (never read by this rank's node
+// rows; gathered once after the last iteration).
+__global__ __launch_bounds__(kBlock) void algdist_edge_final_wire(
+    int E, int KS, int k, const int *__restrict__ rp_e,
+    const float *__restrict__ self_in, const float *__restrict__ part,
+    const float *__restrict__ wire, const int *__restrict__ slot,
+    float *__restrict__ out, const int *__restrict__ mm_prev,
+    int *__restrict__ mm_cur) {
+  __shared__ int s_mm[4096];
+  __shared__ float s_m[2048], s_d[2048];
+  for (int i = threadIdx.x; i < 2 * KS; i += blockDim.x) s_mm[i] = INT_MIN;
+  load_affine(mm_prev, KS, k, s_m, s_d);
+  const int64_t total = (int64_t)E * KS;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < total;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int e = (int)(q / KS), i = (int)(q % KS);
+    const int sl = slot[e];
+    if (sl == -2) continue;
+    const float *P = sl >= 0 ? wire + (int64_t)sl * (k + 1) : part + (int64_t)e * KS;
+    float v = 0.f;
+    if (i == 0) {
+      v = 1.0f / (float)(rp_e[e + 1] - rp_e[e]);
+    } else if (i <= k) {
+      const float sv = (self_in[q] - s_m[i]) / s_d[i];
+      const float mv = P[i] / P[0];
+      v = (sv + mv) * 0.5f;
+      atomicMax(&s_mm[i], f2ord(v));
+      atomicMax(&s_mm[KS + i], ~f2ord(v));
+    }
+    out[q] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * KS; i += blockDim.x) {
+    const int s = i % KS;
+    if (s >= 1 && s <= k && s_mm[i] != INT_MIN)
+      atomicMax(&mm_cur[(size_t)i * kRep + blockIdx.x % kRep], s_mm[i]);
+  }
+}
+
 // dense R x k  ->  rows [1/len, c_0..c_{k-1}, 0...] of KS floats
 __global__ void pack_rows(int R, int k, int KS, const int *__restrict__ rp,
                           const float *__restrict__ dense,
@@ -1343,6 +1399,8 @@ extern "C" int hgx_alg_shard_begin(hgx_ctx *ctx, int32_t row0, int32_t row1,
   }
   ctx->row0 = row0;
   ctx->row1 = row1;
+  ctx->ext_wire = nullptr;
+  ctx->n_wire = 0;
   ctx->ext_partial = (float *)d_partial;
   ctx->ext_mm = (int *)d_mm;
   ctx->ext_iters = iters;
@@ -1378,6 +1436,38 @@ extern "C" int hgx_alg_shard_edge_partial(hgx_ctx *ctx, int it) {
                       ctx->col_el.as<int>(), nullptr, xn, ctx->ext_partial,
                       nullptr, 0, nullptr, avg, ctx->blk_el.as<int>(),
                       ctx->nblk_el, &ctx->long_el));
+  if (ctx->ext_wire && ctx->n_wire > 0) {
+    hipLaunchKernelGGL(algdist_wire_pack,
+                       dim3(grid_for((int64_t)ctx->E * (ctx->k + 1), 256)),
+                       dim3(256), 0, ctx->stream, ctx->E, ctx->ks, ctx->k,
+                       ctx->wire_slot.as<int>(), ctx->ext_partial, ctx->ext_wire);
+    HGX_LAUNCH_CHECK(ctx);
+  }
+  return HGX_OK;
+}
+
+extern "C" int hgx_alg_shard_wire(hgx_ctx *ctx, void *d_wire, int64_t n_shared,
+                                  const int32_t *edge_slot) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->ext_mm, HGX_ESTATE, "hgx_alg_shard_begin not called");
+  HGX_CHECK(ctx, edge_slot && n_shared >= 0 && (d_wire || n_shared == 0),
+            HGX_EINVAL, "null wire or slot map");
+  std::vector<char> seen((size_t)n_shared, 0);
+  for (int e = 0; e < ctx->E; e++) {
+    const int s = edge_slot[e];
+    HGX_CHECK(ctx, s >= -2 && s < n_shared, HGX_EINVAL,
+              "edge %d: slot %d outside [-2, %lld)", e, s, (long long)n_shared);
+    if (s >= 0) {
+      HGX_CHECK(ctx, !seen[s], HGX_EINVAL, "wire row %d given twice", s);
+      seen[s] = 1;
+    }
+  }
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  HGX_TRY(hgx_ensure(ctx, ctx->wire_slot, sizeof(int) * (ctx->E + 1)));
+  HGX_HIP(ctx, hipMemcpy(ctx->wire_slot.p, edge_slot, sizeof(int) * ctx->E,
+                         hipMemcpyHostToDevice));
+  ctx->ext_wire = (float *)d_wire;
+  ctx->n_wire = n_shared;
   return HGX_OK;
 }
 
@@ -1389,10 +1479,17 @@ extern "C" int hgx_alg_shard_edge_final(hgx_ctx *ctx, int it) {
   const int *prev = it ? ctx->ext_mm + slot * (it - 1) : nullptr;
   int *cur = ctx->ext_mm + slot * it;
   float *yc = ctx->Y[ctx->ycur].as<float>(), *yn = ctx->Y[ctx->ycur ^ 1].as<float>();
-  hipLaunchKernelGGL(algdist_edge_final,
-                     dim3(grid_for((int64_t)ctx->E * ctx->ks, 256)), dim3(256),
-                     0, ctx->stream, ctx->E, ctx->ks, ctx->k,
-                     ctx->rp_e.as<int>(), yc, ctx->ext_partial, yn, prev, cur);
+  if (ctx->ext_wire)
+    hipLaunchKernelGGL(algdist_edge_final_wire,
+                       dim3(grid_for((int64_t)ctx->E * ctx->ks, 256)), dim3(256),
+                       0, ctx->stream, ctx->E, ctx->ks, ctx->k,
+                       ctx->rp_e.as<int>(), yc, ctx->ext_partial, ctx->ext_wire,
+                       ctx->wire_slot.as<int>(), yn, prev, cur);
+  else
+    hipLaunchKernelGGL(algdist_edge_final,
+                       dim3(grid_for((int64_t)ctx->E * ctx->ks, 256)), dim3(256),
+                       0, ctx->stream, ctx->E, ctx->ks, ctx->k,
+                       ctx->rp_e.as<int>(), yc, ctx->ext_partial, yn, prev, cur);
   HGX_LAUNCH_CHECK(ctx);
   ctx->xcur ^= 1;
   ctx->ycur ^= 1;
@@ -1408,5 +1505,7 @@ extern "C" int hgx_alg_shard_end(hgx_ctx *ctx) {
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->ext_mm = nullptr;
   ctx->ext_partial = nullptr;
+  ctx->ext_wire = nullptr;
+  ctx->n_wire = 0;
   return HGX_OK;
 }

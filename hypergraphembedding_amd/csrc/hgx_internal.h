@@ -79,6 +79,12 @@ struct hgx_ctx {
   int nblk_sn = 0, nblk_el = 0;
   LongRows long_sn, long_el;
   float *ext_partial = nullptr;  // E x ks
+  // compact exchange (hgx_alg_shard_wire): shared edges' [sum w, sum w x]
+  // rows of k + 1 floats; per edge its wire row (>= 0), -1 private to this
+  // rank (finished from ext_partial), -2 another rank's private edge
+  float *ext_wire = nullptr;
+  int64_t n_wire = 0;
+  DevBuf wire_slot;
   int *ext_mm = nullptr;         // iters x 2 x ks
   int ext_iters = 0;
   double alg_ms = 0, alg_bytes = 0;
@@ -103,6 +109,11 @@ struct hgx_ctx {
   int64_t n_rec = 0;
   int K = 0;
   DevBuf rec_idx, rec_tgt;
+  // record kind blocks of the stream in the reference's order (e.g. nn, ee,
+  // ne node rows, ne edge rows): block i = [rec_bounds[i], rec_bounds[i+1])
+  static constexpr int kMaxRecBlocks = 16;
+  int64_t rec_bounds[kMaxRecBlocks + 1] = {0};
+  int n_rec_blocks = 0;
 
   // ---- model ----
   int d = 0, dp = 0;

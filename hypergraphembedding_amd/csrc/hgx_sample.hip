@@ -46,6 +46,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <initializer_list>
 #include <climits>
 #include <vector>
 
@@ -1142,6 +1143,13 @@ int check_quota(hgx_ctx *ctx, const int32_t *q, int n, const char *what) {
   return HGX_OK;
 }
 
+// kind-block bounds of the record stream just emitted (hgx_records_blocks)
+void set_blocks(hgx_ctx *ctx, std::initializer_list<int64_t> b) {
+  int i = 0;
+  for (int64_t v : b) ctx->rec_bounds[i++] = v;
+  ctx->n_rec_blocks = i - 1;
+}
+
 void reset_stats(hgx_ctx *ctx) {
   ctx->sample_union_rows = ctx->sample_fallback_rows = 0;
   ctx->sample_uniform_rows = 0;
@@ -1204,6 +1212,9 @@ extern "C" int hgx_sample_fobe(hgx_ctx *ctx, uint64_t seed, int K,
     HGX_TRY(neg_emit(ctx, REC_NE_NODE, gne_n, ctx->E, o_gne, seed, 0x303));
     HGX_TRY(neg_emit(ctx, REC_NE_EDGE, gne_e, ctx->N, o_gen, seed, 0x304));
     HGX_TRY(neighbors(ctx, o_gne, total, seed, 0x400));
+    set_blocks(ctx, {0, o_ee, o_ne, o_en, o_neg, o_gee, o_gee2, o_gne, o_gen, total});
+  } else {
+    set_blocks(ctx, {0, o_ee, o_ne, o_en, total});
   }
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (n_records) *n_records = total;
@@ -1246,6 +1257,7 @@ extern "C" int hgx_sample_hobe_rows(hgx_ctx *ctx, uint64_t seed, int K,
   HGX_TRY(hgx_hobe_fill_probs(ctx, 0, 0, o_ee));
   HGX_TRY(hgx_hobe_fill_probs(ctx, 1, o_ee, o_ne));
   HGX_TRY(hgx_hobe_fill_probs(ctx, 2, o_ne, total));
+  set_blocks(ctx, {0, o_ee, o_ne, o_en, total});
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (n_records) *n_records = total;
   return HGX_OK;
@@ -1279,6 +1291,7 @@ int hgx_sample_pairs4(hgx_ctx *ctx, uint64_t seed, int K, const int32_t *node_q,
   HGX_TRY(emit(ctx, REC_NE_NODE, ne_n, o_ne, 0.f));
   HGX_TRY(emit(ctx, REC_NE_EDGE, ne_e, o_en, 0.f));
   HGX_TRY(neighbors(ctx, o_ne, total, seed, 0x600));
+  set_blocks(ctx, {0, o_ee, o_ne, o_en, total});
   *o_ee_out = o_ee;
   *o_ne_out = o_ne;
   *total_out = total;

@@ -1423,6 +1423,74 @@ extern "C" int hgx_records_set(hgx_ctx *ctx, int64_t n, int K,
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->n_rec = n;
   ctx->K = K;
+  ctx->rec_bounds[0] = 0;
+  ctx->rec_bounds[1] = n;
+  ctx->n_rec_blocks = 1;
+  return HGX_OK;
+}
+
+extern "C" int hgx_records_blocks(hgx_ctx *ctx, int *nblocks, int64_t *bounds) {
+  if (!ctx) return HGX_EINVAL;
+  if (nblocks) *nblocks = ctx->n_rec_blocks;
+  if (bounds)
+    for (int i = 0; i <= ctx->n_rec_blocks; i++) bounds[i] = ctx->rec_bounds[i];
+  return HGX_OK;
+}
+
+extern "C" int hgx_records_export(hgx_ctx *ctx, void *d_idx, void *d_tgt) {
+  if (!ctx) return HGX_EINVAL;
+  const int64_t n = ctx->n_rec;
+  const int R = 4 + 2 * ctx->K;
+  if (n == 0) return HGX_OK;
+  HGX_CHECK(ctx, d_idx || d_tgt, HGX_EINVAL, "null export buffer");
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  if (d_idx)
+    HGX_HIP(ctx, hipMemcpyAsync(d_idx, ctx->rec_idx.p, sizeof(int32_t) * n * R,
+                                hipMemcpyDeviceToDevice, ctx->stream));
+  if (d_tgt)
+    HGX_HIP(ctx, hipMemcpyAsync(d_tgt, ctx->rec_tgt.p, sizeof(float) * n * 3,
+                                hipMemcpyDeviceToDevice, ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HGX_OK;
+}
+
+extern "C" int hgx_records_import(hgx_ctx *ctx, int64_t n, int K,
+                                  const void *d_idx, const void *d_tgt,
+                                  int nblocks, const int64_t *bounds) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, n >= 0 && K >= 1 && K <= 16, HGX_EUNSUP,
+            "num_neighbors K=%d outside [1,16]", K);
+  HGX_CHECK(ctx, n == 0 || (d_idx && d_tgt), HGX_EINVAL, "null record buffer");
+  HGX_CHECK(ctx, nblocks >= 0 && nblocks <= hgx_ctx::kMaxRecBlocks, HGX_EINVAL,
+            "%d record blocks (at most %d)", nblocks, hgx_ctx::kMaxRecBlocks);
+  if (nblocks > 0) {
+    HGX_CHECK(ctx, bounds && bounds[0] == 0 && bounds[nblocks] == n, HGX_EINVAL,
+              "block bounds must run from 0 to n");
+    for (int i = 0; i < nblocks; i++)
+      HGX_CHECK(ctx, bounds[i] <= bounds[i + 1], HGX_EINVAL,
+                "block bounds not ascending");
+  }
+  const int R = 4 + 2 * K;
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  HGX_TRY(hgx_ensure(ctx, ctx->rec_idx, sizeof(int32_t) * (n * R + 1)));
+  HGX_TRY(hgx_ensure(ctx, ctx->rec_tgt, sizeof(float) * (n * 3 + 1)));
+  if (n) {
+    HGX_HIP(ctx, hipMemcpyAsync(ctx->rec_idx.p, d_idx, sizeof(int32_t) * n * R,
+                                hipMemcpyDeviceToDevice, ctx->stream));
+    HGX_HIP(ctx, hipMemcpyAsync(ctx->rec_tgt.p, d_tgt, sizeof(float) * n * 3,
+                                hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->n_rec = n;
+  ctx->K = K;
+  if (nblocks > 0) {
+    for (int i = 0; i <= nblocks; i++) ctx->rec_bounds[i] = bounds[i];
+    ctx->n_rec_blocks = nblocks;
+  } else {
+    ctx->rec_bounds[0] = 0;
+    ctx->rec_bounds[1] = n;
+    ctx->n_rec_blocks = 1;
+  }
   return HGX_OK;
 }
 

@@ -100,6 +100,105 @@ def sample_hobe(inc, num_neighbors, num_samples, ctx=None, seed=None,
   return DeviceRecords(ctx, inc, n, num_neighbors)
 
 
+def shard_range(n, world, rank):
+  """Contiguous rows [lo, hi) of `rank` out of n rows split over `world`."""
+  return n * rank // world, n * (rank + 1) // world
+
+
+def sample_sharded(inc, num_neighbors, num_samples, ctx=None, seed=0,
+                   kind="hobe", node_quota=None, edge_quota=None, group=None,
+                   gather=True, device=None):
+  """Row-sharded sampling over the ranks of a torch.distributed group
+  (sampling shards by row with no data-path collective).
+
+  Rank g samples only its node rows [n0, n1) and edge rows [e0, e1)
+  (kind "hobe": AlgebraicDistanceSamples, quota S per row unless quotas are
+  given; kind "fobe": BooleanSamples with the given per-row quotas): the
+  other rows' quotas are 0. Every draw is keyed by (seed, pattern, row), so with the same seed
+  on every rank the ranks' rows are exactly the rows a single process would
+  draw. A count all-gather gives every rank the kind-block sizes of every
+  rank. With `gather`, the per-rank streams are then all-gathered and laid
+  out kind block by kind block, ranks in row order inside each block: the
+  reference's record order (nn, ee, ne node rows, ne edge rows, ...), the
+  stream every training replica needs. The K neighbour draws of node-edge
+  records are keyed by the record's position, so only they differ from a
+  single-process run (same distribution).
+
+  Collectives: RCCL on device buffers for a GPU device (the records never
+  leave HBM), gloo through host arrays otherwise. Returns
+  (records now on ctx, sizes[world][blocks]).
+  """
+  import torch
+  import torch.distributed as dist
+  ctx = ctx or get_context()
+  world, rank = dist.get_world_size(group), dist.get_rank(group)
+  K = num_neighbors
+  n0, n1 = shard_range(inc.N, world, rank)
+  e0, e1 = shard_range(inc.E, world, rank)
+  if node_quota is None:  # HOBE: S per row (hg2v_sample.py:659-703)
+    assert kind == "hobe"
+    node_quota = np.full(inc.N, num_samples, np.int32)
+    edge_quota = np.full(inc.E, num_samples, np.int32)
+  nq = np.zeros(inc.N, np.int32)
+  eq = np.zeros(inc.E, np.int32)
+  nq[n0:n1] = np.asarray(node_quota, np.int32)[n0:n1]
+  eq[e0:e1] = np.asarray(edge_quota, np.int32)[e0:e1]
+  if kind == "hobe":
+    ctx.sample_hobe(seed, K, num_samples, node_q=nq, edge_q=eq)
+  else:
+    ctx.sample_fobe(seed, K, nq, eq)
+  bounds = ctx.records_blocks()
+  sizes = np.diff(bounds)
+  gpu = device is None or torch.device(device).type == "cuda"
+  dev = torch.device("cuda", ctx.device) if device is None else torch.device(device)
+  t = torch.tensor(sizes, dtype=torch.int64, device=dev)
+  got = [torch.zeros_like(t) for _ in range(world)]
+  dist.all_gather(got, t, group=group)
+  allsz = np.stack([g.cpu().numpy() for g in got])  # [world][blocks]
+  if not gather:
+    return int(sizes.sum()), allsz
+  R = 4 + 2 * K
+  n_loc = allsz.sum(1)
+  maxn = int(n_loc.max())
+  total = int(allsz.sum())
+  blk_tot = allsz.sum(0)
+  gbounds = np.concatenate([[0], np.cumsum(blk_tot)]).astype(np.int64)
+  # destination of (rank r, block j): block start + ranks before r
+  dst = gbounds[:-1][None, :] + np.concatenate(
+      [np.zeros((1, allsz.shape[1]), np.int64), np.cumsum(allsz, 0)[:-1]], 0)
+  src = np.concatenate([np.zeros((world, 1), np.int64),
+                        np.cumsum(allsz, 1)[:, :-1]], 1)
+  li = torch.zeros((max(maxn, 1), R), dtype=torch.int32, device=dev)
+  lt = torch.zeros((max(maxn, 1), 3), dtype=torch.float32, device=dev)
+  nl = int(n_loc[rank])
+  if gpu:
+    if nl:
+      ctx.records_export(li.data_ptr(), lt.data_ptr())
+  else:
+    hi, ht = ctx.records_get()
+    li[:nl] = torch.from_numpy(hi)
+    lt[:nl] = torch.from_numpy(ht)
+  gi = [torch.empty_like(li) for _ in range(world)]
+  gt = [torch.empty_like(lt) for _ in range(world)]
+  dist.all_gather(gi, li, group=group)
+  dist.all_gather(gt, lt, group=group)
+  fi = torch.empty((max(total, 1), R), dtype=torch.int32, device=dev)
+  ft = torch.empty((max(total, 1), 3), dtype=torch.float32, device=dev)
+  for r in range(world):
+    for j in range(allsz.shape[1]):
+      c = int(allsz[r, j])
+      if c:
+        d, s0 = int(dst[r, j]), int(src[r, j])
+        fi[d:d + c] = gi[r][s0:s0 + c]
+        ft[d:d + c] = gt[r][s0:s0 + c]
+  if gpu:
+    torch.cuda.synchronize(dev)
+    ctx.records_import(total, K, fi.data_ptr(), ft.data_ptr(), gbounds)
+  else:
+    ctx.records_set(fi[:total].numpy(), ft[:total].numpy())
+  return total, allsz
+
+
 def BooleanSamples(hypergraph, num_neighbors, num_samples, neg_samples=0,
                    disable_pbar=False):
   """hg2v_sample.py:125-242 (expects a compressed hypergraph, as the

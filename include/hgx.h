@@ -107,6 +107,15 @@ int hgx_alg_shard_node(hgx_ctx *ctx, int it);
 int hgx_alg_shard_edge_partial(hgx_ctx *ctx, int it);
 int hgx_alg_shard_edge_final(hgx_ctx *ctx, int it);
 int hgx_alg_shard_end(hgx_ctx *ctx);
+/* Compact exchange (optional, after begin): only edges whose incidences sit
+ * on two or more ranks go on the wire, as rows of k + 1 floats
+ * [sum w, sum w x_1..k] (no padding slot). edge_slot[E] (host): wire row of
+ * a shared edge (0..n_shared-1, the same on every rank), -1 an edge private
+ * to this rank, -2 another rank's private edge (left unset here). The caller
+ * then all-reduces d_wire (n_shared * (k + 1) floats, SUM) in place of
+ * d_partial, which becomes this rank's local scratch. */
+int hgx_alg_shard_wire(hgx_ctx *ctx, void *d_wire, int64_t n_shared,
+                       const int32_t *edge_slot);
 
 /* ---- HOBE probabilities ------------------------------------------------ *
  * _same_type_dist_calc (hg2v_sample.py:527-543) and DiffTypeDistanceSample
@@ -180,6 +189,18 @@ int hgx_records_set(hgx_ctx *ctx, int64_t n, int K, const int32_t *idx,
                     const float *tgt);
 int hgx_records_info(hgx_ctx *ctx, int64_t *n, int *K);
 int hgx_records_get(hgx_ctx *ctx, int32_t *idx, float *tgt);
+/* Kind blocks of the stream in the reference's record order (hgx_sample_*:
+ * nn, ee, ne node rows, ne edge rows [, the five negative blocks]; one block
+ * after hgx_records_set): block i = [bounds[i], bounds[i+1]), at most 16
+ * blocks (bounds holds nblocks + 1 entries). */
+int hgx_records_blocks(hgx_ctx *ctx, int *nblocks, int64_t *bounds);
+/* Device-to-device record copies for collectives over caller-owned device
+ * buffers (e.g. RCCL all-gather of row-sharded samples):
+ * export the n x (4+2K) ids and n x 3 targets; import a stream (nblocks 0 ->
+ * one block). */
+int hgx_records_export(hgx_ctx *ctx, void *d_idx, void *d_tgt);
+int hgx_records_import(hgx_ctx *ctx, int64_t n, int K, const void *d_idx,
+                       const void *d_tgt, int nblocks, const int64_t *bounds);
 
 /* ---- model + trainer ---------------------------------------------------- *
  * Replaces BooleanModel / UnweightedFloatModel (hg2v_model.py:51-203) and

@@ -58,7 +58,15 @@ class ShardEmu:
     self.mm[:] = INT_MIN
     self.deg_n = np.diff(inc.rp_n).astype(np.float32)
     self.deg_e = np.diff(inc.rp_e).astype(np.float32)
+    self.slot = None
     return self.ks
+
+  def alg_shard_wire(self, d_wire, n_shared, edge_slot):
+    """hgx_alg_shard_wire: shared edges' [sum w, sum w x] rows on the wire."""
+    self.slot = np.asarray(edge_slot, np.int32)
+    self.wire = (_view(d_wire, n_shared * (self.k + 1), ctypes.c_float,
+                       np.float32).reshape(n_shared, self.k + 1)
+                 if n_shared else np.zeros((0, self.k + 1), np.float32))
 
   def _affine(self, it):
     """(min, 1/(max-min)) per dim from slot it-1 (identity for it == 0)."""
@@ -99,12 +107,23 @@ class ShardEmu:
       w = 1.0 / self.deg_n[c].astype(np.float64)
       self.part[e, 0] = w.sum()
       self.part[e, 1:self.k + 1] = (w[:, None] * self.Xn[c]).sum(0)
+    if self.slot is not None:
+      sh = self.slot >= 0
+      self.wire[self.slot[sh]] = self.part[sh, :self.k + 1]
 
   def alg_shard_edge_final(self, it):
     m, d = self._affine(it)
-    mean = self.part[:, 1:self.k + 1] / self.part[:, :1]
+    P = self.part[:, :self.k + 1].copy()
+    keep = np.ones(self.inc.E, bool)
+    if self.slot is not None:
+      sh = self.slot >= 0
+      P[sh] = self.wire[self.slot[sh]]
+      keep = self.slot != -2
+    with np.errstate(invalid="ignore", divide="ignore"):
+      mean = P[:, 1:] / P[:, :1]
     yn = (((self.Y - m) * d + mean) * 0.5).astype(np.float32)
-    self._fold(it, yn)
+    yn[~keep] = self.Y[~keep]  # another rank's private edge: not ours
+    self._fold(it, yn[keep])
     self.X, self.Y = self.Xn, yn
 
   def alg_shard_end(self):

@@ -131,3 +131,91 @@ def test_sharded_algdist_rccl_single_rank(tmp_path):
   assert int(d["r0"]) == 0 and int(d["r1"]) == d["x"].shape[0]
   assert np.abs(d["x"] - z["x_20"]).max() <= 1e-4
   assert np.abs(d["y"] - z["y_20"]).max() <= 1e-4
+
+
+# ---- row-sharded sampling -------------------------------
+def _sample_setup(inc, kind, ctx):
+  ctx.upload(inc)
+  if kind == "hobe":
+    r = O.Rng(2)
+    ctx.alg_set(r.random((inc.N, 10)), r.random((inc.E, 10)))
+    ctx.alg_run(5)
+
+
+def _sample_worker(rank, world, port, out_path, kind, backend):
+  import torch
+  import torch.distributed as dist
+  import sys
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  sys.path[:0] = [root, os.path.join(root, "oracle"), os.path.join(root, "tests")]
+  from test_gpu_sharded import _graph, _sample_setup
+  from hypergraphembedding_amd import _hgx
+  from hypergraphembedding_amd.hg2v_sample import sample_sharded
+  os.environ["MASTER_ADDR"] = "127.0.0.1"
+  os.environ["MASTER_PORT"] = str(port)
+  torch.cuda.set_device(0)
+  if backend == "nccl":
+    dist.init_process_group("nccl", rank=rank, world_size=world,
+                            device_id=torch.device("cuda", 0))
+  else:
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+  inc = _graph("powerlaw")
+  ctx = _hgx.Context(0)
+  _sample_setup(inc, kind, ctx)
+  S = 20
+  q = (np.full(inc.N, S, np.int32), np.full(inc.E, S, np.int32))
+  total, sizes = sample_sharded(inc, 5, S, ctx=ctx, seed=123, kind=kind,
+                                node_quota=q[0], edge_quota=q[1],
+                                device=None if backend == "nccl" else "cpu")
+  idx, tgt = ctx.records_get()
+  assert idx.shape[0] == total == int(sizes.sum())
+  np.savez(out_path + f".{rank}.npz", idx=idx, tgt=tgt, sizes=sizes,
+           bounds=ctx.records_blocks())
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,world,backend", [("hobe", 2, "gloo"),
+                                                ("hobe", 3, "gloo"),
+                                                ("fobe", 2, "gloo"),
+                                                ("hobe", 1, "nccl")])
+def test_row_sharded_sampling_equals_single_process(tmp_path, kind, world,
+                                                    backend):
+  """Every rank samples only its rows; after the count all-gather and the
+  record all-gather, every rank holds the single-process stream: the same
+  pairs and probabilities in the reference's kind-block order (draws are
+  keyed by seed and row), and neighbour lists drawn from the right rows."""
+  import torch.multiprocessing as mp
+  from hypergraphembedding_amd import _hgx
+  out = str(tmp_path / "samp")
+  mp.start_processes(_sample_worker,
+                     args=(world, _free_port(), out, kind, backend),
+                     nprocs=world, join=True, start_method="spawn")
+  inc = _graph("powerlaw")
+  ctx = _hgx.Context(0)
+  _sample_setup(inc, kind, ctx)
+  S = 20
+  if kind == "hobe":
+    n = ctx.sample_hobe(123, 5, S)
+  else:
+    n = ctx.sample_fobe(123, 5, np.full(inc.N, S, np.int32),
+                        np.full(inc.E, S, np.int32))
+  ridx, rtgt = ctx.records_get()
+  rb = ctx.records_blocks()
+  ctx.close()
+  for r in range(world):
+    d = np.load(out + f".{r}.npz")
+    idx, tgt = d["idx"], d["tgt"]
+    assert idx.shape[0] == n
+    assert np.array_equal(idx[:, :4], ridx[:, :4])
+    assert np.array_equal(tgt, rtgt)
+    if backend == "nccl":
+      assert np.array_equal(d["bounds"], rb)
+    assert d["sizes"].shape == (world, 4)
+    assert np.array_equal(d["sizes"].sum(0), np.diff(rb))
+    ne = (idx[:, 0] > 0) & (idx[:, 3] > 0) & (idx[:, 2] == 0)
+    sel = np.flatnonzero(ne)[::97]
+    for i in sel:
+      v, e = idx[i, 0] - 1, idx[i, 3] - 1
+      assert np.isin(idx[i, 4:9] - 1, inc.col_e[inc.rp_e[e]:inc.rp_e[e + 1]]).all()
+      assert np.isin(idx[i, 9:14] - 1, inc.col_n[inc.rp_n[v]:inc.rp_n[v + 1]]).all()

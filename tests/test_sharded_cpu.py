@@ -26,7 +26,7 @@ def _free_port():
   return p
 
 
-def _worker(rank, world, port, out_path, iters):
+def _worker(rank, world, port, out_path, iters, compact=True, graph="tiny"):
   import torch
   import torch.distributed as dist
   root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -39,22 +39,47 @@ def _worker(rank, world, port, out_path, iters):
   os.environ["MASTER_ADDR"] = "127.0.0.1"
   os.environ["MASTER_PORT"] = str(port)
   dist.init_process_group("gloo", rank=rank, world_size=world)
-  inc = gi("csr_tiny.npz")
+  inc = gi("csr_tiny.npz") if graph == "tiny" else _local_graph()
   r = O.Rng(0)
   x0, y0 = r.random((inc.N, 10)), r.random((inc.E, 10))
+  st = {}
   (r0, r1, xo), y, _ = alg_dist_sharded(ShardEmu(), inc, x0, y0, iters,
-                                        device=torch.device("cpu"))
-  np.savez(out_path + f".{rank}.npz", r0=r0, r1=r1, x=xo, y=y)
+                                        device=torch.device("cpu"),
+                                        compact=compact, stats=st)
+  np.savez(out_path + f".{rank}.npz", r0=r0, r1=r1, x=xo, y=y,
+           wire=st["partial_bytes_per_iter"],
+           dense=st["dense_partial_bytes_per_iter"])
   dist.barrier()
   dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_driver_gloo(tmp_path, world):
+def _local_graph():
+  """Two communities of 60 nodes / 20 edges each (node ids ordered by
+  community) joined by 3 bridge edges: most edges sit on one rank."""
+  from hypergraphembedding_amd.hypergraph_util import Incidence
+  rs = np.random.RandomState(7)
+  rows, cols = [], []
+  for c in range(2):
+    for v in range(60):
+      for e in rs.choice(20, 3, replace=False):
+        rows.append(60 * c + v)
+        cols.append(20 * c + e)
+  for b in range(3):
+    for v in (b, 60 + b):
+      rows.append(v)
+      cols.append(40 + b)
+  a = np.unique(np.array(rows) * 64 + np.array(cols))
+  rows, cols = a // 64, a % 64
+  rp = np.searchsorted(rows, np.arange(121))
+  return Incidence(120, 43, rp, cols)
+
+
+@pytest.mark.parametrize("world,compact", [(2, True), (3, True), (2, False)])
+def test_sharded_driver_gloo(tmp_path, world, compact):
   import torch.multiprocessing as mp
   iters = 20
   out = str(tmp_path / "shard")
-  mp.start_processes(_worker, args=(world, _free_port(), out, iters),
+  mp.start_processes(_worker, args=(world, _free_port(), out, iters, compact),
                      nprocs=world, join=True, start_method="spawn")
   inc = golden_incidence("csr_tiny.npz")
   z = golden("algdist_tiny.npz")
@@ -92,3 +117,29 @@ def test_order_words_roundtrip():
   assert np.all(np.diff(w.astype(np.int64)) >= 0)  # order preserving
   assert np.array_equal(ord2f(w), v)
   assert np.all(np.diff((~w).astype(np.int64)) <= 0)  # ~ reverses order
+
+
+def test_sharded_compact_exchange_local_edges(tmp_path):
+  """A graph whose edges mostly sit on one rank: only the bridge edges go on
+  the wire (k + 1 floats each), and the result still equals the oracle."""
+  import torch.multiprocessing as mp
+  sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(
+      os.path.abspath(__file__))), "oracle"))
+  import oracle as O
+  world, iters = 2, 15
+  out = str(tmp_path / "local")
+  mp.start_processes(_worker, args=(world, _free_port(), out, iters, True,
+                                    "local"),
+                     nprocs=world, join=True, start_method="spawn")
+  inc = _local_graph()
+  r = O.Rng(0)
+  x0, y0 = r.random((inc.N, 10)), r.random((inc.E, 10))
+  xr, yr = O.algdist(inc, x0, y0, iters)
+  x = np.zeros((inc.N, 10), np.float32)
+  for rk in range(world):
+    d = np.load(out + f".{rk}.npz")
+    x[int(d["r0"]):int(d["r1"])] = d["x"]
+    assert np.abs(d["y"] - yr).max() <= 1e-4  # every rank has every edge
+    assert int(d["wire"]) == 3 * 11 * 4  # the 3 bridge edges, k + 1 floats
+    assert int(d["dense"]) == inc.E * 12 * 4
+  assert np.abs(x - xr).max() <= 1e-4
