@@ -78,6 +78,7 @@ SIGNATURES = {
                          _vp, _vp, _pint]),
     "hgx_train_last_stats": (_int, [_vp, _pdbl, _pi64, _pi64]),
     "hgx_train_path_stats": (_int, [_vp, _pi64, _pi64]),
+    "hgx_train_last_loss": (_int, [_vp, _pdbl]),
     "hgx_synth_powerlaw": (_int, [_i32, _i32, ctypes.c_double, ctypes.c_double,
                                   _u64, _vp, _vp, _pi64,
                                   ctypes.POINTER(ctypes.c_int32)]),
@@ -421,6 +422,12 @@ class Context:
     self._chk(lib().hgx_train_last_stats(self.h, ctypes.byref(ms),
                                          ctypes.byref(rec), ctypes.byref(bat)))
     return ms.value, rec.value, bat.value
+
+  def train_loss_sum(self):
+    """Sum of the per-record losses of the last trained epoch (double)."""
+    v = ctypes.c_double()
+    self._chk(lib().hgx_train_last_loss(self.h, ctypes.byref(v)))
+    return v.value
 
   def train_path_stats(self):
     """(fused, split) batch counts of the last train() call."""

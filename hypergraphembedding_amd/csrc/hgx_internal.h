@@ -120,6 +120,7 @@ struct hgx_ctx {
   int64_t node_rows = 0, edge_rows = 0;
   DevBuf ntab, etab, nacc, eacc;
   double train_ms = 0, train_epoch_ms = 0;
+  double train_loss_sum = 0;  // sum of per-record losses, last epoch
   int64_t train_records = 0, train_batches = 0;
   int64_t train_fused = 0, train_split = 0;
 

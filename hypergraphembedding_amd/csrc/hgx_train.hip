@@ -2080,6 +2080,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
         batch_ms += m;
     }
     const double cur = lsum / (double)n;
+    ctx->train_loss_sum = lsum;
     if (epoch_loss) epoch_loss[ep] = (float)cur;
     if (cur < best - (double)min_delta) {
       best = cur;
@@ -2119,6 +2120,12 @@ extern "C" int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
   if (ms) *ms = ctx->train_ms;
   if (records) *records = ctx->train_records;
   if (batches) *batches = ctx->train_batches;
+  return HGX_OK;
+}
+
+extern "C" int hgx_train_last_loss(hgx_ctx *ctx, double *loss_sum) {
+  if (!ctx) return HGX_EINVAL;
+  if (loss_sum) *loss_sum = ctx->train_loss_sum;
   return HGX_OK;
 }
 

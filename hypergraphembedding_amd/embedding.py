@@ -24,10 +24,10 @@ from .algebraic_distance import EmbedAlgebraicDistance, coords_to_embedding
 from .combine_embeddings_util import (CombineEmbeddingsViaConcatenation,
                                       CombineEmbeddingsViaNodeEdgeClassifier)
 from .hg2v_model import Hg2vModel
-from .hg2v_sample import sample_fobe, sample_hobe, sample_jaccard
+from .hg2v_sample import _quotas, sample_fobe, sample_hobe, sample_jaccard
 from .hypergraph_util import Incidence
 from .proto import HypergraphEmbedding
-from .runtime import get_context
+from .runtime import get_context, numpy_seed
 
 log = logging.getLogger()
 
@@ -106,9 +106,27 @@ def _plot_distributions(path, records):
   fig.savefig(str(path))
 
 
+# Records resident at once before the skeleton streams the record stream in
+# row-range chunks (68 B per record at K = 5: 2^30 records = 73 GB of HBM).
+RECORDS_BUDGET = 1 << 30
+
+
+def _row_chunks(inc, bound_per_row, budget):
+  """Split node rows and edge rows into n contiguous ranges so that each
+  chunk's record upper bound (bound_per_row per node row and per edge row)
+  stays within `budget`."""
+  total = bound_per_row * (inc.N + inc.E)
+  n = max(1, -(-total // budget))
+  nodes = [(inc.N * c // n, inc.N * (c + 1) // n) for c in range(n)]
+  edges = [(inc.E * c // n, inc.E * (c + 1) // n) for c in range(n)]
+  return list(zip(nodes, edges))
+
+
 def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
                              loss, act, fit_batch_size, fit_epochs,
-                             debug_summary_path, disable_pbar, ctx=None):
+                             debug_summary_path, disable_pbar, ctx=None,
+                             chunk_sampler_fn=None, bound_per_row=0,
+                             records_budget=None):
   """embedding.py:269-305, device-resident end to end. `hypergraph` is the
   reference's Hypergraph message or an already compressed Incidence (e.g.
   proto_native.read_incidence of a file too large for Python protobuf)."""
@@ -118,6 +136,18 @@ def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
     inc = hypergraph
   else:
     inc = Incidence.from_hypergraph(hypergraph)  # CompressRange + CSR
+  budget = RECORDS_BUDGET if records_budget is None else records_budget
+  if chunk_sampler_fn is not None and bound_per_row * (inc.N + inc.E) > budget:
+    # the stream does not fit: sample and train row-range chunks in turn
+    chunks = _row_chunks(inc, bound_per_row, budget)
+    seed = numpy_seed()
+    prep = chunk_sampler_fn(inc, ctx)
+    model = Hg2vModel(inc.N + 1, inc.E + 1, dimension, num_neighbors, loss,
+                      act, ctx=ctx)
+    model.fit_streaming(lambda c: prep(seed, *chunks[c]), len(chunks),
+                        batch_size=fit_batch_size, epochs=fit_epochs)
+    node_w, edge_w = model.get_weights()
+    return coords_to_embedding(inc, node_w[1:], edge_w[1:], dimension, "")
   records = sampler_fn(inc, ctx)
   if debug_summary_path is not None:
     _plot_distributions(debug_summary_path, records)
@@ -130,38 +160,87 @@ def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
 
 def EmbedHg2vBoolean(hypergraph, dimension, num_neighbors=5, num_samples=200,
                      batch_size=256, epochs=10, neg_samples=0,
-                     debug_summary_path=None, disable_pbar=False):
-  """FOBE: BooleanSamples + BooleanModel (embedding.py:308-329)."""
+                     debug_summary_path=None, disable_pbar=False,
+                     records_budget=None):
+  """FOBE: BooleanSamples + BooleanModel (embedding.py:308-329). A stream of
+  more than `records_budget` records is sampled and trained in row-range
+  chunks (Hg2vModel.fit_streaming)."""
   sampler_fn = lambda inc, ctx: sample_fobe(inc, num_neighbors, num_samples,
                                             neg_samples, ctx=ctx)
+
+  def chunk_sampler_fn(inc, ctx):
+    ctx.upload(inc)
+    q = [_quotas(w, n) for w in (inc.node_weight, inc.edge_weight)
+         for n in (num_samples, neg_samples)]
+
+    def chunk(seed, nodes, edges):
+      nq, gnq, eq, geq = (np.zeros_like(x) for x in q)
+      nq[nodes[0]:nodes[1]] = q[0][nodes[0]:nodes[1]]
+      gnq[nodes[0]:nodes[1]] = q[1][nodes[0]:nodes[1]]
+      eq[edges[0]:edges[1]] = q[2][edges[0]:edges[1]]
+      geq[edges[0]:edges[1]] = q[3][edges[0]:edges[1]]
+      neg = neg_samples > 0
+      return ctx.sample_fobe(seed, num_neighbors, nq, eq, gnq if neg else None,
+                             geq if neg else None)
+    return chunk
+
+  # per row at most q nn (or ee) and q node-edge records, q = int(w * S)
+  # (hg2v_sample.py:138-194), plus 3 negative blocks of int(w * neg_samples)
+  inc0 = hypergraph if isinstance(hypergraph, Incidence) else None
+  wmax = 1.0 if inc0 is None else float(max(inc0.node_weight.max(initial=1),
+                                            inc0.edge_weight.max(initial=1)))
   emb = _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors,
                                  sampler_fn, _hgx.LOSS_KLD, _hgx.ACT_SIGMOID,
                                  batch_size, epochs, debug_summary_path,
-                                 disable_pbar)
+                                 disable_pbar, chunk_sampler_fn=chunk_sampler_fn,
+                                 bound_per_row=int(wmax * (2 * num_samples +
+                                                           3 * neg_samples)),
+                                 records_budget=records_budget)
   emb.method_name = "HG2V_BOOLEAN"
   return emb
 
 
 def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
                      num_samples=200, batch_size=256, epochs=10,
-                     debug_summary_path=None, disable_pbar=False):
+                     debug_summary_path=None, disable_pbar=False,
+                     records_budget=None):
   """HOBE: alg-dist (k=10, 20 iterations) + AlgebraicDistanceSamples +
   UnweightedFloatModel (embedding.py:389-416). `alpha` is accepted and, as
-  in the reference, not used (_alpha_scale is called with alpha=0)."""
+  in the reference, not used (_alpha_scale is called with alpha=0).
+  A stream of more than `records_budget` records (RECORDS_BUDGET) is
+  sampled and trained in row-range chunks (Hg2vModel.fit_streaming)."""
   del alpha
 
-  def sampler_fn(inc, ctx):
+  def alg_dist(inc, ctx):
     x0 = np.random.random((inc.N, 10))  # algebraic_distance.py:140-141
     y0 = np.random.random((inc.E, 10))
     ctx.upload(inc)
     ctx.alg_set(x0, y0)
     ctx.alg_run(20)  # coords stay resident for the HOBE probabilities
+
+  def sampler_fn(inc, ctx):
+    alg_dist(inc, ctx)
     return sample_hobe(inc, num_neighbors, num_samples, ctx=ctx)
 
+  def chunk_sampler_fn(inc, ctx):
+    alg_dist(inc, ctx)
+
+    def chunk(seed, nodes, edges):
+      nq = np.zeros(inc.N, np.int32)
+      eq = np.zeros(inc.E, np.int32)
+      nq[nodes[0]:nodes[1]] = num_samples
+      eq[edges[0]:edges[1]] = num_samples
+      return ctx.sample_hobe(seed, num_neighbors, num_samples, node_q=nq,
+                             edge_q=eq)
+    return chunk
+
+  # per row at most S nn (or ee) and S node-edge records (hg2v_sample.py:659-703)
   emb = _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors,
                                  sampler_fn, _hgx.LOSS_MSE, _hgx.ACT_RELU,
                                  batch_size, epochs, debug_summary_path,
-                                 disable_pbar)
+                                 disable_pbar, chunk_sampler_fn=chunk_sampler_fn,
+                                 bound_per_row=2 * num_samples,
+                                 records_budget=records_budget)
   emb.method_name = "HG2V_ALG_DIST"
   return emb
 

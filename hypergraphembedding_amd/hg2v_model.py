@@ -37,6 +37,49 @@ class Hg2vModel:
                           shuffle_seed=numpy_seed() if shuffle_seed is None
                           else shuffle_seed, perms=perms)
 
+  def fit_streaming(self, chunk_fn, n_chunks, batch_size=256, epochs=10,
+                    min_delta=1e-3, lr=0.01, eps=1e-7, seed=None,
+                    chunk_perms=None):
+    """fit() over a record stream too large to keep resident (SURVEY §5:
+    "stream samples in chunks"; the reference materialises every record,
+    embedding.py:277-284). chunk_fn(c) makes chunk c resident on the context
+    and returns its record count; chunks must be the same records every
+    epoch (the device samplers are keyed by seed and row, so re-sampling a
+    row range reproduces it). Per epoch the chunk order is shuffled and each
+    chunk's records are shuffled on the device (a windowed shuffle in place
+    of Keras' global one over records that never coexist); model state
+    carries across chunks (one-epoch hgx_train calls), the epoch loss is the
+    record-weighted mean and EarlyStopping(min_delta, patience=0) applies to
+    it. chunk_perms[ep][c] (optional) fixes a chunk's record order.
+    Returns the epoch losses; total records per epoch may exceed 2^31."""
+    import numpy as np
+    rs = np.random.RandomState(numpy_seed() % (2**32) if seed is None else seed)
+    best, losses = float("inf"), []
+    self.records_per_epoch = 0
+    for ep in range(epochs):
+      order = (np.arange(n_chunks) if chunk_perms is not None
+               else rs.permutation(n_chunks))
+      lsum, n = 0.0, 0
+      for c in order:
+        m = chunk_fn(int(c))
+        if m == 0:
+          continue
+        perms = None if chunk_perms is None else chunk_perms[ep][int(c)][None, :]
+        self.ctx.train(batch=batch_size, max_epochs=1, lr=lr, eps=eps,
+                       loss=self.loss, act=self.act, min_delta=-1e30,
+                       shuffle_seed=int(rs.randint(0, 2**62, dtype=np.int64)),
+                       perms=perms)
+        lsum += self.ctx.train_loss_sum()
+        n += m
+      self.records_per_epoch = n
+      cur = lsum / max(n, 1)
+      losses.append(cur)
+      if cur < best - min_delta:
+        best = cur
+      else:
+        break
+    return np.array(losses, np.float32)
+
   def get_weights(self):
     return self.ctx.model_get()
 

@@ -233,6 +233,14 @@ int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
  * padding row's gradient. */
 int hgx_train_path_stats(hgx_ctx *ctx, int64_t *fused_batches,
                          int64_t *split_batches);
+/* Sum of the per-record losses (all three heads) of the last epoch of the
+ * last hgx_train, in double: epoch loss = sum / records. Consecutive
+ * hgx_train calls continue the same model state (tables and Adagrad
+ * accumulators persist; the padding row is written back at the end of each
+ * call), so a stream too large to keep resident trains as a sequence of
+ * one-epoch calls over resident chunks, the caller adding up these sums
+ * (hg2v_model.Hg2vModel.fit_streaming). */
+int hgx_train_last_loss(hgx_ctx *ctx, double *loss_sum);
 
 /* ---- dense MLP engine (combiners + link-prediction classifier) --------- *
  * Replaces the Keras models of
