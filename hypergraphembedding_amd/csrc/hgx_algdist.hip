@@ -52,8 +52,11 @@ enum { MODE_FULL = 0, MODE_PARTIAL = 1 };
 // without its global atomics
 #ifdef HGX_DEBUG_KNOBS
 __constant__ int g_ablate = 0;  // ablation bits (diagnostic builds only)
+// source rows >= g_hot_lim gathered with non-temporal loads (experiment)
+__constant__ int g_hot_lim = 0x7fffffff;
 #else
 static constexpr int g_ablate = 0;
+static constexpr int g_hot_lim = 0x7fffffff;
 #endif
 
 __device__ __forceinline__ float4 f4fma(float w, float4 v, float4 a) {
@@ -306,6 +309,12 @@ __device__ __forceinline__ float quad_stride_sum(float x) {
   return x;
 }
 
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 nt_load4(const float4 *p) {
+  const nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4 *>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 template <int KS, int G, int MODE, int M>
 __global__ __launch_bounds__(kBlock) void algdist_half_quad(
     int row0, int R, const int *__restrict__ rp, const int *__restrict__ col,
@@ -347,9 +356,13 @@ __global__ __launch_bounds__(kBlock) void algdist_half_quad(
       }
       float4 v[M];
 #pragma unroll
-      for (int m = 0; m < M; m++)
-        v[m] = (c[m] >= 0 && vl) ? src4[(size_t)c[m] * NV + p]
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int m = 0; m < M; m++) {
+        v[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c[m] >= 0 && vl) {
+          if (c[m] < g_hot_lim) v[m] = src4[(size_t)c[m] * NV + p];
+          else v[m] = nt_load4(&src4[(size_t)c[m] * NV + p]);
+        }
+      }
 #pragma unroll
       for (int m = 0; m < M; m++) {
         // weight = vector 0 .x of the row, held by lane 0 of the quad
@@ -1279,11 +1292,25 @@ extern "C" int hgx_alg_run(hgx_ctx *ctx, int iters) {
     const bool sample = sample_env && it + 1 < iters;
     float *xc = ctx->X[ctx->xcur].as<float>(), *xn = ctx->X[ctx->xcur ^ 1].as<float>();
     float *yc = ctx->Y[ctx->ycur].as<float>(), *yn = ctx->Y[ctx->ycur ^ 1].as<float>();
+#ifdef HGX_DEBUG_KNOBS
+    {
+      const int hn = hgx_debug_env("HGX_ALG_HOT", 0x7fffffff);
+      hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hot_lim), &hn, sizeof(int), 0,
+                             hipMemcpyHostToDevice, ctx->stream);
+    }
+#endif
     // node half: self x (scaled), gathered y (scaled)
     HGX_TRY(launch_half(ctx, MODE_FULL, 0, ctx->N, ctx->rp_n.as<int>(),
                         ctx->col_n.as<int>(), xc, yc, xn, prev, prev != nullptr,
                         cur, ctx->avg_deg_n, ctx->blk_n.as<int>(), ctx->nblk_n,
                         &ctx->long_n, sample));
+#ifdef HGX_DEBUG_KNOBS
+    {
+      const int he = hgx_debug_env("HGX_ALG_HOT_E", 0x7fffffff);
+      hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hot_lim), &he, sizeof(int), 0,
+                             hipMemcpyHostToDevice, ctx->stream);
+    }
+#endif
     // edge half: self y (scaled), gathered NEW x (raw)
     HGX_TRY(launch_half(ctx, MODE_FULL, 0, ctx->E, ctx->rp_e.as<int>(),
                         ctx->col_e.as<int>(), yc, xn, yn, prev, 0, cur,
