@@ -46,7 +46,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = ("training samples/sec + alg-dist SpMV GB/s, HOBE dim=128 at "
           "1/2/4/8 MI355X")
-PMC_TRAIN = os.path.join(ROOT, "profiles", "r02_pmc_train.json")
+PMC_TRAIN = os.path.join(ROOT, "profiles", "r02_step_pmc_train.json")
 
 
 def parse():
@@ -195,8 +195,8 @@ def main():
   records = n * args.steps * world
   value = records / elapsed
 
-  # ---- roofline of the dominant kernel: one batch step (train_fused, or
-  # K1 + K2 for the batches that do not pack) ----
+  # ---- roofline of the dominant kernel: one batch step (train_step; K1 + K2
+  # only where the step does not apply) ----
   b_rec = 224.0 * args.dim + 68.0  # SURVEY §8d algorithmic bytes / record
   per_batch_ms = dev_ms / max(batches, 1)
   batch_bytes = b_rec * (n * args.steps / max(batches, 1))
@@ -211,9 +211,9 @@ def main():
               "peak": HBM_PEAK_GBPS, "unit": "GB/s",
               "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
               "traffic_source": pmc_src,
-              "kernel": ("train_fused (one launch per batch step)" if fused_b
+              "kernel": ("train_step (one launch per batch step)" if fused_b
                          else "train_fwd_bwd+train_update (one batch step)"),
-              "batch_steps": {"train_fused": fused_b,
+              "batch_steps": {"train_step": fused_b,
                               "train_fwd_bwd+train_update": split_b},
               "per_launch_us": round(per_batch_ms * 1e3, 2),
               "algorithmic_bytes_per_launch": round(batch_bytes)}
@@ -278,7 +278,7 @@ def main():
           "sampling_s": round(c2_sample_s, 3),
           "train_records_per_s": round(n2 / c2_s, 1),
           "per_batch_us": round(ms2 * 1e3 / max(bat2, 1), 2),
-          "batch_steps": dict(zip(("train_fused", "train_fwd_bwd+train_update"),
+          "batch_steps": dict(zip(("train_step", "train_fwd_bwd+train_update"),
                                   ctx.train_path_stats()))}
 
     # ---- end to end: one real EmbedHg2vAlgDist call (embedding.py:389) ----
@@ -435,7 +435,8 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
            "sampling_records_per_s": round(n4 / hobe_sample_s, 1),
            "dim": d4, "train_records_per_s": round(n4 / t4, 1),
            "per_batch_us": round(ms4t * 1e3 / max(bat4, 1), 2),
-           "batch_steps": {"train_fused": fz4, "train_fwd_bwd+train_update": sp4},
+           "batch_steps": {"train_step": fz4, "train_fwd_bwd+train_update": sp4},
+           "restarts": ctx.train_restarts(),
            "loss": "MSE", "act": "relu"}
   if rank == 0 and world == 1 and not args.no_cpu:
     # CPU port on 1M records of the same stream, tables of the same size

@@ -16,6 +16,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "hgx.h")
 
 HGX_OK, HGX_EINVAL, HGX_EHIP, HGX_ENOMEM = 0, -1, -2, -3
 HGX_EZERODIV, HGX_ESTATE, HGX_EUNSUP, HGX_EVALUE = -4, -5, -6, -7
+HGX_ENUMERIC = -8
 LOSS_KLD, LOSS_MSE = 0, 1
 ACT_SIGMOID, ACT_RELU = 0, 1
 HOBE_NN, HOBE_EE, HOBE_NE = 0, 1, 2
@@ -78,6 +79,7 @@ SIGNATURES = {
                          _vp, _vp, _pint]),
     "hgx_train_last_stats": (_int, [_vp, _pdbl, _pi64, _pi64]),
     "hgx_train_path_stats": (_int, [_vp, _pi64, _pi64]),
+    "hgx_train_restarts": (_int, [_vp, _pi64]),
     "hgx_train_last_loss": (_int, [_vp, _pdbl]),
     "hgx_synth_powerlaw": (_int, [_i32, _i32, ctypes.c_double, ctypes.c_double,
                                   _u64, _vp, _vp, _pi64,
@@ -150,6 +152,8 @@ def _raise(rc, msg):
     raise ZeroDivisionError(msg)
   if rc == HGX_EVALUE:
     raise ValueError(msg)
+  if rc == HGX_ENUMERIC:
+    raise FloatingPointError(msg)
   raise HgxError(f"libhgx error {rc}: {msg}")
 
 
@@ -435,6 +439,12 @@ class Context:
     self._chk(lib().hgx_train_path_stats(self.h, ctypes.byref(f),
                                          ctypes.byref(sp)))
     return f.value, sp.value
+
+  def train_restarts(self):
+    """Step batches of the last train() that followed a mid-epoch flush."""
+    v = ctypes.c_int64()
+    self._chk(lib().hgx_train_restarts(self.h, ctypes.byref(v)))
+    return v.value
 
 
 class Mlp:

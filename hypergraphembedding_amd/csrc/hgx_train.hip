@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "hgx_internal.h"
@@ -47,7 +48,8 @@ constexpr int kGraphBatches = 64;  // batches per chunk buffer and per graph
 // diagnostic ablation bits (HGX_TRAIN_ABLATE, timing experiments only;
 // results are wrong when set): 1 empty K1, 2 empty K2, 4 K1 gathers hit
 // row 0, 8 K1 skips gradient stores, 16 K2 skips slot sums, 32 K2 skips
-// the table read-modify-write.
+// the table read-modify-write; train_step: 1024 shared-row gradients by
+// plain stores.
 #ifdef HGX_DEBUG_KNOBS
 __constant__ int g_tab = 0;  // ablation bits (diagnostic builds only)
 #else
@@ -92,23 +94,39 @@ struct TrainArgs {
   int lstride;  // per-batch stride of lossbuf (>= the blocks of either path)
   float lr, eps;
   int loss, act;
-  // fused path (train_fused): records packed so that every row touched by
-  // more than one slot of a batch has all its slots in ONE workgroup.
-  // Per chunk-local batch: NBF workgroups x prpb groups of R ids / codes / 3
-  // targets, valid groups per workgroup, and whether the batch packed.
-  int fused, prpb, NBF, MS;
-  int *pidx, *pcode, *pnval, *pnblk, *pfast;
+  // deferred-row step (train_step, train_place): per chunk-local batch
+  // ceil(B / prpb) workgroups x prpb groups of RW words (R slot ids / codes
+  // + kFX flush slots) and 3 targets; per-slot codes and the deferred rows'
+  // keys from train_prep; deferred entries per batch (pM), flush overflow
+  // list (pfo). gacc [3][MX][dp] fixed-point sums and shadow [3][MX][2][dp]
+  // base rows of deferred entries by batch parity (entries 0 / 1: row 0 of
+  // the node / edge table, shadow only); gp [2][NBF][2][dp] the padding
+  // row's per-workgroup gradient partials; ovf the fixed-point range flag.
+  int fused, prpb, RW, MX, Mmax;
+  int *pidx, *pbrk;
+  unsigned *pcode, *scode;
   float *ptgt;
-  float *r0;  // [2 parity][2 table][p, acc][dp]: padding-row state handed on
-  float *gp;  // [2 parity][NBF][2 table][dp]: padding-row partials per block
+  int2 *pfo;
+  long long *gacc;
+  float *shadow, *gp;
+  int *ovf;
 };
 
-// slot codes of the fused path (train_prep -> train_fused)
-constexpr unsigned kCodeMulti = 0x80000000u;  // row has >1 slot: LDS pos
-constexpr unsigned kCodeOwn = 0x40000000u;    // this slot applies the update
-constexpr int kPackB = 512;                   // max records per fused batch
-constexpr int kPackM = 1024;                  // max multi-slot rows per batch
-constexpr int kPackNBF = 64;                  // max fused workgroups per batch
+// slot codes of the deferred-row step (train_prep / train_place -> train_step)
+constexpr unsigned kSShared = 0x80000000u;  // row in several records: deferred entry m
+constexpr unsigned kSOwn = 0x40000000u;     // this slot writes the row (or its shadow)
+constexpr unsigned kSPend = 0x20000000u;    // row deferred by the previous batch: entry m'
+constexpr unsigned kSLocal = 0x10000000u;   // row in several slots of ONE record
+constexpr unsigned kSFirst = 0x08000000u;   // local: first slot in emit order (no read)
+                                            // local: bits 0..3 the owner slot
+constexpr unsigned kFEdge = 0x10000000u;    // flush slot words: edge table
+constexpr int kDefBits = 14;                // m / slot mask in bits 0..13, m' in 14..25
+constexpr unsigned kDefMask = 0xfffu;
+constexpr unsigned kSlotMask = 0x3fffu;
+constexpr int kFX = 4;                      // flush slots per record group
+constexpr int kWX = kFX + 2;                // + batch words: overflow flushes,
+                                            //   gacc entries to zero
+constexpr int kPackB = 512;                 // max records per step batch
 constexpr int kPrepB = 1366;  // max records per prepared batch: 8192 slots / R >= 6
 
 __device__ __forceinline__ bool slot_is_edge(int s, int K) {
@@ -480,364 +498,6 @@ __global__ __launch_bounds__(TB) void train_update(TrainArgs a, int cb) {
 // fixed order (thread `sub` of a column: partials sub, sub+TPC, ...; then
 // the TPC sums in order) and returns the column's (p, acc) on sub == 0.
 // col < 2L covers both tables (table = col / L, float4 column col % L).
-template <int L, int TB, int NBFM>
-struct Row0Loads {
-  static constexpr int NC = 2 * L, TPC = TB / NC, MAXPER = (NBFM + TPC - 1) / TPC;
-  float4 gv[MAXPER];
-  float4 rp, ra;  // the selected row-0 state (pending or table)
-};
-
-template <int L, int TB, int NBFM>
-__device__ __forceinline__ void row0_issue_state(const TrainArgs &a,
-                                                 const float4 *r0src, int mode,
-                                                 Row0Loads<L, TB, NBFM> &ld) {
-  using RL = Row0Loads<L, TB, NBFM>;
-  static_assert(TB % RL::NC == 0, "workgroup covers whole columns");
-  const int col = threadIdx.x % RL::NC;
-  const int tab = col / L, c = col % L;
-  // the address is selected (mode is wave-uniform), not the loaded value:
-  // two loads instead of four on the first round trip
-  const float4 *sp = mode ? r0src + (tab * 2) * L
-                          : reinterpret_cast<const float4 *>(tab ? a.etab : a.ntab);
-  const float4 *sa = mode ? r0src + (tab * 2 + 1) * L
-                          : reinterpret_cast<const float4 *>(tab ? a.eacc : a.nacc);
-  ld.rp = sp[c];
-  ld.ra = sa[c];
-}
-
-// partials [0, nmax) of gpsrc (nmax <= NBFM, the instantiation's workgroup
-// cap: MAXPER = NBFM / TPC loads per thread), issued unconditionally
-// (index clamped: a branch around a load makes the compiler wait for it at
-// the join); row0_stage masks the clamped copies (the gp buffer is zeroed at
-// hgx_train entry, so it only ever holds finite partials).
-template <int L, int TB, int NBFM>
-__device__ __forceinline__ void row0_issue_partials(int nmax, const float4 *gpsrc,
-                                                    Row0Loads<L, TB, NBFM> &ld) {
-  using RL = Row0Loads<L, TB, NBFM>;
-  const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
-  const int last = max(nmax - 1, 0);
-#pragma unroll
-  for (int u = 0; u < RL::MAXPER; u++)
-    ld.gv[u] = gpsrc[(size_t)min(sub + u * RL::TPC, last) * RL::NC + col];
-}
-
-// this thread's fixed-order partial sum of partials [0, np) -> s_red
-template <int L, int TB, int NBFM>
-__device__ __forceinline__ void row0_stage(int np, const Row0Loads<L, TB, NBFM> &ld,
-                                           float4 (*s_red)[2 * L]) {
-  using RL = Row0Loads<L, TB, NBFM>;
-  const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
-  float4 g = f4(0.f);
-#pragma unroll
-  for (int u = 0; u < RL::MAXPER; u++) {
-    const float m = (float)(sub + u * RL::TPC < np);
-    const float4 v = ld.gv[u];
-    g = g + make_float4(v.x * m, v.y * m, v.z * m, v.w * m);
-  }
-  s_red[sub][col] = g;
-}
-
-// after row0_stage: the workgroup barrier, then the column owners (sub == 0)
-// add the TPC staged sums in order and apply Adagrad (mode 1)
-// p0 / a0 arrive holding the selected state (mode ? pending : table),
-// picked right after row0_stage: that forces the state loads' wait BEFORE the
-// gathers are issued (a wait for them after the wave-uniform list-gather
-// branch would be counted conservatively and drain most gathers).
-template <int L, int TB, int NBFM>
-__device__ __forceinline__ void row0_finish(const TrainArgs &a, int mode,
-                                            float4 (*s_red)[2 * L], float4 &p0,
-                                            float4 &a0) {
-  using RL = Row0Loads<L, TB, NBFM>;
-  const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
-  __syncthreads();
-  if (sub == 0 && mode) {
-    float4 gs = f4(0.f);
-#pragma unroll
-    for (int j = 0; j < RL::TPC; j++) gs = gs + s_red[j][col];
-    adagrad4(p0, a0, gs, a.lr, a.eps);
-  }
-}
-
-// Fused batch step: K1 + K2 of one batch in ONE launch (no K1 -> K2
-// boundary, no per-slot gradient round trip through HBM).
-//  - train_prep packed the batch so that every row with several slots has
-//    them all in one workgroup; single-slot rows (most) are updated by their
-//    own group right after the backward pass, multi-slot rows by their first
-//    slot's group after an LDS exchange and a workgroup barrier, summing in
-//    sorted-slot order like train_update.
-//  - The padding row 0 (touched by nearly every record) is deferred: its
-//    per-workgroup partials go to gp[q & 1]; the NEXT fused launch (q + 1)
-//    folds them in (row0_issue/finish) before its gathers, train_row0_flush
-//    writes the final state back after the last fused batch of a run.
-// One L-lane group per record (dp == 4L), prpb = TB / L records per
-// workgroup, NBF workgroups; q = position in the run of consecutive fused
-// launches, mode = q > 0.
-template <int L, int KMAX, int MODE, int TB, int NBFM>
-__global__ __launch_bounds__(TB) void train_fused(TrainArgs a, int cb, int gb,
-                                                  int nb, int np, int q,
-                                                  int mode) {
-  constexpr int RPB = TB / L, R = 4 + 2 * KMAX, K = KMAX;
-  extern __shared__ float4 s_ms[];  // [MS][L]: gradients of multi-slot rows
-  __shared__ float4 s_z[2][RPB][L];
-  __shared__ float4 s_red[TB / (2 * L)][2 * L];
-  __shared__ float4 s_r0[2][L];
-  __shared__ float s_loss[RPB];
-  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (g_trace) ts[0] = __builtin_amdgcn_s_memrealtime();
-  const int grp = threadIdx.x / L, lane = threadIdx.x % L;
-  const int NBF = a.NBF;
-  if (g_tab & 64) mode = 0;  // ablation: no partial reads
-  // round trip 1 (kernel arguments only): the group's record ids, slot
-  // codes and targets, the workgroup's record count, the row-0 state and
-  // the np padding-row partials of the previous batch (np = its workgroup
-  // count, a kernel argument)
-  const size_t gi = ((size_t)cb * NBF + blockIdx.x) * RPB + grp;
-  const int *ri = a.pidx + gi * R;
-  const unsigned *rc = reinterpret_cast<const unsigned *>(a.pcode) + gi * R;
-  const float *yt = a.ptgt + gi * 3;
-  int row[R];
-  unsigned code[R];
-  {
-    // one id and one code load per lane (lane s of the group loads slot s),
-    // then readlanes broadcast the group's slots: 2 load instructions
-    // instead of 2R on the first round trip. L = 64: one record per wave,
-    // the ids land in scalar registers; L = 32: two records per wave.
-    static_assert(L == 32 || L == 64, "fused step geometry");
-    const int sl = lane < R ? lane : 0;
-    const int rv = ri[sl];
-    const int cv = (int)rc[sl];
-#pragma unroll
-    for (int s = 0; s < R; s++) {
-      if (L == 64) {
-        row[s] = __builtin_amdgcn_readlane(rv, s);
-        code[s] = (unsigned)__builtin_amdgcn_readlane(cv, s);
-      } else {
-        const bool hi = threadIdx.x & 32;
-        const int r0 = __builtin_amdgcn_readlane(rv, s), r1 = __builtin_amdgcn_readlane(rv, 32 + s);
-        const int c0 = __builtin_amdgcn_readlane(cv, s), c1 = __builtin_amdgcn_readlane(cv, 32 + s);
-        row[s] = hi ? r1 : r0;
-        code[s] = (unsigned)(hi ? c1 : c0);
-      }
-    }
-  }
-  // targets: at L = 64 (one record per wave) lane c < 3 loads target c and
-  // readlanes broadcast them (scalar); at L = 32 three broadcast loads
-  // measured faster than the two-record select
-  float yt0, yt1, yt2;
-  if (L == 64) {
-    const int tv = __float_as_int(yt[lane < 3 ? lane : 0]);
-    yt0 = __int_as_float(__builtin_amdgcn_readlane(tv, 0));
-    yt1 = __int_as_float(__builtin_amdgcn_readlane(tv, 1));
-    yt2 = __int_as_float(__builtin_amdgcn_readlane(tv, 2));
-  } else {
-    yt0 = yt[0];
-    yt1 = yt[1];
-    yt2 = yt[2];
-  }
-  const int nval = a.pnval[(size_t)cb * NBF + blockIdx.x];
-  if (!mode) np = 0;
-  const size_t par = (size_t)NBF * 2 * L;  // float4 per gp parity
-  Row0Loads<L, TB, NBFM> r0l;
-  row0_issue_state<L, TB, NBFM>(a, reinterpret_cast<const float4 *>(a.r0) + (q & 1) * 4 * L,
-                                mode, r0l);
-  row0_issue_partials<L, TB, NBFM>(np, reinterpret_cast<const float4 *>(a.gp) + ((q - 1) & 1) * par,
-                             r0l);
-  HGX_STAMP(ts[1]);
-  if (nval == 0) return;  // unused workgroup of this batch
-  const bool has = grp < nval;
-  // staged before the gathers: frees the partials' registers
-  row0_stage<L, TB, NBFM>(np, r0l, s_red);
-  float4 p0 = r0l.rp, a0 = r0l.ra;
-  // pin the selects here (the compiler would sink them past the gathers)
-  asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(a0.x),
-               "+v"(a0.y), "+v"(a0.z), "+v"(a0.w));
-  // round trip 2: every slot's table row and owner slots' accumulator
-  // rows. Per slot unconditional (row 0 / non-owner slots read row 0, a hot
-  // line): a load under a per-lane branch is waited for at the join, which
-  // would serialise the gathers. The neighbour-list slots 4.. are skipped by
-  // a WAVE-uniform branch when no record of the wave has a list (nn / ee
-  // records: all list slots are the padding row, whose value comes from
-  // s_r0 below): they are 20 of a record's 28 row loads, and a CU's load
-  // issue (64 B/clk) is a large part of this phase. HGX_TRAIN_ABLATE & 256
-  // disables the skip.
-  float4 Pv[R], Av[R];
-  bool lists = false;
-#pragma unroll
-  for (int s = 4; s < R; s++) lists |= row[s] != 0;
-  const bool wave_lists = (g_tab & 256) || __any(lists);
-#pragma unroll
-  for (int s = 0; s < 4; s++) {
-    // every record kind has two padding slots among the first four (ne:
-    // le, rn; nn: le, re; ee: ln, rn). At L = 64 (one record per wave, the
-    // ids are scalar) they are skipped: their value comes from s_r0 below.
-    // At L = 32 the two records of a wave may differ in kind, and the
-    // per-slot branch measured slower (7.80 -> 7.90 us per batch).
-    if (L == 64 && !(g_tab & 512) && row[s] == 0) {
-      Pv[s] = Av[s] = f4(0.f);
-      continue;
-    }
-    const bool edge = slot_is_edge(s, K);
-    const float4 *T = reinterpret_cast<const float4 *>(edge ? a.etab : a.ntab);
-    const float4 *Ac = reinterpret_cast<const float4 *>(edge ? a.eacc : a.nacc);
-    const int arow = (code[s] & kCodeOwn) ? row[s] : 0;
-    Pv[s] = T[(size_t)row[s] * L + lane];
-    Av[s] = Ac[(size_t)arow * L + lane];
-  }
-  if (wave_lists) {
-#pragma unroll
-    for (int s = 4; s < R; s++) {
-      const bool edge = slot_is_edge(s, K);
-      const float4 *T = reinterpret_cast<const float4 *>(edge ? a.etab : a.ntab);
-      const float4 *Ac = reinterpret_cast<const float4 *>(edge ? a.eacc : a.nacc);
-      const int arow = (code[s] & kCodeOwn) ? row[s] : 0;
-      Pv[s] = T[(size_t)row[s] * L + lane];
-      Av[s] = Ac[(size_t)arow * L + lane];
-    }
-  }
-  {
-    row0_finish<L, TB, NBFM>(a, mode, s_red, p0, a0);
-    const int col = threadIdx.x % (2 * L), sub = threadIdx.x / (2 * L);
-    if (sub == 0) {
-      s_r0[col / L][col % L] = p0;
-      if (blockIdx.x == 0) {
-        float4 *r0d = reinterpret_cast<float4 *>(a.r0) + ((q + 1) & 1) * 4 * L;
-        r0d[(col / L) * 2 * L + col % L] = p0;
-        r0d[((col / L) * 2 + 1) * L + col % L] = a0;
-      }
-    }
-    __syncthreads();
-  }
-  HGX_STAMP(ts[2]);
-  float4 zN = f4(0.f), zE = f4(0.f);
-  float lrec = 0.f;
-  if (has) {
-#pragma unroll
-    for (int s = 0; s < R; s++)
-      if (row[s] == 0) Pv[s] = s_r0[slot_is_edge(s, K) ? 1 : 0][lane];
-    const float inv_b = 1.0f / (float)nb;
-    const float4 &Nl = Pv[0], &El = Pv[1], &Nr = Pv[2], &Er = Pv[3];
-    float z1 = group_sum<L>(dot4(Nl, Nr)), z2 = group_sum<L>(dot4(El, Er));
-    float za[K], zb[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      za[k] = group_sum<L>(dot4(Pv[4 + k], Nl));
-      zb[k] = group_sum<L>(dot4(Pv[4 + K + k], Er));
-    }
-    const int act = MODE == 1 ? 0 : 1;
-    const int lossk = MODE == 1 ? 0 : 1;
-    const float y1 = act_f(act, z1), y2 = act_f(act, z2);
-    float sa[K], sb[K], P = 0.f, Q = 0.f;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      sa[k] = act_f(act, za[k]);
-      sb[k] = act_f(act, zb[k]);
-      P += sa[k];
-      Q += sb[k];
-    }
-    P = P / (float)K;
-    Q = Q / (float)K;
-    const float y3 = P * Q;
-    float l1, l2, l3, g1, g2, g3;
-    head_loss(lossk, y1, yt0, l1, g1);
-    head_loss(lossk, y2, yt1, l2, g2);
-    head_loss(lossk, y3, yt2, l3, g3);
-    lrec = l1 + l2 + l3;
-    HGX_STAMP(ts[3]);
-    g1 *= inv_b;
-    g2 *= inv_b;
-    g3 *= inv_b;
-    const float dz1 = g1 * act_d(act, z1, y1);
-    const float dz2 = g2 * act_d(act, z2, y2);
-    const float dP = g3 * Q / (float)K, dQ = g3 * P / (float)K;
-    auto emit = [&](int s, float4 g) {
-      if (row[s] == 0) {
-        if (slot_is_edge(s, K)) zE = zE + g;
-        else zN = zN + g;
-      } else if (code[s] & kCodeMulti) {
-        s_ms[(code[s] & 0xfffu) * L + lane] = g;
-      } else if (!(g_tab & 128)) {
-        const bool edge = slot_is_edge(s, K);
-        float4 pv = Pv[s], av = Av[s];
-        adagrad4_hw(pv, av, f4(0.f) + g, a.lr, a.eps);
-        reinterpret_cast<float4 *>(edge ? a.etab : a.ntab)[(size_t)row[s] * L + lane] = pv;
-        reinterpret_cast<float4 *>(edge ? a.eacc : a.nacc)[(size_t)row[s] * L + lane] = av;
-      }
-    };
-    float4 gln = fma4(dz1, Nr, f4(0.f)), gre = fma4(dz2, El, f4(0.f));
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      const float da = dP * act_d(act, za[k], sa[k]);
-      const float db = dQ * act_d(act, zb[k], sb[k]);
-      gln = fma4(da, Pv[4 + k], gln);
-      gre = fma4(db, Pv[4 + K + k], gre);
-      emit(4 + k, fma4(da, Nl, f4(0.f)));
-      emit(4 + K + k, fma4(db, Er, f4(0.f)));
-    }
-    emit(0, gln);
-    emit(3, gre);
-    emit(2, fma4(dz1, Nl, f4(0.f)));
-    emit(1, fma4(dz2, Er, f4(0.f)));
-    HGX_STAMP(ts[4]);
-  }
-  s_z[0][grp][lane] = zN;
-  s_z[1][grp][lane] = zE;
-  if (lane == 0) s_loss[grp] = lrec;
-  __syncthreads();
-  if (has) {
-#pragma unroll
-    for (int s = 0; s < R; s++) {
-      const unsigned cd = code[s];
-      if (row[s] != 0 && (cd & kCodeMulti) && (cd & kCodeOwn)) {
-        const int pos = cd & 0xfffu, cnt = (cd >> 12) & 0xfffu;
-        float4 g = f4(0.f);
-        for (int j = 0; j < cnt; j++) g = g + s_ms[(pos + j) * L + lane];
-        const bool edge = slot_is_edge(s, K);
-        float4 pv = Pv[s], av = Av[s];
-        adagrad4_hw(pv, av, g, a.lr, a.eps);
-        reinterpret_cast<float4 *>(edge ? a.etab : a.ntab)[(size_t)row[s] * L + lane] = pv;
-        reinterpret_cast<float4 *>(edge ? a.eacc : a.nacc)[(size_t)row[s] * L + lane] = av;
-      }
-    }
-  }
-  HGX_STAMP(ts[5]);
-  float4 *gpd = reinterpret_cast<float4 *>(a.gp) + (q & 1) * par;
-  for (int t = threadIdx.x; t < 2 * L; t += TB) {
-    const int tab = t / L, j = t % L;
-    float4 sz = f4(0.f);
-    for (int g = 0; g < RPB; g++) sz = sz + s_z[tab][g][j];
-    gpd[((size_t)blockIdx.x * 2 + tab) * L + j] = sz;
-  }
-  if (threadIdx.x == 0) {
-    float sl = 0.f;
-    for (int g = 0; g < RPB; g++) sl += s_loss[g];
-    a.lossbuf[(size_t)gb * a.lstride + blockIdx.x] = sl;
-  }
-  HGX_STAMP(ts[6]);
-  trace_put(gb, 0, 7, ts);
-}
-
-// After the last launch q of a fused run: the pending padding-row update ->
-// row 0 of both tables and accumulators.
-template <int L, int TB, int NBFM>
-__global__ __launch_bounds__(TB) void train_row0_flush(TrainArgs a, int cb, int q) {
-  __shared__ float4 s_red[TB / (2 * L)][2 * L];
-  const size_t par = (size_t)a.NBF * 2 * L;
-  Row0Loads<L, TB, NBFM> r0l;
-  row0_issue_state<L, TB, NBFM>(a, reinterpret_cast<const float4 *>(a.r0) + ((q + 1) & 1) * 4 * L,
-                                1, r0l);
-  row0_issue_partials<L, TB, NBFM>(a.NBF, reinterpret_cast<const float4 *>(a.gp) + (q & 1) * par,
-                             r0l);
-  row0_stage<L, TB, NBFM>(a.pnblk[cb], r0l, s_red);
-  float4 p0 = r0l.rp, a0 = r0l.ra;
-  row0_finish<L, TB, NBFM>(a, 1, s_red, p0, a0);
-  const int col = threadIdx.x % (2 * L), sub = threadIdx.x / (2 * L);
-  if (sub == 0) {
-    const int tab = col / L, c = col % L;
-    reinterpret_cast<float4 *>(tab ? a.etab : a.ntab)[c] = p0;
-    reinterpret_cast<float4 *>(tab ? a.eacc : a.nacc)[c] = a0;
-  }
-}
-
 // Block-wide exclusive scan of one int per thread.
 __device__ int block_exclusive_scan(int v, int *total, int *s_ws) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -859,268 +519,781 @@ __device__ int block_exclusive_scan(int v, int *total, int *s_ws) {
   return base + inc - v;
 }
 
-// Fused-path packing of one batch (tail of train_prep, same workgroup, the
-// batch's (row, slot) keys sorted in LDS).
-//  1. Records that share a non-padding row are connected; components by
-//     min-label propagation with pointer jumping (bounded; no convergence ->
-//     the batch takes the two-kernel path).
-//  2. Components are placed whole, in order of their first record, into
-//     workgroups of prpb groups with at most MS multi-slot rows' slots each
-//     (first fit in sequence; a component too large for one workgroup, or
-//     more than NBF workgroups -> two-kernel path).
-//  3. Each slot gets a code: single-slot row -> kCodeOwn (its group applies
-//     Adagrad directly); multi-slot row -> kCodeMulti | LDS position, the
-//     row's slots on consecutive positions in sorted-slot order, the first
-//     also kCodeOwn | count << 12 (it sums them in that order and applies
-//     Adagrad: the same order and arithmetic as train_update).
-// Every serial step runs on thread 0 in record / sorted order: the packing is
-// a deterministic function of the batch.
-__device__ void pack_batch(const TrainArgs &a, int cb, int nb, int V, int P,
-                           const unsigned long long *s_key, int *s_ws) {
-  __shared__ int s_lab[kPackB], s_csz[kPackB], s_cms[kPackB], s_cblk[kPackB],
-      s_cmoff[kPackB], s_grp[kPackB];
-  __shared__ int s_mrun[kPackM], s_mlen[kPackM], s_mbase[kPackM];
-  __shared__ int s_bfill[kPackNBF], s_bshort[kPackNBF];
-  __shared__ unsigned char s_short[kPackB];
-  __shared__ int s_flag[2], s_ok;
-  const int R = a.R, RPB = a.prpb, NBF = a.NBF, MS = a.MS;
-  volatile int *lab = s_lab;
-  auto rowkey = [&](int t) { return (unsigned)(s_key[t] >> 32); };
-  auto slotof = [&](int t) { return (int)(unsigned)(s_key[t] & 0xffffffffu); };
-  for (int i = threadIdx.x; i < nb; i += kTB) {
-    s_lab[i] = i;
-    s_csz[i] = 0;
-    s_cms[i] = 0;
+// ---------------------------------------------------------------------------
+// Deferred-row batch step (train_step): one launch per batch, no packing
+// constraint on which workgroup holds which record.
+//
+// Keras applies one Adagrad update per batch with the gradients of a row's
+// slots summed (hg2v_model.py:51-203 through TF's dense IndexedSlices sum).
+//  - A row with ONE slot in batch b (most rows) is updated in place by the
+//    lane group of its record, right after the backward pass.
+//  - A row with several slots in b ("deferred" row, entry m of b) cannot be
+//    summed in one place without a grid-wide barrier. Each slot adds its
+//    gradient to gacc[b % 3][m] as 2^44 fixed point with integer atomics:
+//    the sum is exact and independent of arrival order, so the step stays
+//    bitwise reproducible. The row's owner slot writes the row's state as b
+//    read it, (p, a), to shadow[b % 3][m]. The update itself is applied by
+//    launch b + 1: every slot of b + 1 that touches the row ("pending" slot,
+//    code kSPend, entry m') reads shadow + gacc and folds the Adagrad step
+//    of b in registers (all readers compute the same bits); a deferred row of
+//    b that b + 1 does not touch is written back by a "flush slot" of b + 1.
+//  - The padding row 0 of both tables (nearly every record) goes the same
+//    way without atomics: each workgroup stores its fixed-order LDS partial
+//    (plain stores: an atomic add's completion at the kernel tail measured
+//    0.7 us), every workgroup of b + 1 sums the partials in a fixed order and
+//    folds the step; workgroup 0 keeps the base in shadow entry 0 / 1.
+// Nothing of batch b + 1 reads a location batch b + 1 writes: the table rows
+// it writes are single-slot rows of b + 1 (read only by their own group) or
+// flushed rows (not read by b + 1); shadow and gacc are triple-buffered by
+// batch parity, gp double-buffered. train_flush applies the last batch's
+// deferred rows at the end of every epoch. A parity's gacc entries are zeroed
+// two launches after their use (the count rides in the record words).
+// ---------------------------------------------------------------------------
+
+// fixed point of the deferred-row gradient sums: 2^44 units, |one added
+// value| < kFixLimit; at most 2^13 adds per entry and batch keep the sum
+// below 2^63. A value outside the range (a diverged run, or NaN) raises the
+// step's overflow flag and hgx_train fails with HGX_ENUMERIC.
+constexpr double kFixScale = 17592186044416.0;  // 2^44
+constexpr double kFixInv = 1.0 / 17592186044416.0;
+constexpr float kFixLimit = 32.f;
+
+__device__ __forceinline__ unsigned long long to_fix(float v) {
+  return (unsigned long long)(long long)((double)v * kFixScale);
+}
+__device__ __forceinline__ float from_fix(long long v) {
+  return (float)((double)v * kFixInv);
+}
+// v -> gacc entry (4 consecutive int64 of this lane), fixed point
+__device__ __forceinline__ void fix_add4(long long *dst, float4 v, int &bad) {
+  bad |= !(fabsf(v.x) < kFixLimit) | !(fabsf(v.y) < kFixLimit) |
+         !(fabsf(v.z) < kFixLimit) | !(fabsf(v.w) < kFixLimit);
+  unsigned long long *d = reinterpret_cast<unsigned long long *>(dst);
+  atomicAdd(d + 0, to_fix(v.x));
+  atomicAdd(d + 1, to_fix(v.y));
+  atomicAdd(d + 2, to_fix(v.z));
+  atomicAdd(d + 3, to_fix(v.w));
+}
+// the deferred Adagrad step of the previous batch: (p, a) += sum
+__device__ __forceinline__ void fold4(float4 &p, float4 &ac, longlong2 g01,
+                                      longlong2 g23, float lr, float eps) {
+  const float4 g = make_float4(from_fix(g01.x), from_fix(g01.y), from_fix(g23.x),
+                               from_fix(g23.y));
+  adagrad4_hw(p, ac, g, lr, eps);
+}
+
+// views of the deferred-row buffers (L lanes x float4 per row: dp = 4L)
+template <int L>
+__device__ __forceinline__ float4 *sh_row(const TrainArgs &a, int par, int m, int which) {
+  return reinterpret_cast<float4 *>(a.shadow) + (((size_t)par * a.MX + m) * 2 + which) * L;
+}
+template <int L>
+__device__ __forceinline__ longlong2 *gacc_row(const TrainArgs &a, int par, int m) {
+  return reinterpret_cast<longlong2 *>(a.gacc) + ((size_t)par * a.MX + m) * (2 * L);
+}
+template <int L>
+__device__ __forceinline__ float4 *tab_row(const TrainArgs &a, bool edge, int acc, int row) {
+  float *t = acc ? (edge ? a.eacc : a.nacc) : (edge ? a.etab : a.ntab);
+  return reinterpret_cast<float4 *>(t) + (size_t)row * L;
+}
+
+// one flush entry: the deferred row (table bit 30 | row) of entry m of the
+// previous batch folded and written back
+template <int L>
+__device__ __forceinline__ void flush_row(const TrainArgs &a, int par, int key, int m,
+                                          int lane) {
+  const bool edge = key >> 30;
+  const int row = key & 0x3fffffff;
+  float4 p = sh_row<L>(a, par, m, 0)[lane], ac = sh_row<L>(a, par, m, 1)[lane];
+  const longlong2 *g = gacc_row<L>(a, par, m);
+  fold4(p, ac, g[2 * lane], g[2 * lane + 1], a.lr, a.eps);
+  tab_row<L>(a, edge, 0, row)[lane] = p;
+  tab_row<L>(a, edge, 1, row)[lane] = ac;
+}
+
+// The padding row's partials of the previous batch (np workgroups, at most
+// NBFM: MAXPER = NBFM / TPC loads per thread, index clamped, masked in
+// row0_stage) and its base (shadow of the previous batch, or the table for
+// the first batch of an epoch), issued on the first round trip.
+template <int L, int TB, int NBFM>
+struct Row0Loads {
+  static constexpr int NC = 2 * L, TPC = TB / NC, MAXPER = (NBFM + TPC - 1) / TPC;
+  float4 gv[MAXPER];
+  float4 rp, ra;
+};
+template <int L, int TB, int NBFM>
+__device__ __forceinline__ void row0_issue(const TrainArgs &a, int q, int np,
+                                           Row0Loads<L, TB, NBFM> &ld) {
+  using RL = Row0Loads<L, TB, NBFM>;
+  static_assert(TB % RL::NC == 0, "workgroup covers whole columns");
+  const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
+  const int tab = col / L, c = col % L, ppar = (q + 2) % 3;
+  // the address is selected (q is uniform), not the loaded value
+  ld.rp = (q ? sh_row<L>(a, ppar, tab, 0) : tab_row<L>(a, tab, 0, 0))[c];
+  ld.ra = (q ? sh_row<L>(a, ppar, tab, 1) : tab_row<L>(a, tab, 1, 0))[c];
+  const float4 *gp = reinterpret_cast<const float4 *>(a.gp) +
+                     (size_t)((q + 1) & 1) * NBFM * RL::NC;
+  const int last = max(np - 1, 0);
+#pragma unroll
+  for (int u = 0; u < RL::MAXPER; u++)
+    ld.gv[u] = gp[(size_t)min(sub + u * RL::TPC, last) * RL::NC + col];
+}
+// this thread's fixed-order partial sum of partials [0, np) -> s_red
+template <int L, int TB, int NBFM>
+__device__ __forceinline__ void row0_stage(int np, const Row0Loads<L, TB, NBFM> &ld,
+                                           float4 (*s_red)[2 * L]) {
+  using RL = Row0Loads<L, TB, NBFM>;
+  const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
+  float4 g = f4(0.f);
+#pragma unroll
+  for (int u = 0; u < RL::MAXPER; u++) {
+    const float m = (float)(sub + u * RL::TPC < np);
+    const float4 v = ld.gv[u];
+    g = g + make_float4(v.x * m, v.y * m, v.z * m, v.w * m);
   }
-  if (threadIdx.x == 0) {
-    s_flag[0] = s_flag[1] = 0;
-    s_ok = nb <= kPackB;
+  s_red[sub][col] = g;
+}
+// after a workgroup barrier: column owners (sub == 0) add the TPC staged sums
+// in order and apply the previous batch's row-0 step (zero gradient for the
+// first batch of an epoch: an identity)
+template <int L, int TB, int NBFM>
+__device__ __forceinline__ void row0_finish(const TrainArgs &a, float4 (*s_red)[2 * L],
+                                            float4 &p0, float4 &a0) {
+  using RL = Row0Loads<L, TB, NBFM>;
+  const int col = threadIdx.x % RL::NC;
+  float4 gs = f4(0.f);
+#pragma unroll
+  for (int j = 0; j < RL::TPC; j++) gs = gs + s_red[j][col];
+  adagrad4_hw(p0, a0, gs, a.lr, a.eps);
+}
+
+// One launch = one batch. q = the batch's index in the epoch (parities
+// q % 3 and q & 1). One L-lane group per record (dp == 4L), RPB = TB / L
+// records per workgroup, ceil(B / RPB) <= NBFM workgroups; records placed by
+// train_place, those without neighbour lists first (whole waves skip the list
+// gathers).
+template <int L, int KMAX, int MODE, int TB, int NBFM>
+__global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, int nb, int q) {
+  constexpr int RPB = TB / L, R = 4 + 2 * KMAX, K = KMAX, NC = 2 * L;
+  static_assert(L == 32 || L == 64, "step geometry");
+  static_assert(R + kWX <= 32, "slot and batch words fit the first 32 lanes");
+  __shared__ float4 s_z[2][RPB][L];
+  __shared__ float4 s_gl[RPB][R][L];  // gradients of local (one-record) rows
+  __shared__ float4 s_red[TB / NC][NC];
+  __shared__ float4 s_r0[2][L];
+  __shared__ float s_loss[RPB];
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (g_trace) ts[0] = __builtin_amdgcn_s_memrealtime();
+  const int grp = threadIdx.x / L, lane = threadIdx.x % L;
+  const int NBF = gridDim.x, RW = a.RW;
+  const int par = q % 3, ppar = (q + 2) % 3, zpar = (q + 1) % 3;
+  // round trip 1 (kernel arguments only): record ids and slot codes (one
+  // load per lane, readlane broadcast), flush slots, the batch words,
+  // targets, the row-0 base and the previous batch's row-0 partials
+  const size_t gi = ((size_t)cb * NBF + blockIdx.x) * RPB + grp;
+  const int *ri = a.pidx + gi * RW;
+  const unsigned *rc = a.pcode + gi * RW;
+  const float *yt = a.ptgt + gi * 3;
+  int row[R], frow[kFX];
+  unsigned code[R], fcode[kFX];
+  int nfo, zc;  // batch words: overflow flushes, gacc entries to zero
+  // every round-trip-1 load is issued before the first use of any of them
+  // (the readlane broadcasts below wait for the id words)
+  const int sl = lane < RW ? lane : 0;
+  const int rv = ri[sl];
+  const int cv = (int)rc[sl];
+  const int tv = __float_as_int(yt[L == 64 ? (lane < 3 ? lane : 0) : 0]);
+  float yt1 = 0.f, yt2 = 0.f;
+  if (L == 32) {
+    yt1 = yt[1];
+    yt2 = yt[2];
+  }
+  // the previous launch was a full batch: its NBF workgroups all stored
+  // (none for the first batch of an epoch: row 0 from the table)
+  const int np = q ? NBF : 0;
+  Row0Loads<L, TB, NBFM> r0l;
+  row0_issue<L, TB, NBFM>(a, q, np, r0l);
+  {
+#pragma unroll
+    for (int s = 0; s < R + kFX; s++) {
+      int r, c;
+      if (L == 64) {
+        r = __builtin_amdgcn_readlane(rv, s);
+        c = __builtin_amdgcn_readlane(cv, s);
+      } else {
+        const bool hi = threadIdx.x & 32;
+        const int r0 = __builtin_amdgcn_readlane(rv, s), r1 = __builtin_amdgcn_readlane(rv, 32 + s);
+        const int c0 = __builtin_amdgcn_readlane(cv, s), c1 = __builtin_amdgcn_readlane(cv, 32 + s);
+        r = hi ? r1 : r0;
+        c = hi ? c1 : c0;
+      }
+      if (s < R) {
+        row[s] = r;
+        code[s] = (unsigned)c;
+      } else {
+        frow[s - R] = r;
+        fcode[s - R] = (unsigned)c;
+      }
+    }
+    // the same in every group of the batch: lane R + kFX + i of the low half
+    nfo = __builtin_amdgcn_readlane(rv, R + kFX);
+    zc = __builtin_amdgcn_readlane(rv, R + kFX + 1);
+  }
+  float yt0 = __int_as_float(tv);
+  if (L == 64) {
+    // lane c < 3 loaded target c: readlanes broadcast them (scalar)
+    yt0 = __int_as_float(__builtin_amdgcn_readlane(tv, 0));
+    yt1 = __int_as_float(__builtin_amdgcn_readlane(tv, 1));
+    yt2 = __int_as_float(__builtin_amdgcn_readlane(tv, 2));
+  }
+  HGX_STAMP(ts[1]);
+  // records were dealt round robin over the workgroups (train_place)
+  const int nval = min(max(nb - (int)blockIdx.x + NBF - 1, 0) / NBF, RPB);
+  const bool has = grp < nval;
+  const int col = threadIdx.x % NC, sub = threadIdx.x / NC, tab0 = col / L, c0 = col % L;
+  int bad = 0;
+  if (nval > 0) {
+    // staged before the gathers: frees the partials' registers (and waits
+    // for round trip 1 before the branchy gather issue)
+    row0_stage<L, TB, NBFM>(np, r0l, s_red);
+    float4 p0 = r0l.rp, a0 = r0l.ra;
+    asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(a0.x),
+                 "+v"(a0.y), "+v"(a0.z), "+v"(a0.w));
+    // round trip 2: every slot's table row and the accumulator row where
+    // this slot owns the row's update (else the hot row 0; a pending slot's
+    // rows are replaced by the previous batch's shadow below). List slots
+    // are skipped by a WAVE-uniform branch when no record of the wave has a
+    // list.
+    float4 Pv[R], Av[R];
+    bool lists = false;
+#pragma unroll
+    for (int s = 4; s < R; s++) lists |= row[s] != 0;
+    const bool wave_lists = __any(lists);
+    // (table rows only: a per-lane select between the table and the shadow
+    // as the load base made the gathers 64-bit per-lane addresses and cost
+    // 0.6 us per batch)
+    auto gather = [&](int s) {
+      const bool edge = slot_is_edge(s, K);
+      const float4 *T = reinterpret_cast<const float4 *>(edge ? a.etab : a.ntab);
+      const float4 *Ac = reinterpret_cast<const float4 *>(edge ? a.eacc : a.nacc);
+      const int arow = (code[s] & kSOwn) ? row[s] : 0;
+      Pv[s] = T[(size_t)row[s] * L + lane];
+      Av[s] = Ac[(size_t)arow * L + lane];
+    };
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      // at L = 64 (one record per wave, scalar ids) the two padding slots of
+      // the first four are skipped: their value comes from s_r0 below
+      if (L == 64 && row[s] == 0) {
+        Pv[s] = Av[s] = f4(0.f);
+        continue;
+      }
+      gather(s);
+    }
+    if (wave_lists) {
+#pragma unroll
+      for (int s = 4; s < R; s++) gather(s);
+    }
+    // flush slot 0 (one deferred row per group in the common case) rides on
+    // the same round trip
+    // (no default values: a conditional assignment over a default makes the
+    // compiler copy the loaded registers at the join, i.e. wait for them and
+    // drain every gather before the barrier)
+    float4 fp, fa;
+    longlong2 fga, fgb;
+    if (__any(frow[0] != 0)) {
+      const int mf = (fcode[0] >> kDefBits) & kDefMask;
+      fp = sh_row<L>(a, ppar, mf, 0)[lane];
+      fa = sh_row<L>(a, ppar, mf, 1)[lane];
+      const longlong2 *g = gacc_row<L>(a, ppar, mf);
+      fga = g[2 * lane];
+      fgb = g[2 * lane + 1];
+    }
+    __syncthreads();  // s_red
+    if (sub == 0) {
+      row0_finish<L, TB, NBFM>(a, s_red, p0, a0);
+      s_r0[tab0][c0] = p0;
+      if (blockIdx.x == 0) {
+        sh_row<L>(a, par, tab0, 0)[c0] = p0;
+        sh_row<L>(a, par, tab0, 1)[c0] = a0;
+      }
+    }
+    __syncthreads();  // s_r0
+    HGX_STAMP(ts[2]);
+    // flush slot 0: folded and written back now (its registers are free
+    // for the forward pass; nothing of this batch reads the row)
+    if (has && frow[0] != 0) {
+      fold4(fp, fa, fga, fgb, a.lr, a.eps);
+      const bool fe = fcode[0] & kFEdge;
+      tab_row<L>(a, fe, 0, frow[0])[lane] = fp;
+      tab_row<L>(a, fe, 1, frow[0])[lane] = fa;
+    }
+    // pending slots (rows deferred by the previous batch): base row from the
+    // previous batch's shadow, folded with its gacc sum, written to every
+    // slot of the record that names the same entry. train_place guarantees
+    // one such entry per record (a batch where some record names two runs
+    // after a train_flush of the previous batch instead, without pending
+    // slots): one pass, its entry picked by v_cndmask (no dynamic register
+    // index), normally not taken.
+    unsigned pm = 0;
+#pragma unroll
+    for (int s = 0; s < R; s++)
+      if (code[s] & kSPend) pm |= 1u << s;
+    if (!has) pm = 0;
+    if (__any(pm != 0)) {
+      const int ps = pm ? __builtin_ctz(pm) : 0;
+      unsigned cd = 0;
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (s == ps) cd = code[s];
+      const unsigned mp = (cd >> kDefBits) & kDefMask;
+      const longlong2 *g = gacc_row<L>(a, ppar, mp);
+      const longlong2 ga = g[2 * lane], gb2 = g[2 * lane + 1];
+      float4 pp = sh_row<L>(a, ppar, mp, 0)[lane], aa = sh_row<L>(a, ppar, mp, 1)[lane];
+      // the record's slots naming the same entry (a mask: the write-back
+      // below is one bit test per slot)
+      unsigned wm = 0;
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (((code[s] >> kDefBits) & kDefMask) == mp) wm |= 1u << s;
+      wm &= pm;
+      fold4(pp, aa, ga, gb2, a.lr, a.eps);
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if ((wm >> s) & 1u) {
+          Pv[s] = pp;
+          Av[s] = aa;
+        }
+    }
+    float4 zN = f4(0.f), zE = f4(0.f);
+    float lrec = 0.f;
+    if (has) {
+#pragma unroll
+      for (int s = 0; s < R; s++)
+        if (row[s] == 0) Pv[s] = s_r0[slot_is_edge(s, K) ? 1 : 0][lane];
+      const float inv_b = 1.0f / (float)nb;
+      const float4 &Nl = Pv[0], &El = Pv[1], &Nr = Pv[2], &Er = Pv[3];
+      float z1 = group_sum<L>(dot4(Nl, Nr)), z2 = group_sum<L>(dot4(El, Er));
+      float za[K], zb[K];
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        za[k] = group_sum<L>(dot4(Pv[4 + k], Nl));
+        zb[k] = group_sum<L>(dot4(Pv[4 + K + k], Er));
+      }
+      const int act = MODE == 1 ? 0 : 1;
+      const int lossk = MODE == 1 ? 0 : 1;
+      const float y1 = act_f(act, z1), y2 = act_f(act, z2);
+      float sa[K], sb[K], P = 0.f, Q = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        sa[k] = act_f(act, za[k]);
+        sb[k] = act_f(act, zb[k]);
+        P += sa[k];
+        Q += sb[k];
+      }
+      P = P / (float)K;
+      Q = Q / (float)K;
+      const float y3 = P * Q;
+      float l1, l2, l3, g1, g2, g3;
+      head_loss(lossk, y1, yt0, l1, g1);
+      head_loss(lossk, y2, yt1, l2, g2);
+      head_loss(lossk, y3, yt2, l3, g3);
+      lrec = l1 + l2 + l3;
+      HGX_STAMP(ts[3]);
+      g1 *= inv_b;
+      g2 *= inv_b;
+      g3 *= inv_b;
+      const float dz1 = g1 * act_d(act, z1, y1);
+      const float dz2 = g2 * act_d(act, z2, y2);
+      const float dP = g3 * Q / (float)K, dQ = g3 * P / (float)K;
+      auto emit = [&](int s, float4 g) {
+        const unsigned cd = code[s];
+        const bool edge = slot_is_edge(s, K);
+        if (row[s] == 0) {
+          if (edge) zE = zE + g;
+          else zN = zN + g;
+        } else if (cd & kSLocal) {
+          // one record's slots of a row, summed in emit order in LDS (the
+          // wave's own accesses, in order); the last one (owner) updates
+          float4 *acc = &s_gl[grp][cd & 15u][lane];
+          if (cd & kSOwn) {
+            float4 pv = Pv[s], av = Av[s];
+            adagrad4_hw(pv, av, *acc + g, a.lr, a.eps);
+            tab_row<L>(a, edge, 0, row[s])[lane] = pv;
+            tab_row<L>(a, edge, 1, row[s])[lane] = av;
+          } else {
+            *acc = (cd & kSFirst) ? g : *acc + g;
+          }
+        } else if (cd & kSShared) {
+          const int m = cd & kDefMask;
+          if (g_tab & 1024)  // (debug ablation: plain stores, wrong sums)
+            reinterpret_cast<float4 *>(gacc_row<L>(a, par, m))[lane] = g;
+          else
+            fix_add4(reinterpret_cast<long long *>(gacc_row<L>(a, par, m) + 2 * lane), g, bad);
+          if (cd & kSOwn) {
+            sh_row<L>(a, par, m, 0)[lane] = Pv[s];
+            sh_row<L>(a, par, m, 1)[lane] = Av[s];
+          }
+        } else {
+          float4 pv = Pv[s], av = Av[s];
+          adagrad4_hw(pv, av, g, a.lr, a.eps);
+          tab_row<L>(a, edge, 0, row[s])[lane] = pv;
+          tab_row<L>(a, edge, 1, row[s])[lane] = av;
+        }
+      };
+      float4 gln = fma4(dz1, Nr, f4(0.f)), gre = fma4(dz2, El, f4(0.f));
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const float da = dP * act_d(act, za[k], sa[k]);
+        const float db = dQ * act_d(act, zb[k], sb[k]);
+        gln = fma4(da, Pv[4 + k], gln);
+        gre = fma4(db, Pv[4 + K + k], gre);
+        emit(4 + k, fma4(da, Nl, f4(0.f)));
+        emit(4 + K + k, fma4(db, Er, f4(0.f)));
+      }
+      emit(0, gln);
+      emit(3, gre);
+      emit(2, fma4(dz1, Nl, f4(0.f)));
+      emit(1, fma4(dz2, Er, f4(0.f)));
+      HGX_STAMP(ts[4]);
+    }
+    s_z[0][grp][lane] = zN;
+    s_z[1][grp][lane] = zE;
+    if (lane == 0) s_loss[grp] = lrec;
+    __syncthreads();
+    // this batch's row-0 partial: the workgroup's fixed-order sum
+    if (threadIdx.x < NC) {
+      float4 sz = f4(0.f);
+      for (int g = 0; g < RPB; g++) sz = sz + s_z[tab0][g][c0];
+      reinterpret_cast<float4 *>(a.gp)[((size_t)(q & 1) * NBFM + blockIdx.x) * NC + col] = sz;
+    }
+    if (threadIdx.x == 0) {
+      float sl = 0.f;
+      for (int g = 0; g < RPB; g++) sl += s_loss[g];
+      a.lossbuf[(size_t)gb * a.lstride + blockIdx.x] = sl;
+    }
+    // flush slots 1.. (more deferred rows than records in the batch)
+    bool more = false;
+#pragma unroll
+    for (int f = 1; f < kFX; f++) more |= frow[f] != 0;
+    if (__any(more)) {
+#pragma unroll
+      for (int f = 1; f < kFX; f++)
+        if (frow[f] != 0)
+          flush_row<L>(a, ppar, (fcode[f] & kFEdge ? 1 << 30 : 0) | frow[f],
+                       (fcode[f] >> kDefBits) & kDefMask, lane);
+    }
+  }
+  HGX_STAMP(ts[5]);
+  // flush overflow list (rare: more deferred rows than kFX per record)
+  for (int e = blockIdx.x * RPB + grp; e < nfo; e += NBF * RPB) {
+    const int2 en = a.pfo[(size_t)cb * a.Mmax + e];
+    flush_row<L>(a, ppar, en.x, en.y, lane);
+  }
+  // zero the gacc parity the next batch adds into (its deferred entries
+  // [2, 2 + zc) were used two batches ago)
+  {
+    longlong2 *z = gacc_row<L>(a, zpar, 2);
+    const int tot = zc * 2 * L;
+    for (int i = blockIdx.x * TB + threadIdx.x; i < tot; i += NBF * TB)
+      z[i] = make_longlong2(0, 0);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(a.ovf, 1);
+  HGX_STAMP(ts[6]);
+  trace_put(gb, 0, 7, ts);
+}
+
+// End of an epoch: the last batch's deferred rows folded into the tables
+// (row 0 of both tables from its np partials, its shared rows from gacc;
+// keys from train_prep), and every gacc entry still in use zeroed (the last
+// batch's and the one before it, Ml and Mp entries). One L-lane group per
+// entry.
+template <int L, int NBFM, int TPC>
+__global__ __launch_bounds__(256) void train_flush(TrainArgs a, const int *keys,
+                                                   const int *Ml, const int *Mp,
+                                                   int q, int np) {
+  constexpr int GPB = 256 / L;
+  const int grp = threadIdx.x / L, lane = threadIdx.x % L;
+  const int par = q % 3, opar = (q + 2) % 3;
+  const int M = 2 + *Ml, zc = Mp ? *Mp : 0;
+  for (int e = blockIdx.x * GPB + grp; e < M; e += gridDim.x * GPB) {
+    if (e < 2) {  // row 0: the partials summed in train_step's order
+      const float4 *gp = reinterpret_cast<const float4 *>(a.gp) +
+                         (size_t)(q & 1) * NBFM * 2 * L + e * L;
+      float4 g = f4(0.f);
+      for (int sub = 0; sub < TPC; sub++) {
+        float4 gs = f4(0.f);
+        for (int w = sub; w < np; w += TPC) gs = gs + gp[(size_t)w * 2 * L + lane];
+        g = g + gs;
+      }
+      float4 p = sh_row<L>(a, par, e, 0)[lane], ac = sh_row<L>(a, par, e, 1)[lane];
+      adagrad4_hw(p, ac, g, a.lr, a.eps);
+      tab_row<L>(a, e, 0, 0)[lane] = p;
+      tab_row<L>(a, e, 1, 0)[lane] = ac;
+      sh_row<L>(a, par, e, 0)[lane] = p;
+      sh_row<L>(a, par, e, 1)[lane] = ac;
+      continue;
+    }
+    flush_row<L>(a, par, keys[e - 2], e, lane);
+    longlong2 *g = gacc_row<L>(a, par, e);
+    g[2 * lane] = g[2 * lane + 1] = make_longlong2(0, 0);
+  }
+  // a step launched after this flush (mid-epoch, q + 1) folds row 0 from
+  // shadow entry 0 / 1 and the np partials of parity q & 1: the folded state
+  // and zero partials make that fold the identity (workgroup 0 computed row
+  // 0 above, groups 0 and 1)
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    float4 *gpz = reinterpret_cast<float4 *>(a.gp) + (size_t)(q & 1) * NBFM * 2 * L;
+    for (int i = threadIdx.x; i < NBFM * 2 * L; i += 256) gpz[i] = f4(0.f);
+  }
+  longlong2 *z = gacc_row<L>(a, opar, 2);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < zc * 2 * L; i += gridDim.x * 256)
+    z[i] = make_longlong2(0, 0);
+}
+
+// Slot codes of one batch (tail of train_prep, the batch's (row, slot) keys
+// sorted in LDS). Per run of equal rows:
+//  - one slot: kSOwn (in-place update by its group);
+//  - several slots of ONE record: kSLocal; its group sums the slots'
+//    gradients in LDS in emit order, the last slot in that order owns the
+//    update (no deferral, no atomics);
+//  - slots in several records: deferred entry m = 2 + its rank among the
+//    batch's deferred rows (sorted key order), kSShared, the first slot owns
+//    the shadow write.
+// Writes per-slot codes (batch slot order), the deferred rows' keys
+// (ascending) and their count. u0 = the unique-run index of this thread's
+// first sorted position.
+// position of slot s in train_step's emit order: 4 + k, 4 + K + k for
+// k = 0..K-1, then 0, 3, 2, 1
+__device__ __forceinline__ int emit_pos(int s, int K) {
+  if (s >= 4 + K) return 2 * (s - 4 - K) + 1;
+  if (s >= 4) return 2 * (s - 4);
+  return 2 * K + (s == 0 ? 0 : s == 3 ? 1 : s == 2 ? 2 : 3);
+}
+
+__device__ void defer_codes(const TrainArgs &a, int cb, int V, int P, int u0,
+                            const unsigned long long *s_key, int *s_ws, int *s_runm,
+                            int *skey, int *sM) {
+  const int per = P / kTB, t0 = threadIdx.x * per, t1 = min(t0 + per, V);
+  const int R = a.R;
+  constexpr int kDefer = 1 << 30;  // run class: deferred (m assigned below)
+  auto k32 = [&](int t) { return (unsigned)(s_key[t] >> 32); };
+  auto slot = [&](int t) { return (int)(unsigned)(s_key[t] & 0xffffffffu); };
+  auto starts = [&](int t) { return t == 0 || k32(t - 1) != k32(t); };
+  // classify the runs starting in this thread's chunk: 0 single, a slot mask
+  // (local), or kDefer
+  int ns = 0;
+  int u = u0;
+  for (int t = t0; t < t1; t++) {
+    if (!starts(t)) continue;
+    int e = t + 1;
+    while (e < V && k32(e) == k32(t)) e++;
+    int cls = 0;
+    if (e - t > 1) {
+      if (slot(t) / R == slot(e - 1) / R) {
+        cls = 1;  // local
+      } else {
+        cls = kDefer;
+        ns++;
+      }
+    }
+    s_runm[u++] = cls;
+  }
+  int S = 0;
+  int m = block_exclusive_scan(ns, &S, s_ws);
+  int *keys = skey + (size_t)cb * a.Mmax;
+  u = u0;
+  for (int t = t0; t < t1; t++) {
+    if (!starts(t)) continue;
+    if (s_runm[u] == kDefer) {
+      s_runm[u] = kDefer | (2 + m);
+      keys[m++] = (int)k32(t);
+    }
+    u++;
   }
   __syncthreads();
-  if (!s_ok) {
-    if (threadIdx.x == 0) a.pfast[cb] = 0;
-    return;
-  }
-  int conv = 0;
-  for (int it = 0; it < 64; it++) {
-    for (int t = 1 + threadIdx.x; t < V; t += kTB) {
-      if (rowkey(t) == rowkey(t - 1)) {
-        const int ra = slotof(t - 1) / R, rb = slotof(t) / R;
-        const int la = lab[ra], lb = lab[rb];
-        if (la != lb) {
-          const int m = min(la, lb);
-          atomicMin(&s_lab[ra], m);
-          atomicMin(&s_lab[rb], m);
-          s_flag[it & 1] = 1;
-        }
+  unsigned *sc = a.scode + (size_t)cb * a.SB;
+  u = u0;
+  for (int t = t0; t < t1; t++) {
+    const bool st = starts(t);
+    u += st;
+    const int cls = s_runm[u - 1];
+    unsigned code = kSOwn;
+    if (cls & kDefer) {
+      code = kSShared | (st ? kSOwn : 0u) | (unsigned)(cls & (kDefer - 1));
+    } else if (cls) {
+      // local: the run's slots in train_step's emit order; the last owns the
+      // update, the first writes the LDS sum, bits 0..3 = the owner's slot
+      int rs = t;  // the run start
+      while (rs > 0 && k32(rs - 1) == k32(t)) rs--;
+      int re = t + 1;
+      while (re < V && k32(re) == k32(t)) re++;
+      const int me = emit_pos(slot(t) % R, a.K);
+      int first = 1, last = 1, own = slot(t) % R;
+      for (int j = rs; j < re; j++) {
+        const int e2 = emit_pos(slot(j) % R, a.K);
+        first &= e2 >= me;
+        last &= e2 <= me;
+        if (e2 > emit_pos(own, a.K)) own = slot(j) % R;
       }
+      code = kSLocal | (last ? kSOwn : 0u) | (first ? kSFirst : 0u) | (unsigned)own;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) s_flag[(it + 1) & 1] = 0;
-    for (int i = threadIdx.x; i < nb; i += kTB) {
-      const int l = lab[i];
-      const int ll = lab[l];
-      if (ll < l) atomicMin(&s_lab[i], ll);
-    }
-    __syncthreads();
-    if (!s_flag[it & 1]) {
-      conv = 1;
-      break;
-    }
+    sc[slot(t)] = code;
   }
-  // component sizes and multi-slot counts
-  for (int i = threadIdx.x; i < nb; i += kTB) atomicAdd(&s_csz[lab[i]], 1);
-  const int per = P / kTB, t0 = threadIdx.x * per;
-  int nm = 0;
-  for (int t = t0; t < t0 + per && t < V; t++) {
-    const bool prev = t > 0 && rowkey(t) == rowkey(t - 1);
-    const bool next = t + 1 < V && rowkey(t + 1) == rowkey(t);
-    if (prev || next) atomicAdd(&s_cms[lab[slotof(t) / R]], 1);
-    if (!prev && next) nm++;
+  if (threadIdx.x == 0) sM[cb] = S;
+}
+
+__device__ __forceinline__ int bsearch_lds(const int *v, int n, int key) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (v[mid] < key) lo = mid + 1;
+    else hi = mid;
   }
-  int M = 0;
-  int m0 = block_exclusive_scan(nm, &M, s_ws);
-  if (M <= kPackM) {
-    for (int t = t0; t < t0 + per && t < V; t++) {
-      const bool prev = t > 0 && rowkey(t) == rowkey(t - 1);
-      const bool next = t + 1 < V && rowkey(t + 1) == rowkey(t);
-      if (!prev && next) {
-        int c = 2;
-        while (t + c < V && rowkey(t + c) == rowkey(t)) c++;
-        s_mrun[m0] = t;
-        s_mlen[m0] = c;
-        m0++;
-      }
-    }
+  return lo < n && v[lo] == key ? lo : -1;
+}
+
+// Record placement of one batch for train_step (one workgroup per batch of
+// the chunk, after train_prep): records without neighbour lists first
+// (stable; position p to workgroup p % NBF), RW words per group (R slot ids / codes, kFX flush slots, the
+// batch words: overflow flushes and the gacc entries train_step zeroes,
+// i.e. the deferred rows of the batch two before this one). Slot
+// codes get kSPend | m' << 12 where the row is deferred entry m' of the
+// previous batch (that batch's keys: skey_cur[cb - 1], or the previous
+// chunk's last batch). The previous batch's deferred rows this batch does not
+// touch become flush slots (the group of record position f % nb, slot f / nb), past kFX * nb the
+// overflow list.
+__global__ __launch_bounds__(kTB) void train_place(TrainArgs a, int nbc, int CB,
+                                                   const int *skey_cur, const int *sM_cur,
+                                                   const int *skey_pc, const int *sM_pc,
+                                                   int has_prev) {
+  extern __shared__ int s_dyn[];
+  __shared__ int s_pos[kPackB];
+  __shared__ int s_ws[kTB / 64];
+  const int cb = blockIdx.x;
+  if (cb >= nbc) return;
+  const int nb = a.bmeta[cb].x;
+  const int R = a.R, K = a.K, RW = a.RW, RPB = a.prpb, SB = a.SB;
+  const int G = (a.B + RPB - 1) / RPB * RPB;
+  const int *prev = nullptr;
+  int Mp = 0, Mpp = 0;  // deferred rows of the batches one and two before
+  if (cb > 0) {
+    prev = skey_cur + (size_t)(cb - 1) * a.Mmax;
+    Mp = sM_cur[cb - 1];
+  } else if (has_prev) {
+    prev = skey_pc + (size_t)(CB - 1) * a.Mmax;
+    Mp = sM_pc[CB - 1];
   }
-  // records without neighbour lists (nn / ee): placed first in their
-  // workgroup so that whole waves skip the list-slot gathers in train_fused
-  // (from the batch-ordered copies train_prep wrote: contiguous, no
-  // dependent record-id load)
+  if (cb > 1) Mpp = sM_cur[cb - 2];
+  else if (has_prev) Mpp = sM_pc[CB - 2 + cb];
+  const int U = a.ucount[cb];
+  int *s_prev = s_dyn, *s_u = s_dyn + a.Mmax;
+  __shared__ int s_brk;
+  if (threadIdx.x == 0) s_brk = 0;
+  for (int j = threadIdx.x; j < Mp; j += kTB) s_prev[j] = prev[j];
+  for (int j = threadIdx.x; j < U; j += kTB) s_u[j] = a.ukey[(size_t)cb * SB + j];
   const int *bidx = a.bidx + (size_t)cb * a.B * R;
   const float *btgt = a.btgt + (size_t)cb * a.B * 3;
-  for (int i = threadIdx.x; i < nb; i += kTB) {
-    const int *ri = bidx + i * R;
-    int any = 0;
-    for (int s2 = 4; s2 < R; s2++) any |= ri[s2];
-    s_short[i] = any == 0;
-  }
   __syncthreads();
-  // Component placement, first fit in record order. The scan is sequential,
-  // so wave 0 runs it in scalar registers: every record's packed
-  // (size | multi-slot count << 10, 0 for a non-root) sits in a VGPR of its
-  // lane and is read by a wave-uniform readlane; the results go back into
-  // the root's lane by a lane-select. No LDS round trip sits on the chain (one
-  // thread walking LDS arrays took most of train_prep's time).
-  if (threadIdx.x < 64) {
-    constexpr int U = kPackB / 64;
-    const int lane = threadIdx.x;
-    int pk[U], rb[U], ro[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int i = u * 64 + lane;
-      pk[u] = (i < nb && lab[i] == i) ? (s_csz[i] | (s_cms[i] << 10)) : 0;
-      rb[u] = ro[u] = 0;
-    }
-    int ok = conv && M <= kPackM && NBF <= kPackNBF;
-    int fill = 0, msf = 0, blk = 0;
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      if (u * 64 >= nb) break;
-      for (int l = 0; l < 64 && ok; l++) {
-        const int v = __builtin_amdgcn_readlane(pk[u], l);
-        if (v == 0) continue;
-        const int sz = v & 1023, q = v >> 10;
-        if (sz > RPB || q > MS) {
-          ok = 0;
-          break;
-        }
-        if (fill + sz > RPB || msf + q > MS) {
-          if (lane == 0) s_bfill[blk] = fill;
-          blk++;
-          fill = msf = 0;
-        }
-        if (blk >= NBF) {
-          ok = 0;
-          break;
-        }
-        if (lane == l) {
-          rb[u] = blk;
-          ro[u] = msf;
-        }
-        fill += sz;
-        msf += q;
-      }
-    }
-    if (ok) {
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        if (pk[u] != 0) {
-          s_cblk[u * 64 + lane] = rb[u];
-          s_cmoff[u * 64 + lane] = ro[u];
-        }
-      }
-    }
-    if (lane == 0) {
-      if (ok) s_bfill[blk] = fill;
-      s_ok = ok;
-      s_flag[0] = blk + 1;
-      a.pfast[cb] = ok;
-      a.pnblk[cb] = ok ? blk + 1 : 0;
+  // restart: a record naming two of the previous batch's deferred rows (the
+  // step folds one per record). The host flushes the previous batch first
+  // (train_flush), and this batch sees no deferred rows.
+  for (int i = threadIdx.x; i < nb && Mp; i += kTB) {
+    int e0 = -1;
+    for (int s2 = 0; s2 < R; s2++) {
+      const int row = bidx[i * R + s2];
+      if (row == 0) continue;
+      const int j = bsearch_lds(s_prev, Mp, ((int)slot_is_edge(s2, K) << 30) | row);
+      if (j < 0) continue;
+      if (e0 >= 0 && j != e0) s_brk = 1;
+      e0 = j;
     }
   }
   __syncthreads();
-  if (!s_ok) return;
+  if (s_brk) Mp = 0;
+  if (threadIdx.x == 0) a.pbrk[cb] = s_brk;
+  // stable partition: records without lists first
   {
-    // positions inside a workgroup: records without lists first, then the
-    // others, each in record order (the workgroup of a record, and so the
-    // packing, is unchanged; multi-slot codes index LDS, not positions).
-    // s_csz now holds each record's key = block * 2 + no-list flag; s_mlen
-    // gets its run's component in the upper half.
-    const int nblk = s_flag[0];
-    for (int j = threadIdx.x; j < NBF; j += kTB) {
-      if (j < nblk) s_bshort[j] = 0;
-      else s_bfill[j] = 0;
+    const int per = (nb + kTB - 1) / kTB, i0 = threadIdx.x * per, i1 = min(i0 + per, nb);
+    int cs = 0;
+    for (int i = i0; i < i1; i++) {
+      int any = 0;
+      for (int s = 4; s < R; s++) any |= bidx[i * R + s];
+      s_pos[i] = any;  // temporarily: has a list
+      cs += any == 0;
     }
-    for (int i = threadIdx.x; i < nb; i += kTB) s_csz[i] = s_cblk[lab[i]] * 2 + s_short[i];
-    for (int k = threadIdx.x; k < M; k += kTB)
-      s_mlen[k] |= lab[slotof(s_mrun[k]) / R] << 16;
-    __syncthreads();
-    for (int i = threadIdx.x; i < nb; i += kTB)
-      if (s_short[i]) atomicAdd(&s_bshort[s_csz[i] >> 1], 1);
-    __syncthreads();
-    // rank among the earlier records of the same key; a multi-slot run's
-    // base = its component's offset + the runs of that component before it
-    for (int i = threadIdx.x; i < nb; i += kTB) {
-      const int key = s_csz[i], b = key >> 1;
-      int r = 0;
-      for (int j = 0; j < i; j++) r += s_csz[j] == key;
-      s_grp[i] = b * RPB + ((key & 1) ? r : s_bshort[b] + r);
-    }
-    for (int k = threadIdx.x; k < M; k += kTB) {
-      const int comp = s_mlen[k] >> 16;
-      int base = s_cmoff[comp];
-      for (int j = 0; j < k; j++)
-        if ((s_mlen[j] >> 16) == comp) base += s_mlen[j] & 0xffff;
-      s_mbase[k] = base;
+    int NS = 0;
+    int bs = block_exclusive_scan(cs, &NS, s_ws);
+    // position p of the partitioned order -> workgroup p % NBF, group p / NBF:
+    // every workgroup gets its share of the list records (the step's slowest
+    // workgroup sets the batch time), its list-less records first
+    const int NBF = G / RPB;
+    for (int i = i0; i < i1; i++) {
+      const bool sh = s_pos[i] == 0;
+      const int p = sh ? bs : NS + (i - bs);
+      s_pos[i] = (p % NBF) * RPB + p / NBF;
+      bs += sh;
     }
   }
-  const int G = NBF * RPB;
-  int *pidx = a.pidx + (size_t)cb * G * R;
-  unsigned *pcode = reinterpret_cast<unsigned *>(a.pcode) + (size_t)cb * G * R;
+  int *pidx = a.pidx + (size_t)cb * G * RW;
+  unsigned *pcode = a.pcode + (size_t)cb * G * RW;
   float *ptgt = a.ptgt + (size_t)cb * G * 3;
-  for (int t = threadIdx.x; t < G * R; t += kTB) {
+  for (int t = threadIdx.x; t < G * RW; t += kTB) {
     pidx[t] = 0;
     pcode[t] = 0u;
   }
   for (int t = threadIdx.x; t < G * 3; t += kTB) ptgt[t] = 0.f;
-  for (int j = threadIdx.x; j < NBF; j += kTB) a.pnval[(size_t)cb * NBF + j] = s_bfill[j];
-  __syncthreads();  // zero fill before the scattered writes (same workgroup)
-  // 8 loads per thread in flight before the stores (a global store between
-  // two loads would make each load wait for the previous one)
-  for (int t0 = threadIdx.x; t0 < nb * R; t0 += 8 * kTB) {
-    int v[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int t = t0 + u * kTB;
-      v[u] = t < nb * R ? bidx[t] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int t = t0 + u * kTB;
-      if (t < nb * R) {
-        const int i = t / R;
-        pidx[s_grp[i] * R + (t - i * R)] = v[u];
+  __syncthreads();  // s_pos, s_prev, s_u; zero fill before the scattered writes
+  const unsigned *sc = a.scode + (size_t)cb * SB;
+  for (int t = threadIdx.x; t < nb * R; t += kTB) {
+    const int i = t / R, s = t - i * R;
+    const int row = bidx[t];
+    unsigned code = 0;
+    if (row != 0) {
+      code = sc[t];
+      if (Mp) {
+        const int j = bsearch_lds(s_prev, Mp, ((int)slot_is_edge(s, K) << 30) | row);
+        if (j >= 0) code |= kSPend | ((unsigned)(2 + j) << kDefBits);
       }
     }
+    pidx[s_pos[i] * RW + s] = row;
+    pcode[s_pos[i] * RW + s] = code;
   }
   for (int t = threadIdx.x; t < nb * 3; t += kTB) {
-    const int i = t / 3, c = t - i * 3;
-    ptgt[s_grp[i] * 3 + c] = btgt[t];
+    const int i = t / 3;
+    ptgt[s_pos[i] * 3 + (t - 3 * i)] = btgt[t];
   }
-  for (int t = threadIdx.x; t < V; t += kTB) {
-    const bool prev = t > 0 && rowkey(t) == rowkey(t - 1);
-    const bool next = t + 1 < V && rowkey(t + 1) == rowkey(t);
-    if (!prev && !next) {
-      const int sl = slotof(t), i = sl / R;
-      pcode[s_grp[i] * R + (sl - i * R)] = kCodeOwn;
+  // flush entries, in the previous batch's entry order
+  const int per = (Mp + kTB - 1) / kTB, j0 = threadIdx.x * per, j1 = min(j0 + per, Mp);
+  int cf = 0;
+  for (int j = j0; j < j1; j++) cf += bsearch_lds(s_u, U, s_prev[j]) < 0;
+  int F = 0;
+  int f = block_exclusive_scan(cf, &F, s_ws);
+  const int cap = kFX * nb;
+  for (int j = j0; j < j1; j++) {
+    const int key = s_prev[j];
+    if (bsearch_lds(s_u, U, key) >= 0) continue;
+    if (f < cap) {
+      const int p = f % nb, k = f / nb, g = (p % (G / RPB)) * RPB + p / (G / RPB);
+      pidx[g * RW + R + k] = key & 0x3fffffff;
+      pcode[g * RW + R + k] = ((key >> 30) ? kFEdge : 0u) | ((unsigned)(2 + j) << kDefBits);
+    } else {
+      a.pfo[(size_t)cb * a.Mmax + (f - cap)] = make_int2(key, 2 + j);
     }
+    f++;
   }
-  for (int k = threadIdx.x; k < M; k += kTB) {
-    const int t = s_mrun[k], c = s_mlen[k] & 0xffff, base = s_mbase[k];
-    for (int j = 0; j < c; j++) {
-      const int sl = slotof(t + j), i = sl / R;
-      unsigned code = kCodeMulti | (unsigned)(base + j);
-      if (j == 0) code |= kCodeOwn | ((unsigned)c << 12);
-      pcode[s_grp[i] * R + (sl - i * R)] = code;
-    }
+  const int nfo = max(F - cap, 0);
+  for (int g = threadIdx.x; g < G; g += kTB) {
+    pidx[g * RW + R + kFX] = nfo;
+    pidx[g * RW + R + kFX + 1] = Mpp;
   }
 }
 
 // One workgroup per batch of the chunk: sorted unique (table,row) keys of
 // the non-padding slots and, per key, its slot ids in ascending order.
 __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
-                                                  int nbc, int P) {
+                                                  int nbc, int P, int *skey, int *sM) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long s_key[];
   __shared__ int s_ws[kTB / 64];
   const int cb = blockIdx.x;
@@ -1195,6 +1368,7 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
   }
   int U = 0, V = 0;
   int u = block_exclusive_scan(cnt, &U, s_ws);
+  const int u0 = u;
   block_exclusive_scan(valid, &V, s_ws);
   int *ukey = a.ukey + (size_t)cb * a.SB;
   int *uoff = a.uoff + (size_t)cb * (a.SB + 1);
@@ -1213,7 +1387,8 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
     uoff[U] = V;
     a.ucount[cb] = U;
   }
-  if (a.fused) pack_batch(a, cb, nb, V, P, s_key, s_ws);
+  if (a.fused)
+    defer_codes(a, cb, V, P, u0, s_key, s_ws, reinterpret_cast<int *>(s_key + P), skey, sM);
 }
 
 // deterministic two-level sum of the chunk's per-block losses:
@@ -1348,35 +1523,38 @@ KFn fwd_for(int K, int loss, int act, int tb1) {
   return train_fwd_bwd<L, VPL, 16, false, 0, kTB>;
 }
 
-using KFusedFn = void (*)(TrainArgs, int, int, int, int, int, int);
-using KFlushFn = void (*)(TrainArgs, int, int);
+using KStepFn = void (*)(TrainArgs, int, int, int, int);
+using KFlushFn = void (*)(TrainArgs, const int *, const int *, const int *, int, int);
 
-// fused one-launch step: d in (64, 256] (one float4 per lane, L = 32 or 64),
-// K = 5 with the FOBE (sigmoid/KLD) or HOBE (relu/MSE) heads. NBFM = the
-// workgroup cap of the instantiation (40 when the batch packs into at most
-// 40 workgroups, else kPackNBF): every workgroup of the next launch loads
-// ceil(NBFM / TPC) padding-row partials per thread.
+// deferred-row step: d in (64, 256] (one float4 per lane, L = 32 or 64),
+// K = 5 with the FOBE (sigmoid/KLD) or HOBE (relu/MSE) heads. tb = the
+// workgroup size (records per workgroup = tb / L); nbfm = the workgroup cap
+// of the instantiation (every workgroup loads nbfm / (tb / 2L) row-0
+// partials per thread).
 template <int L, int TB, int NBFM>
-void fused_fns(int loss, KFusedFn &kf, KFlushFn &kfl) {
-  kf = loss == 0 ? train_fused<L, 5, 1, TB, NBFM> : train_fused<L, 5, 2, TB, NBFM>;
-  kfl = train_row0_flush<L, TB, NBFM>;
+void step_fns(int loss, KStepFn &kf, KFlushFn &kfl) {
+  kf = loss == 0 ? train_step<L, 5, 1, TB, NBFM> : train_step<L, 5, 2, TB, NBFM>;
+  kfl = train_flush<L, NBFM, TB / (2 * L)>;
 }
-bool pick_fused(int L, int VPL, int K, int loss, int act, int nbfm, KFusedFn &kf,
-                KFlushFn &kfl, int &tb) {
+bool pick_step(int L, int VPL, int K, int loss, int act, int batch, int &tb, int &nbfm,
+               KStepFn &kf, KFlushFn &kfl) {
   if (VPL != 1 || K != 5 || loss != act) return false;
+  // measured r02 (tools/ab_train.py, interleaved): d=128 L=32 at 128
+  // threads 7.92 / 8.27 us per batch (random / C3 HOBE records) vs 8.33 / 8.75
+  // at 256; d=256 L=64 at 256 threads
+  if (L == 32) tb = tb == 256 ? 256 : 128;
+  else if (L == 64) tb = 256;
+  else return false;
+  const int nbf = (batch + tb / L - 1) / (tb / L);
+  nbfm = nbf <= 32 ? 32 : 64;
+  if (nbf > nbfm) return false;
   if (L == 32) {
-    tb = 256;
-    if (nbfm <= 40) fused_fns<32, 256, 40>(loss, kf, kfl);
-    else fused_fns<32, 256, kPackNBF>(loss, kf, kfl);
-    return true;
+    if (tb == 128) nbfm == 32 ? step_fns<32, 128, 32>(loss, kf, kfl) : step_fns<32, 128, 64>(loss, kf, kfl);
+    else nbfm == 32 ? step_fns<32, 256, 32>(loss, kf, kfl) : step_fns<32, 256, 64>(loss, kf, kfl);
+  } else {
+    nbfm == 32 ? step_fns<64, 256, 32>(loss, kf, kfl) : step_fns<64, 256, 64>(loss, kf, kfl);
   }
-  if (L == 64) {
-    tb = 512;
-    if (nbfm <= 40) fused_fns<64, 512, 40>(loss, kf, kfl);
-    else fused_fns<64, 512, kPackNBF>(loss, kf, kfl);
-    return true;
-  }
-  return false;
+  return true;
 }
 
 bool pick_kernels(int L, int VPL, int K, int loss, int act, int &tb1, int tb2,
@@ -1691,36 +1869,21 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   }
   const int RPB = tb1 / L;
   const int nblk1 = (batch + RPB - 1) / RPB;
-  // fused step: eligible geometry, batch <= kPackB records, NBF workgroups
-  // (packing leaves holes: nblk1 + 50% + 2, at most kPackNBF)
-  KFusedFn kf = nullptr;
+  // deferred-row step: eligible geometry and batch <= kPackB records (every
+  // batch of the run then takes it); else the two-kernel step for every batch
+  KStepFn kf = nullptr;
   KFlushFn kfl = nullptr;
-  int tbf = 0;
-  // train_fused tuning 0: off; else HGX_TRAIN_FUSED (debug builds): 0 off,
-  // 1 only d in (64, 128] (L = 32), 2 (default)
-  // also d in (128, 256] (L = 64; r01: 12.7 vs 12.7 us/batch with the wide
-  // workgroup cap, 11.3 vs 12.7 with the 40-workgroup cap and the list-gather
-  // skip)
-  const int fz = ctx->tune.train_fused ? env_int("HGX_TRAIN_FUSED", 2) : 0;
-  // workgroups per fused batch: the records' lane groups plus headroom for
-  // packing holes (components placed whole, first fit): +8 when that stays
-  // within 40 (the NBFM = 40 instantiation, fewer padding-row partial loads
-  // per workgroup; HGX_TRAIN_NBF_WIDE=1 keeps the wide cap), else 50% + 2 up
-  // to kPackNBF. A batch that needs more takes the two-kernel step.
-  const int tb_f = L == 64 ? 512 : 256;
-  const int prpb0 = tb_f / L;
-  const int need0 = (batch + prpb0 - 1) / prpb0;
-  const bool narrow_nbf = need0 + 8 <= 40 && env_int("HGX_TRAIN_NBF_WIDE", 0) != 1;
-  const int nbf_target = narrow_nbf ? need0 + 8 : std::min(kPackNBF, need0 + need0 / 2 + 2);
-  bool fused = fz != 0 && (L == 32 || fz == 2) &&
-               env_int("HGX_TRAIN_GENERIC", 0) != 1 &&
-               pick_fused(L, VPL, K, loss, act, nbf_target, kf, kfl, tbf) &&
-               batch <= kPackB;
+  int tbf = env_int("HGX_STEP_TB", 0);  // workgroup size (debug builds)
+  int NBFM = 0;
+  const bool fused = ctx->tune.train_fused && env_int("HGX_TRAIN_GENERIC", 0) != 1 &&
+                     batch <= kPackB &&
+                     pick_step(L, VPL, K, loss, act, batch, tbf, NBFM, kf, kfl);
   const int prpb = fused ? tbf / L : 0;
-  const int nbf_need = fused ? (batch + prpb - 1) / prpb : 0;
-  const int NBF = fused ? nbf_target : 0;
-  if (fused && NBF < nbf_need) fused = false;
-  const int MS = 48;  // LDS rows for multi-slot gradients per workgroup
+  const int NBF = fused ? (batch + prpb - 1) / prpb : 0;
+  const int RW = R + kWX;
+  const int Mmax = SB / 2 + 1;        // deferred rows per batch: <= SB / 2
+  const int MX = fused ? 2 + Mmax : 0;
+  HGX_CHECK(ctx, MX <= (int)kDefMask + 1, HGX_EUNSUP, "batch too large for the step");
   const int lstride = std::max(nblk1, NBF);
   const int GPB2 = tb2 / L;
   // one unique-row task per group, plus the two padding-row workgroups
@@ -1728,8 +1891,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   const int64_t nbatches = (n + batch - 1) / batch;
   const int GB = kGraphBatches;
   // prep chunk: CB batches (a multiple of GB) prepared by one launch, then
-  // trained by CB / GB graph replays (graph g holds chunk-local batches
-  // [g*GB, (g+1)*GB), their indices baked into the node arguments)
+  // trained (two-kernel step: by CB / GB graph replays when HGX_GRAPH=1)
   const int CB = (int)std::min<int64_t>(1024, (nbatches + GB - 1) / GB * GB);
   const int NG = CB / GB;
   const int64_t nchunks = (nbatches + CB - 1) / CB;
@@ -1738,36 +1900,33 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   const size_t bidx_n = (size_t)CB * batch * R + (size_t)RPB * R * 2 + 64;
   const size_t btgt_n = (size_t)CB * batch * 3 + (size_t)RPB * 3 * 2 + 64;
   const size_t inv_n = (size_t)CB * SB + (size_t)RPB * R * 2 + 64;
-  const size_t pg = fused ? (size_t)CB * NBF * prpb : 0;  // packed groups
-  const size_t pack_ints = fused ? pg * R * 2 + pg * 3 + (size_t)CB * NBF + 2 * CB + 64 : 0;
+  const size_t pg = fused ? (size_t)CB * NBF * prpb : 0;  // placed groups
+  // step buffers: pfo, pidx, pcode, ptgt, scode, skey [2], sM [2], pbrk
+  const size_t step_ints = fused ? 2 * (size_t)CB * Mmax + pg * RW * 2 + pg * 3 +
+                                       (size_t)CB * SB + 2 * (size_t)CB * Mmax +
+                                       3 * (size_t)CB + 64
+                                 : 0;
   const size_t prep_ints = bidx_n + btgt_n + inv_n + (size_t)CB * SB +
-                           (size_t)CB * (SB + 1) + CB + 2 * CB + 64 + pack_ints;
+                           (size_t)CB * (SB + 1) + CB + 2 * CB + 64 + step_ints;
   HGX_TRY(hgx_ensure(ctx, ctx->s1, sizeof(int) * (n + 1)));              // perm
   HGX_TRY(hgx_ensure(ctx, ctx->s2, sizeof(float) * (size_t)SB * dp));    // gslot
-  // gzero (K1 partials) | r0 [2][2][2][dp] | gp [2][NBF][2][dp]
-  const size_t s3_f = (size_t)nblk1 * 2 * dp + 8 * (size_t)dp + (size_t)2 * NBF * 2 * dp;
+  // gzero (K1 partials) | gacc [3][MX][dp] int64 | shadow [3][MX][2][dp] |
+  // gp [2][NBFM][2][dp] | ovf
+  const size_t gz_f = (size_t)nblk1 * 2 * dp;
+  const size_t gacc_f = (size_t)3 * MX * dp * 2;  // in floats
+  const size_t sh_f = (size_t)3 * MX * 2 * dp;
+  const size_t gp_f = (size_t)2 * NBFM * 2 * dp;
+  const size_t s3_f = (gz_f + 3) / 4 * 4 + gacc_f + sh_f + gp_f + 16;
   HGX_TRY(hgx_ensure(ctx, ctx->s3, sizeof(float) * s3_f));
   HGX_TRY(hgx_ensure(ctx, ctx->s4, sizeof(float) * (size_t)nbatches * lstride + 16));
-  // chunk buffers in two parities: train_prep of chunk c + 1 runs on a side
-  // stream while chunk c trains (graph replay bakes parity 0: one parity)
   const bool use_graph = env_int("HGX_GRAPH", 0) == 1 && !fused;
-  // HGX_TRAIN_PIPE: 0 (default) = one parity, prep of chunk c + 1 queued
-  // right after chunk c (the host waits for it with the GPU idle, ~0.1 ms per
-  // 1024 batches); 1 = two parities, prep of chunk c + 1 queued on the same
-  // stream BEFORE chunk c's batches (no host bubble); 2 = two parities, prep
-  // on a side stream beside the batches. Measured r01 at d=128 (4M records):
-  // 8.61 / 8.90 / 9.45 us per batch. The packed records a prep has just
-  // written sit in the Infinity Cache when the batches right behind it read
-  // them; preparing a chunk ahead lets 9 ms of training traffic evict them,
-  // and a second active stream also slows every batch launch.
-  const int pipe = use_graph ? 0 : env_int("HGX_TRAIN_PIPE", 0);
-  const int NPAR = pipe == 0 ? 1 : 2;
-  HGX_TRY(hgx_ensure(ctx, ctx->s5, sizeof(int) * prep_ints * NPAR));
+  HGX_TRY(hgx_ensure(ctx, ctx->s5, sizeof(int) * prep_ints));
   HGX_TRY(hgx_ensure(ctx, ctx->s6, 64 + sizeof(double) * kLossBlocks));  // loss
   int *perm = ctx->s1.as<int>();
-  HGX_HIP(ctx, hipMemsetAsync(ctx->s5.p, 0, sizeof(int) * prep_ints * NPAR, ctx->stream));
+  HGX_HIP(ctx, hipMemsetAsync(ctx->s5.p, 0, sizeof(int) * prep_ints, ctx->stream));
   HGX_HIP(ctx, hipMemsetAsync(ctx->s3.p, 0, sizeof(float) * s3_f, ctx->stream));
   TrainArgs a;
+  memset(&a, 0, sizeof(a));
   a.idx = ctx->rec_idx.as<int>();
   a.tgt = ctx->rec_tgt.as<float>();
   a.perm = perm;
@@ -1788,14 +1947,24 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   a.lstride = lstride;
   a.fused = fused ? 1 : 0;
   a.prpb = prpb;
-  a.NBF = NBF;
-  a.MS = MS;
-  a.r0 = a.gzero + (size_t)nblk1 * 2 * dp;
-  a.gp = a.r0 + 8 * (size_t)dp;
+  a.RW = RW;
+  a.MX = MX;
+  a.Mmax = Mmax;
+  {
+    float *f = a.gzero + (gz_f + 3) / 4 * 4;
+    a.gacc = reinterpret_cast<long long *>(f);
+    f += gacc_f;
+    a.shadow = f;
+    f += sh_f;
+    a.gp = f;
+    f += gp_f;
+    a.ovf = reinterpret_cast<int *>(f);
+  }
   a.lr = lr;
   a.eps = eps;
   a.loss = loss;
   a.act = act;
+  int *skey[2] = {nullptr, nullptr}, *sM[2] = {nullptr, nullptr};
   {
     int *q = ctx->s5.as<int>();
     a.bidx = q;
@@ -1813,36 +1982,25 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     q += ((uintptr_t)q / sizeof(int)) % 2;  // 8-B align
     a.bmeta = reinterpret_cast<int2 *>(q);
     q += 2 * CB;
-    a.pidx = q;
-    q += pg * R;
-    a.pcode = q;
-    q += pg * R;
-    a.ptgt = reinterpret_cast<float *>(q);
-    q += pg * 3;
-    a.pnval = q;
-    q += (size_t)CB * NBF;
-    a.pnblk = q;
-    q += CB;
-    a.pfast = q;
-  }
-  // parity 1: the same layout shifted by prep_ints
-  TrainArgs ap[2] = {a, a};
-  if (NPAR == 2) {
-    const size_t sh = prep_ints;
-    TrainArgs &b = ap[1];
-    b.bidx += sh;
-    b.btgt += sh;
-    b.inv += sh;
-    b.ukey += sh;
-    b.uoff += sh;
-    b.ucount += sh;
-    b.bmeta = reinterpret_cast<int2 *>(reinterpret_cast<int *>(b.bmeta) + sh);
-    b.pidx += sh;
-    b.pcode += sh;
-    b.ptgt += sh;
-    b.pnval += sh;
-    b.pnblk += sh;
-    b.pfast += sh;
+    if (fused) {
+      a.pfo = reinterpret_cast<int2 *>(q);
+      q += 2 * (size_t)CB * Mmax;
+      a.pidx = q;
+      q += pg * RW;
+      a.pcode = reinterpret_cast<unsigned *>(q);
+      q += pg * RW;
+      a.ptgt = reinterpret_cast<float *>(q);
+      q += pg * 3;
+      a.scode = reinterpret_cast<unsigned *>(q);
+      q += (size_t)CB * SB;
+      for (int i = 0; i < 2; i++) {
+        skey[i] = q;
+        q += (size_t)CB * Mmax;
+        sM[i] = q;
+        q += CB;
+      }
+      a.pbrk = q;
+    }
   }
   double *dloss = reinterpret_cast<double *>(ctx->s6.as<char>() + 32);
   double *dpart = reinterpret_cast<double *>(ctx->s6.as<char>() + 64);
@@ -1871,16 +2029,15 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
       for (auto g : gexec) (void)hipGraphExecDestroy(g);
       for (auto g : graph) (void)hipGraphDestroy(g);
       for (auto e : ev) (void)hipEventDestroy(e);
-      if (side) (void)hipStreamDestroy(side);
-      if (hflags) (void)hipHostFree(hflags);
+      if (hbrk) (void)hipHostFree(hbrk);
     }
-    hipStream_t side = nullptr;
-    int *hflags = nullptr;  // pinned [NPAR][2][CB]: pfast, pnblk per parity
+    int *hbrk = nullptr;  // pinned: the chunk's restart flags (train_place)
   } res;
+  if (fused) HGX_HIP(ctx, hipHostMalloc(reinterpret_cast<void **>(&res.hbrk), sizeof(int) * CB));
   // Direct launches by default: measured as fast as hipGraph replay of the
   // same kernels (10.6 us per batch both ways at d=128) with less host time,
   // and rocprofv3 kernel tracing crashes on the replays. HGX_GRAPH=1 replays
-  // captured graphs instead.
+  // captured graphs of the two-kernel step instead.
   auto launch_run = [&](const TrainArgs &ac, int cb0, int nrun) {
     for (int b = cb0; b < cb0 + nrun; b++) {
       hipLaunchKernelGGL(k1, dim3(nblk1), dim3(tb1), 0, ctx->stream, ac, b);
@@ -1909,54 +2066,22 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     HGX_HIP(ctx, hipEventCreate(&e));
     res.ev.push_back(e);
   }
-
-  // prep pipeline: side stream, per parity "prep done + flags copied" and
-  // "chunk trained" events
-  hipEvent_t ev_prep[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr},
-             ev_perm = nullptr;
-  if (pipe == 2) HGX_HIP(ctx, hipStreamCreateWithFlags(&res.side, hipStreamNonBlocking));
-  hipStream_t ps = pipe == 2 ? res.side : ctx->stream;  // prep stream
-  HGX_HIP(ctx, hipHostMalloc(reinterpret_cast<void **>(&res.hflags),
-                             sizeof(int) * 4 * (size_t)CB));
-  for (int i = 0; i < 2; i++) {
-    HGX_HIP(ctx, hipEventCreateWithFlags(&ev_prep[i], hipEventDisableTiming));
-    res.ev.push_back(ev_prep[i]);
-    HGX_HIP(ctx, hipEventCreateWithFlags(&ev_free[i], hipEventDisableTiming));
-    res.ev.push_back(ev_free[i]);
-  }
-  HGX_HIP(ctx, hipEventCreateWithFlags(&ev_perm, hipEventDisableTiming));
-  res.ev.push_back(ev_perm);
-  // both parities start free
-  for (int i = 0; i < 2; i++) HGX_HIP(ctx, hipEventRecord(ev_free[i], ctx->stream));
-  // train_prep of chunk c into parity c % NPAR on the side stream, after the
-  // epoch's permutation and after the parity's previous chunk trained; then
-  // its packing flags to pinned host memory
-  auto issue_prep = [&](int64_t c) -> int {
-    const int par = (int)(c % NPAR);
-    const TrainArgs &ac = ap[par];
-    const int64_t base = c * CB;
-    const int nbc = (int)std::min<int64_t>(CB, nbatches - base);
-    if (ps != ctx->stream) {
-      HGX_HIP(ctx, hipStreamWaitEvent(ps, ev_perm, 0));
-      HGX_HIP(ctx, hipStreamWaitEvent(ps, ev_free[par], 0));
-    }
-    hipLaunchKernelGGL(train_prep, dim3(CB), dim3(kTB),
-                       (size_t)P * sizeof(unsigned long long), ps, ac,
-                       base, nbc, P);
-    HGX_LAUNCH_CHECK(ctx);
-    if (fused) {
-      int *hf = res.hflags + (size_t)par * 2 * CB;
-      HGX_HIP(ctx, hipMemcpyAsync(hf, ac.pfast, sizeof(int) * nbc,
-                                  hipMemcpyDeviceToHost, ps));
-      HGX_HIP(ctx, hipMemcpyAsync(hf + CB, ac.pnblk, sizeof(int) * nbc,
-                                  hipMemcpyDeviceToHost, ps));
-    }
-    HGX_HIP(ctx, hipEventRecord(ev_prep[par], ps));
-    return HGX_OK;
+  const size_t prep_smem = (size_t)P * (sizeof(unsigned long long) + sizeof(int));
+  const size_t place_smem = sizeof(int) * ((size_t)Mmax + SB);
+  // Preparation of chunk c (same stream, right before its batches: the
+  // records it writes are still in the Infinity Cache when they are read).
+  // The step: one launch per batch, q = the batch's index in the epoch.
+  auto prep_chunk = [&](int64_t c, int nbc) {
+    const int cp = (int)(c & 1);
+    hipLaunchKernelGGL(train_prep, dim3(CB), dim3(kTB), prep_smem, ctx->stream, a,
+                       c * CB, nbc, P, skey[cp], sM[cp]);
+    if (fused)
+      hipLaunchKernelGGL(train_place, dim3(CB), dim3(kTB), place_smem, ctx->stream, a,
+                         nbc, CB, skey[cp], sM[cp], skey[cp ^ 1], sM[cp ^ 1], c > 0 ? 1 : 0);
   };
 
   std::vector<int> hperm;
-  int64_t nfused = 0, nsplit = 0;
+  int64_t nfused = 0, nsplit = 0, nrestart = 0;
   double batch_ms = 0.0;
   double best = INFINITY;
   int ep = 0;
@@ -1995,57 +2120,44 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     (void)hipMemsetAsync(dloss, 0, sizeof(double), ctx->stream);
     (void)hipMemsetAsync(a.lossbuf, 0, sizeof(float) * (size_t)nbatches * lstride,
                          ctx->stream);
-    if (hipEventRecord(ev_perm, ctx->stream) != hipSuccess ||
-        (rc = issue_prep(0)) != HGX_OK) {
-      if (!rc) rc = hgx_fail(ctx, HGX_EHIP, "prep pipeline failed");
-      break;
-    }
-    for (int64_t c = 0; c < nchunks && rc == HGX_OK; c++) {
-      const int par = (int)(c % NPAR);
-      const TrainArgs &ac = ap[par];
+    int last_nbc = 0;
+    for (int64_t c = 0; c < nchunks; c++) {
       const int64_t base = c * CB;
       const int nbc = (int)std::min<int64_t>(CB, nbatches - base);
-      const int *hfast = res.hflags + (size_t)par * 2 * CB;
-      const int *hnblk = hfast + CB;
-      // which batches packed: one host wait per chunk, normally long done
-      // (prep c ran beside chunk c - 1)
-      if (hipEventSynchronize(ev_prep[par]) != hipSuccess ||
-          (ps != ctx->stream &&
-           hipStreamWaitEvent(ctx->stream, ev_prep[par], 0) != hipSuccess)) {
-        rc = hgx_fail(ctx, HGX_EHIP, "batch preparation failed: %s",
-                      hipGetErrorString(hipGetLastError()));
-        break;
-      }
-      if (NPAR == 1 && c + 1 < nchunks) {
-        // one parity: chunk c + 1's prep must follow chunk c (queued below)
-      } else if (c + 1 < nchunks && (rc = issue_prep(c + 1)) != HGX_OK) {
-        break;
+      prep_chunk(c, nbc);
+      if (fused) {
+        // the chunk's restart flags: one host wait per chunk of 1024 batches
+        if (hipMemcpyAsync(res.hbrk, a.pbrk, sizeof(int) * nbc, hipMemcpyDeviceToHost,
+                           ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess) {
+          rc = hgx_fail(ctx, HGX_EHIP, "batch preparation failed: %s",
+                        hipGetErrorString(hipGetLastError()));
+          break;
+        }
       }
       (void)hipEventRecord(bev[2 * c], ctx->stream);
       if (fused) {
-        int qrun = 0;  // position in the current run of fused launches
+        const int cp = (int)(c & 1);
         for (int b = 0; b < nbc; b++) {
-          if (hfast[b]) {
-            const int64_t gbat = base + b;
-            const int nrec = (int)std::min<int64_t>(batch, n - gbat * batch);
-            hipLaunchKernelGGL(kf, dim3(NBF), dim3(tbf),
-                               (size_t)MS * L * sizeof(float4), ctx->stream, ac,
-                               b, (int)gbat, nrec, qrun > 0 ? hnblk[b - 1] : 0,
-                               qrun, qrun > 0 ? 1 : 0);
-            qrun++;
-            nfused++;
-          } else {
-            if (qrun > 0)
-              hipLaunchKernelGGL(kfl, dim3(1), dim3(tbf), 0, ctx->stream, ac,
-                                 b - 1, qrun - 1);
-            qrun = 0;
-            launch_run(ac, b, 1);
-            nsplit++;
+          const int64_t gbat = base + b;
+          const int nrec = (int)std::min<int64_t>(batch, n - gbat * batch);
+          if (res.hbrk[b] && gbat > 0) {
+            // restart: the previous batch's deferred rows -> tables first
+            // (it is batch cb - 1 of this chunk or the previous chunk's last)
+            const int *kp = b > 0 ? skey[cp] + (size_t)(b - 1) * Mmax
+                                  : skey[cp ^ 1] + (size_t)(CB - 1) * Mmax;
+            const int *ml = b > 0 ? sM[cp] + (b - 1) : sM[cp ^ 1] + (CB - 1);
+            const int *mp = gbat < 2 ? nullptr
+                            : b > 1  ? sM[cp] + (b - 2)
+                                     : sM[cp ^ 1] + (CB - 2 + b);
+            hipLaunchKernelGGL(kfl, dim3(64), dim3(256), 0, ctx->stream, a, kp, ml, mp,
+                               (int)(gbat - 1), NBF);
+            nrestart++;
           }
+          hipLaunchKernelGGL(kf, dim3(NBF), dim3(tbf), 0, ctx->stream, a, b, (int)gbat,
+                             nrec, (int)gbat);
         }
-        if (qrun > 0)
-          hipLaunchKernelGGL(kfl, dim3(1), dim3(tbf), 0, ctx->stream, ac,
-                             nbc - 1, qrun - 1);
+        nfused += nbc;
       } else if (use_graph) {
         for (int g = 0; g * GB < nbc; g++) {
           if (hipGraphLaunch(res.gexec[g], ctx->stream) != hipSuccess) {
@@ -2053,25 +2165,48 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
             break;
           }
         }
+        nsplit += nbc;
       } else {
-        launch_run(ac, 0, nbc);
+        launch_run(a, 0, nbc);
         nsplit += nbc;
       }
       (void)hipEventRecord(bev[2 * c + 1], ctx->stream);
-      (void)hipEventRecord(ev_free[par], ctx->stream);
-      if (NPAR == 1 && c + 1 < nchunks && (rc = issue_prep(c + 1)) != HGX_OK) break;
+      last_nbc = nbc;
+      if (rc) break;
     }
     if (rc) break;
+    if (fused) {
+      // the last batch's deferred rows -> tables; gacc clean for the next
+      // epoch (the last batch's entries and the one before it)
+      const int cp = (int)((nchunks - 1) & 1);
+      const int *ml = sM[cp] + (last_nbc - 1);
+      const int *mp = last_nbc >= 2 ? sM[cp] + (last_nbc - 2)
+                                    : (nchunks >= 2 ? sM[cp ^ 1] + (CB - 1) : nullptr);
+      const int nlast = (int)(n - (nbatches - 1) * batch);
+      hipLaunchKernelGGL(kfl, dim3(64), dim3(256), 0, ctx->stream, a,
+                         skey[cp] + (size_t)(last_nbc - 1) * Mmax, ml, mp,
+                         (int)(nbatches - 1), std::min(NBF, nlast));
+    }
     hipLaunchKernelGGL(loss_partial, dim3(kLossBlocks), dim3(kTB), 0,
                        ctx->stream, a.lossbuf, nbatches * lstride, dpart);
     hipLaunchKernelGGL(loss_final, dim3(1), dim3(kLossBlocks), 0, ctx->stream,
                        dpart, dloss);
     double lsum = 0.0;
+    int ovf = 0;
     if (hipMemcpyAsync(&lsum, dloss, sizeof(double), hipMemcpyDeviceToHost,
                        ctx->stream) != hipSuccess ||
+        (fused && hipMemcpyAsync(&ovf, a.ovf, sizeof(int), hipMemcpyDeviceToHost,
+                                 ctx->stream) != hipSuccess) ||
         hipStreamSynchronize(ctx->stream) != hipSuccess) {
       rc = hgx_fail(ctx, HGX_EHIP, "epoch failed: %s",
                     hipGetErrorString(hipGetLastError()));
+      break;
+    }
+    if (ovf) {
+      rc = hgx_fail(ctx, HGX_ENUMERIC,
+                    "a gradient left the step's fixed-point range (|g| >= %g after "
+                    "the 1/batch factor, or NaN): training diverged",
+                    (double)kFixLimit);
       break;
     }
     for (int64_t c = 0; c < nchunks; c++) {
@@ -2110,6 +2245,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   ctx->train_batches = (int64_t)ep * nbatches;
   ctx->train_fused = nfused;
   ctx->train_split = nsplit;
+  ctx->train_restart = nrestart;
   if (epochs_run) *epochs_run = ep;
   return HGX_OK;
 }
@@ -2126,6 +2262,12 @@ extern "C" int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
 extern "C" int hgx_train_last_loss(hgx_ctx *ctx, double *loss_sum) {
   if (!ctx) return HGX_EINVAL;
   if (loss_sum) *loss_sum = ctx->train_loss_sum;
+  return HGX_OK;
+}
+
+extern "C" int hgx_train_restarts(hgx_ctx *ctx, int64_t *restarts) {
+  if (!ctx) return HGX_EINVAL;
+  if (restarts) *restarts = ctx->train_restart;
   return HGX_OK;
 }
 

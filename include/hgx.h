@@ -33,6 +33,8 @@ extern "C" {
 #define HGX_EUNSUP -6    /* shape outside what this build supports          */
 #define HGX_EVALUE -7    /* ValueError in the reference (np.random.choice on
                             an empty row, hg2v_sample.py:49-51)             */
+#define HGX_ENUMERIC -8  /* trainer: a gradient left the batch step's fixed-
+                            point range (diverged run, NaN)                 */
 
 #define HGX_LOSS_KLD 0   /* BooleanModel: kullback_leibler_divergence       */
 #define HGX_LOSS_MSE 1   /* UnweightedFloatModel: mean_squared_error        */
@@ -224,15 +226,18 @@ int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr, float eps,
  * processed. */
 int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
                          int64_t *batches);
-/* Of the last hgx_train: batches run by the fused one-launch step
- * (train_fused: rows shared inside a batch packed into one workgroup,
- * padding-row update deferred to the next launch) and batches that took the
- * two-kernel step (train_fwd_bwd + train_update). HGX_TRAIN_FUSED=0 forces
- * the two-kernel step. Same Keras semantics either way (embedding.py:269-305,
- * hg2v_model.py:51-203); the two differ only in the summation order of the
- * padding row's gradient. */
+/* Of the last hgx_train: batches run by the one-launch deferred-row step
+ * (train_step: rows in several records of a batch summed as fixed point and
+ * applied by the next launch, the padding row likewise) and batches that
+ * took the two-kernel step (train_fwd_bwd + train_update; tuning
+ * "train_fused" 0 forces it). Same Keras semantics either way
+ * (embedding.py:269-305, hg2v_model.py:51-203); the two differ only in the
+ * summation order of a row's slot gradients. */
 int hgx_train_path_stats(hgx_ctx *ctx, int64_t *fused_batches,
                          int64_t *split_batches);
+/* Of the last hgx_train: step batches launched after a mid-epoch flush of the
+ * previous batch's deferred rows (a record of theirs named two of them). */
+int hgx_train_restarts(hgx_ctx *ctx, int64_t *restarts);
 /* Sum of the per-record losses (all three heads) of the last epoch of the
  * last hgx_train, in double: epoch loss = sum / records. Consecutive
  * hgx_train calls continue the same model state (tables and Adagrad

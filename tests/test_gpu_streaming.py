@@ -77,7 +77,7 @@ def test_fit_streaming_embed_hobe_chunks(ctx):
   c.alg_set(r.random((inc.N, 10)), r.random((inc.E, 10)))
   c.alg_run(20)
   n_all = c.sample_hobe(9, 5, 20)
-  chunks = embedding._row_chunks(inc, 40, 5000)
+  chunks = embedding._row_chunks(inc, 40, 2000)
   assert len(chunks) >= 3
 
   def make(ci):

@@ -166,10 +166,11 @@ def _mixed_reuse_records(rs, nb, B, K, hub_batches, wide=20000):
                                         (256, O.LOSS_KLD, O.ACT_SIGMOID)])
 def test_fused_step_mixed_runs_vs_oracle_and_split(ctx, d, loss, act,
                                                    monkeypatch):
-  """The fused one-launch step (train_fused) against the oracle and the
-  two-kernel step: runs of fused batches interrupted by unpackable batches
-  (hub rows) exercise the deferred padding-row update, its flush before a
-  two-kernel batch and the restart after it; a ragged last batch too."""
+  """The one-launch deferred-row step (train_step) against the oracle and
+  the two-kernel step. Hub batches (every id from 5 rows) make nearly every
+  row of the batch a deferred row; consecutive hub batches chain them
+  (pending slots, several per record); the wide batch after a hub batch
+  flushes the hub rows it does not touch; a ragged last batch too."""
   rs = np.random.RandomState(11)
   K, B, nb = 5, 256, 12
   idx, tgt = _mixed_reuse_records(rs, nb, B, K, hub_batches={3, 4, 8})
@@ -193,13 +194,14 @@ def test_fused_step_mixed_runs_vs_oracle_and_split(ctx, d, loss, act,
   finally:
     ctx.set_tuning("train_fused", 1)
   fused, split = res["2"][3], res["0"][3]
-  assert fused == (nb - 3, 3), fused
+  assert fused == (nb, 0), fused
   assert split == (0, nb), split
   for mode in ("2", "0"):
     gnt, get_, gl, _ = res[mode]
     assert np.allclose(gl, ol, rtol=1e-4, atol=1e-7), (mode, gl, ol)
     assert np.abs(gnt - ont).max() < 1e-5 and np.abs(get_ - oet).max() < 1e-5
-  # the two device paths differ only in the padding row's summation order
+  # the two device paths differ only in how the gradients of a row's slots
+  # are summed (2^44 fixed point vs sequential fp32)
   for a, b in zip(res["2"][:2], res["0"][:2]):
     assert np.abs(a - b).max() < 1e-6
 
@@ -217,3 +219,84 @@ def test_fused_step_bitwise_deterministic(ctx):
     out.append(ctx.model_get())
   assert np.array_equal(out[0][0], out[1][0])
   assert np.array_equal(out[0][1], out[1][1])
+
+
+def test_step_flush_overflow_and_pending_chains_vs_oracle(ctx):
+  """Batch 0: 128 ne records with distinct rows, each twice (1536 rows with
+  exactly two slots: all deferred); batch 1 touches none of them, so it
+  flushes more rows than its 4 flush slots per record hold (the overflow
+  list). Then hub batches back to back (every slot of a record pending, the
+  slot-by-slot fold), a wide batch, and a ragged 3-record last batch after a
+  hub batch. Against the oracle, in order, FOBE and HOBE heads."""
+  rs = np.random.RandomState(21)
+  K, B, d = 5, 256, 128
+  R = 4 + 2 * K
+
+  def batch(lo, hi, n=B):
+    idx = np.zeros((n, R), np.int32)
+    kind = rs.randint(0, 3, n)
+    m0, m1, m2 = kind == 0, kind == 1, kind == 2
+    idx[m0, 0] = rs.randint(lo, hi, m0.sum())
+    idx[m0, 2] = rs.randint(lo, hi, m0.sum())
+    idx[m1, 1] = rs.randint(lo, hi, m1.sum())
+    idx[m1, 3] = rs.randint(lo, hi, m1.sum())
+    idx[m2, 0] = rs.randint(lo, hi, m2.sum())
+    idx[m2, 3] = rs.randint(lo, hi, m2.sum())
+    idx[m2, 4:4 + K] = rs.randint(lo, hi, (m2.sum(), K))
+    idx[m2, 4 + K:] = rs.randint(lo, hi, (m2.sum(), K))
+    tgt = np.zeros((n, 3), np.float32)
+    tgt[np.arange(n), kind] = rs.uniform(0, 1, n).astype(np.float32)
+    return idx, tgt
+
+  # batch 0: ne records, distinct node ids (ln + list) and edge ids (re +
+  # list) over the 128 records, each record twice
+  half = np.zeros((128, R), np.int32)
+  nodes = rs.permutation(np.arange(1, 5000))[:128 * (1 + K)].reshape(128, 1 + K)
+  edges = rs.permutation(np.arange(1, 5000))[:128 * (1 + K)].reshape(128, 1 + K)
+  half[:, 0] = nodes[:, 0]
+  half[:, 4:4 + K] = nodes[:, 1:]
+  half[:, 3] = edges[:, 0]
+  half[:, 4 + K:] = edges[:, 1:]
+  t0 = np.zeros((B, 3), np.float32)
+  t0[:, 2] = rs.uniform(0, 1, B).astype(np.float32)
+  blocks = [(np.concatenate([half, half]), t0), batch(10000, 30000),
+            batch(1, 6), batch(1, 6), batch(1, 6), batch(10000, 30000),
+            batch(1, 6), batch(30000, 40000, 3)]
+  idx = np.concatenate([b[0] for b in blocks])
+  tgt = np.concatenate([b[1] for b in blocks])
+  perms = np.arange(idx.shape[0])[None, :]
+  nrows = int(idx[:, [0, 2] + list(range(4, 4 + K))].max()) + 2
+  erows = int(idx[:, [1, 3] + list(range(4 + K, 4 + 2 * K))].max()) + 2
+  nt = rs.uniform(-0.05, 0.05, (nrows, d)).astype(np.float32)
+  et = rs.uniform(-0.05, 0.05, (erows, d)).astype(np.float32)
+  for loss, act in ((O.LOSS_MSE, O.ACT_RELU), (O.LOSS_KLD, O.ACT_SIGMOID)):
+    pp = np.repeat(perms, 2, 0)
+    ont, oet, ol, _, _ = O.train(idx, tgt, K, nt, et, loss, act, batch=B,
+                                 max_epochs=2, perms=pp, min_delta=-1.0)
+    ctx.records_set(idx, tgt)
+    ctx.model_init(d, nrows, erows, node_tab=nt, edge_tab=et)
+    gl = ctx.train(batch=B, max_epochs=2, loss=loss, act=act, perms=pp,
+                   min_delta=-1.0)
+    assert ctx.train_path_stats() == (2 * len(blocks), 0)
+    # hub batches after hub batches: records naming two deferred rows of the
+    # previous batch -> flush + restart
+    assert ctx.train_restarts() > 0
+    gnt, get_ = ctx.model_get()
+    assert np.allclose(gl, ol, rtol=1e-4, atol=1e-7), (gl, ol)
+    assert np.abs(gnt - ont).max() < 1e-5 and np.abs(get_ - oet).max() < 1e-5
+
+
+def test_step_diverged_gradients_raise(ctx):
+  """Gradients beyond the step's fixed-point range (a diverged run) raise
+  FloatingPointError instead of wrapping silently."""
+  rs = np.random.RandomState(2)
+  idx, tgt = _mixed_reuse_records(rs, 4, 256, 5, hub_batches={1})
+  nrows = int(idx[:, [0, 2] + list(range(4, 14))].max()) + 2
+  erows = int(idx[:, [1, 3] + list(range(9, 14))].max()) + 2
+  ctx.records_set(idx, tgt)
+  ctx.model_init(128, nrows, erows,
+                 node_tab=np.full((nrows, 128), 30.0, np.float32),
+                 edge_tab=np.full((erows, 128), 30.0, np.float32))
+  with pytest.raises(FloatingPointError):
+    ctx.train(batch=256, max_epochs=1, loss=O.LOSS_MSE, act=O.ACT_RELU,
+              perms=np.arange(idx.shape[0])[None, :])

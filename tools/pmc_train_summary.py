@@ -1,6 +1,6 @@
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (of bench.py, or
 tools/perf_train.py) into profiles/<round>_pmc_train.json: HBM bytes per
-batch step (train_fused, or train_fwd_bwd + train_update), gfx950 FETCH
+batch step (train_step, or train_fwd_bwd + train_update), gfx950 FETCH
 correction x2 (MI355X_MICROARCH.md, HBM section). Usage:
   python tools/pmc_train_summary.py FETCH_CSV WRITE_CSV OUT_JSON d ROUND [CMD]"""
 import csv, json, sys
@@ -15,7 +15,7 @@ def per_kernel(path, counter):
     if r["Counter_Name"] != counter:
       continue
     name = r["Kernel_Name"]
-    for key in ("train_fwd_bwd", "train_update", "train_fused", "train_row0_flush"):
+    for key in ("train_fwd_bwd", "train_update", "train_step", "train_flush"):
       if key in name:
         vals.setdefault(key, []).append(float(r["Counter_Value"]))
   return {k: float(np.mean(v)) for k, v in vals.items()}, \
@@ -24,9 +24,9 @@ def per_kernel(path, counter):
 
 f, nf = per_kernel(fetch_csv, "FETCH_SIZE")
 w, nw = per_kernel(write_csv, "WRITE_SIZE")
-# per batch step: every batch runs train_fused (or K1 + K2); the flush runs
-# once per run of fused batches (per chunk), so it is averaged over batches
-steps = max(nf.get("train_fused", 0) + nf.get("train_fwd_bwd", 0), 1)
+# per batch step: every batch runs train_step (or K1 + K2); the flush runs
+# once per epoch (and before a restart), so it is averaged over batches
+steps = max(nf.get("train_step", 0) + nf.get("train_fwd_bwd", 0), 1)
 def per_step(vals, counts):
   return sum(vals[k] * counts[k] for k in vals) / steps
 hbm = 1024 * (2 * per_step(f, nf) + per_step(w, nw))
@@ -38,8 +38,8 @@ res = {
                 + (sys.argv[6] if len(sys.argv) > 6 else
                    "bench.py --steps 1 --warmup 0 --no-cpu --no-c4 --no-extra")),
     "note": ("Per batch of 256 records at d=%d on 100k/50k-row tables, summed over "
-             "the per-batch kernels (train_fused, or train_fwd_bwd + train_update, and the "
-             "row-0 flush once per run), per batch step. FETCH_SIZE / "
+             "the per-batch kernels (train_step, or train_fwd_bwd + train_update, and the "
+             "deferred-row flush once per epoch), per batch step. FETCH_SIZE / "
              "WRITE_SIZE are KB; gfx950 correction: FETCH doubled (wide 16-B-per-"
              "lane reads are tallied at half), WRITE as is. Infinity-Cache hits "
              "are counted by these counters." % d),

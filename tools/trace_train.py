@@ -7,7 +7,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hypergraphembedding_amd import _hgx
 
 d = int(sys.argv[1]) if len(sys.argv) > 1 else 128
-n = int(sys.argv[2]) if len(sys.argv) > 2 else 400_000
+hobe = len(sys.argv) > 2 and sys.argv[2] == "hobe"  # the C3 HOBE stream
+n = int(sys.argv[2]) if len(sys.argv) > 2 and not hobe else 400_000
 extra = dict(kv.split("=") for kv in sys.argv[3].split("+")) if len(sys.argv) > 3 else {}
 rs = np.random.RandomState(0)
 N, E, K = 100000, 50000, 5
@@ -23,6 +24,17 @@ idx[m2, 4 + K:] = rs.randint(1, E + 1, (m2.sum(), K))
 tgt = np.zeros((n, 3), np.float32)
 tgt[np.arange(n), kind] = rs.uniform(0, 1, n)
 ctx = _hgx.Context(0)
+if hobe:
+  from hypergraphembedding_amd.synthetic import random_hypergraph
+  inc = random_hypergraph(seed=0)
+  ctx.upload(inc)
+  r = np.random.RandomState(4)
+  ctx.alg_set(r.random_sample((inc.N, 10)), r.random_sample((inc.E, 10)))
+  ctx.alg_run(20)
+  m = ctx.sample_hobe(17, 5, 200)
+  idx, tgt = ctx.records_get()
+  sel = np.random.RandomState(1).permutation(m)[:n]
+  idx, tgt = idx[sel], tgt[sel]
 ctx.records_set(idx, tgt)
 ctx.model_init(d, N + 2, E + 2, seed=1)
 os.environ.update(extra)
@@ -55,6 +67,11 @@ if ctx.train_path_stats()[0] > 0:
         f"blocks {m[4]*100:.0f} active {m[5]*100:.0f}")
   print("per-WG median: ids %.2f gathers+row0 %.2f compute %.2f emits %.2f multi %.2f tail %.2f" % tuple(m[6:12]))
   print("per-WG max:    ids %.2f gathers+row0 %.2f compute %.2f emits %.2f multi %.2f tail %.2f" % tuple(m[12:18]))
+  # per workgroup index: median phase durations over batches (which block is slow)
+  nb_ = int(m[4] * 100)
+  per = np.array([np.median(np.diff(t[16:250, 0, w, :7], axis=1), axis=0) for w in range(nb_)]) * 0.01
+  for w in range(nb_):
+    print("  wg %2d: " % w + " ".join("%.2f" % v for v in per[w]))
   sys.exit(0)
 k1 = t[:, 0, :, :6]
 k2 = t[:, 1, :, :4]
