@@ -436,7 +436,7 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
            "dim": d4, "train_records_per_s": round(n4 / t4, 1),
            "per_batch_us": round(ms4t * 1e3 / max(bat4, 1), 2),
            "batch_steps": {"train_step": fz4, "train_fwd_bwd+train_update": sp4},
-           "restarts": ctx.train_restarts(),
+           "multi_pending_batches": ctx.train_multi_pending(),
            "loss": "MSE", "act": "relu"}
   if rank == 0 and world == 1 and not args.no_cpu:
     # CPU port on 1M records of the same stream, tables of the same size

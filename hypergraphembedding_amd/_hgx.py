@@ -79,7 +79,7 @@ SIGNATURES = {
                          _vp, _vp, _pint]),
     "hgx_train_last_stats": (_int, [_vp, _pdbl, _pi64, _pi64]),
     "hgx_train_path_stats": (_int, [_vp, _pi64, _pi64]),
-    "hgx_train_restarts": (_int, [_vp, _pi64]),
+    "hgx_train_multi_pending": (_int, [_vp, _pi64]),
     "hgx_train_last_loss": (_int, [_vp, _pdbl]),
     "hgx_synth_powerlaw": (_int, [_i32, _i32, ctypes.c_double, ctypes.c_double,
                                   _u64, _vp, _vp, _pi64,
@@ -440,10 +440,10 @@ class Context:
                                          ctypes.byref(sp)))
     return f.value, sp.value
 
-  def train_restarts(self):
-    """Step batches of the last train() that followed a mid-epoch flush."""
+  def train_multi_pending(self):
+    """Step batches of the last train() in the MULTI pending-slot form."""
     v = ctypes.c_int64()
-    self._chk(lib().hgx_train_restarts(self.h, ctypes.byref(v)))
+    self._chk(lib().hgx_train_multi_pending(self.h, ctypes.byref(v)))
     return v.value
 
 

@@ -123,7 +123,7 @@ struct hgx_ctx {
   double train_loss_sum = 0;  // sum of per-record losses, last epoch
   int64_t train_records = 0, train_batches = 0;
   int64_t train_fused = 0, train_split = 0;
-  int64_t train_restart = 0;  // step batches that followed a mid-epoch flush
+  int64_t train_multi = 0;  // step batches in the MULTI pending-slot form
 
   // ---- scratch ----
   DevBuf s0, s1, s2, s3, s4, s5, s6, s7;

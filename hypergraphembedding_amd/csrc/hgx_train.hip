@@ -672,7 +672,7 @@ __device__ __forceinline__ void row0_finish(const TrainArgs &a, float4 (*s_red)[
 // records per workgroup, ceil(B / RPB) <= NBFM workgroups; records placed by
 // train_place, those without neighbour lists first (whole waves skip the list
 // gathers).
-template <int L, int KMAX, int MODE, int TB, int NBFM>
+template <int L, int KMAX, int MODE, int TB, int NBFM, bool MULTI>
 __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, int nb, int q) {
   constexpr int RPB = TB / L, R = 4 + 2 * KMAX, K = KMAX, NC = 2 * L;
   static_assert(L == 32 || L == 64, "step geometry");
@@ -830,17 +830,18 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
     }
     // pending slots (rows deferred by the previous batch): base row from the
     // previous batch's shadow, folded with its gacc sum, written to every
-    // slot of the record that names the same entry. train_place guarantees
-    // one such entry per record (a batch where some record names two runs
-    // after a train_flush of the previous batch instead, without pending
-    // slots): one pass, its entry picked by v_cndmask (no dynamic register
-    // index), normally not taken.
+    // slot of the record that names the same entry. A select pass handles
+    // one entry per record (picked by v_cndmask: no dynamic register index,
+    // no loop-carried copies of the rows). MULTI = 0: train_place found at
+    // most one entry per record in this batch, one pass (normally not
+    // taken); MULTI = 1: two passes, then slot by slot.
     unsigned pm = 0;
 #pragma unroll
     for (int s = 0; s < R; s++)
       if (code[s] & kSPend) pm |= 1u << s;
     if (!has) pm = 0;
-    if (__any(pm != 0)) {
+    auto fold_pass = [&]() {
+      if (!__any(pm != 0)) return;
       const int ps = pm ? __builtin_ctz(pm) : 0;
       unsigned cd = 0;
 #pragma unroll
@@ -864,6 +865,26 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
           Pv[s] = pp;
           Av[s] = aa;
         }
+      pm &= ~wm;
+    };
+    fold_pass();
+    if (MULTI) {
+      fold_pass();
+      if (__any(pm != 0)) {
+#pragma unroll
+        for (int s = 0; s < R; s++) {
+          if (!__any((pm >> s) & 1u)) continue;
+          const int mp = (code[s] >> kDefBits) & kDefMask;
+          const longlong2 *g = gacc_row<L>(a, ppar, mp);
+          const longlong2 ga = g[2 * lane], gb2 = g[2 * lane + 1];
+          float4 pp = sh_row<L>(a, ppar, mp, 0)[lane], aa = sh_row<L>(a, ppar, mp, 1)[lane];
+          fold4(pp, aa, ga, gb2, a.lr, a.eps);
+          if ((pm >> s) & 1u) {
+            Pv[s] = pp;
+            Av[s] = aa;
+          }
+        }
+      }
     }
     float4 zN = f4(0.f), zE = f4(0.f);
     float lrec = 0.f;
@@ -1030,23 +1051,13 @@ __global__ __launch_bounds__(256) void train_flush(TrainArgs a, const int *keys,
       adagrad4_hw(p, ac, g, a.lr, a.eps);
       tab_row<L>(a, e, 0, 0)[lane] = p;
       tab_row<L>(a, e, 1, 0)[lane] = ac;
-      sh_row<L>(a, par, e, 0)[lane] = p;
-      sh_row<L>(a, par, e, 1)[lane] = ac;
       continue;
     }
     flush_row<L>(a, par, keys[e - 2], e, lane);
     longlong2 *g = gacc_row<L>(a, par, e);
     g[2 * lane] = g[2 * lane + 1] = make_longlong2(0, 0);
   }
-  // a step launched after this flush (mid-epoch, q + 1) folds row 0 from
-  // shadow entry 0 / 1 and the np partials of parity q & 1: the folded state
-  // and zero partials make that fold the identity (workgroup 0 computed row
-  // 0 above, groups 0 and 1)
-  __syncthreads();
-  if (blockIdx.x == 0) {
-    float4 *gpz = reinterpret_cast<float4 *>(a.gp) + (size_t)(q & 1) * NBFM * 2 * L;
-    for (int i = threadIdx.x; i < NBFM * 2 * L; i += 256) gpz[i] = f4(0.f);
-  }
+
   longlong2 *z = gacc_row<L>(a, opar, 2);
   for (int i = blockIdx.x * 256 + threadIdx.x; i < zc * 2 * L; i += gridDim.x * 256)
     z[i] = make_longlong2(0, 0);
@@ -1196,9 +1207,8 @@ __global__ __launch_bounds__(kTB) void train_place(TrainArgs a, int nbc, int CB,
   const int *bidx = a.bidx + (size_t)cb * a.B * R;
   const float *btgt = a.btgt + (size_t)cb * a.B * 3;
   __syncthreads();
-  // restart: a record naming two of the previous batch's deferred rows (the
-  // step folds one per record). The host flushes the previous batch first
-  // (train_flush), and this batch sees no deferred rows.
+  // a record naming two of the previous batch's deferred rows: the batch
+  // takes train_step's MULTI form (the light form folds one per record)
   for (int i = threadIdx.x; i < nb && Mp; i += kTB) {
     int e0 = -1;
     for (int s2 = 0; s2 < R; s2++) {
@@ -1211,7 +1221,6 @@ __global__ __launch_bounds__(kTB) void train_place(TrainArgs a, int nbc, int CB,
     }
   }
   __syncthreads();
-  if (s_brk) Mp = 0;
   if (threadIdx.x == 0) a.pbrk[cb] = s_brk;
   // stable partition: records without lists first
   {
@@ -1532,12 +1541,13 @@ using KFlushFn = void (*)(TrainArgs, const int *, const int *, const int *, int,
 // of the instantiation (every workgroup loads nbfm / (tb / 2L) row-0
 // partials per thread).
 template <int L, int TB, int NBFM>
-void step_fns(int loss, KStepFn &kf, KFlushFn &kfl) {
-  kf = loss == 0 ? train_step<L, 5, 1, TB, NBFM> : train_step<L, 5, 2, TB, NBFM>;
+void step_fns(int loss, KStepFn *kf, KFlushFn &kfl) {
+  kf[0] = loss == 0 ? train_step<L, 5, 1, TB, NBFM, false> : train_step<L, 5, 2, TB, NBFM, false>;
+  kf[1] = loss == 0 ? train_step<L, 5, 1, TB, NBFM, true> : train_step<L, 5, 2, TB, NBFM, true>;
   kfl = train_flush<L, NBFM, TB / (2 * L)>;
 }
 bool pick_step(int L, int VPL, int K, int loss, int act, int batch, int &tb, int &nbfm,
-               KStepFn &kf, KFlushFn &kfl) {
+               KStepFn *kf, KFlushFn &kfl) {
   if (VPL != 1 || K != 5 || loss != act) return false;
   // measured r02 (tools/ab_train.py, interleaved): d=128 L=32 at 128
   // threads 7.92 / 8.27 us per batch (random / C3 HOBE records) vs 8.33 / 8.75
@@ -1871,7 +1881,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   const int nblk1 = (batch + RPB - 1) / RPB;
   // deferred-row step: eligible geometry and batch <= kPackB records (every
   // batch of the run then takes it); else the two-kernel step for every batch
-  KStepFn kf = nullptr;
+  KStepFn kf[2] = {nullptr, nullptr};  // light / MULTI pending-slot forms
   KFlushFn kfl = nullptr;
   int tbf = env_int("HGX_STEP_TB", 0);  // workgroup size (debug builds)
   int NBFM = 0;
@@ -2031,7 +2041,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
       for (auto e : ev) (void)hipEventDestroy(e);
       if (hbrk) (void)hipHostFree(hbrk);
     }
-    int *hbrk = nullptr;  // pinned: the chunk's restart flags (train_place)
+    int *hbrk = nullptr;  // pinned: the chunk's MULTI flags (train_place)
   } res;
   if (fused) HGX_HIP(ctx, hipHostMalloc(reinterpret_cast<void **>(&res.hbrk), sizeof(int) * CB));
   // Direct launches by default: measured as fast as hipGraph replay of the
@@ -2081,7 +2091,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   };
 
   std::vector<int> hperm;
-  int64_t nfused = 0, nsplit = 0, nrestart = 0;
+  int64_t nfused = 0, nsplit = 0, nmulti = 0;
   double batch_ms = 0.0;
   double best = INFINITY;
   int ep = 0;
@@ -2126,7 +2136,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
       const int nbc = (int)std::min<int64_t>(CB, nbatches - base);
       prep_chunk(c, nbc);
       if (fused) {
-        // the chunk's restart flags: one host wait per chunk of 1024 batches
+        // the chunk's MULTI flags: one host wait per chunk of 1024 batches
         if (hipMemcpyAsync(res.hbrk, a.pbrk, sizeof(int) * nbc, hipMemcpyDeviceToHost,
                            ctx->stream) != hipSuccess ||
             hipStreamSynchronize(ctx->stream) != hipSuccess) {
@@ -2141,20 +2151,9 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
         for (int b = 0; b < nbc; b++) {
           const int64_t gbat = base + b;
           const int nrec = (int)std::min<int64_t>(batch, n - gbat * batch);
-          if (res.hbrk[b] && gbat > 0) {
-            // restart: the previous batch's deferred rows -> tables first
-            // (it is batch cb - 1 of this chunk or the previous chunk's last)
-            const int *kp = b > 0 ? skey[cp] + (size_t)(b - 1) * Mmax
-                                  : skey[cp ^ 1] + (size_t)(CB - 1) * Mmax;
-            const int *ml = b > 0 ? sM[cp] + (b - 1) : sM[cp ^ 1] + (CB - 1);
-            const int *mp = gbat < 2 ? nullptr
-                            : b > 1  ? sM[cp] + (b - 2)
-                                     : sM[cp ^ 1] + (CB - 2 + b);
-            hipLaunchKernelGGL(kfl, dim3(64), dim3(256), 0, ctx->stream, a, kp, ml, mp,
-                               (int)(gbat - 1), NBF);
-            nrestart++;
-          }
-          hipLaunchKernelGGL(kf, dim3(NBF), dim3(tbf), 0, ctx->stream, a, b, (int)gbat,
+          const int multi = res.hbrk[b] && gbat > 0;
+          nmulti += multi;
+          hipLaunchKernelGGL(kf[multi], dim3(NBF), dim3(tbf), 0, ctx->stream, a, b, (int)gbat,
                              nrec, (int)gbat);
         }
         nfused += nbc;
@@ -2245,7 +2244,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   ctx->train_batches = (int64_t)ep * nbatches;
   ctx->train_fused = nfused;
   ctx->train_split = nsplit;
-  ctx->train_restart = nrestart;
+  ctx->train_multi = nmulti;
   if (epochs_run) *epochs_run = ep;
   return HGX_OK;
 }
@@ -2265,9 +2264,9 @@ extern "C" int hgx_train_last_loss(hgx_ctx *ctx, double *loss_sum) {
   return HGX_OK;
 }
 
-extern "C" int hgx_train_restarts(hgx_ctx *ctx, int64_t *restarts) {
+extern "C" int hgx_train_multi_pending(hgx_ctx *ctx, int64_t *batches) {
   if (!ctx) return HGX_EINVAL;
-  if (restarts) *restarts = ctx->train_restart;
+  if (batches) *batches = ctx->train_multi;
   return HGX_OK;
 }
 

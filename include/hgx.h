@@ -235,9 +235,9 @@ int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
  * summation order of a row's slot gradients. */
 int hgx_train_path_stats(hgx_ctx *ctx, int64_t *fused_batches,
                          int64_t *split_batches);
-/* Of the last hgx_train: step batches launched after a mid-epoch flush of the
- * previous batch's deferred rows (a record of theirs named two of them). */
-int hgx_train_restarts(hgx_ctx *ctx, int64_t *restarts);
+/* Of the last hgx_train: step batches launched in the MULTI pending-slot form
+ * (a record of theirs names two rows deferred by the previous batch). */
+int hgx_train_multi_pending(hgx_ctx *ctx, int64_t *batches);
 /* Sum of the per-record losses (all three heads) of the last epoch of the
  * last hgx_train, in double: epoch loss = sum / records. Consecutive
  * hgx_train calls continue the same model state (tables and Adagrad

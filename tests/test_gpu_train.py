@@ -279,8 +279,8 @@ def test_step_flush_overflow_and_pending_chains_vs_oracle(ctx):
                    min_delta=-1.0)
     assert ctx.train_path_stats() == (2 * len(blocks), 0)
     # hub batches after hub batches: records naming two deferred rows of the
-    # previous batch -> flush + restart
-    assert ctx.train_restarts() > 0
+    # previous batch -> the MULTI form of the step
+    assert ctx.train_multi_pending() > 0
     gnt, get_ = ctx.model_get()
     assert np.allclose(gl, ol, rtol=1e-4, atol=1e-7), (gl, ol)
     assert np.abs(gnt - ont).max() < 1e-5 and np.abs(get_ - oet).max() < 1e-5
