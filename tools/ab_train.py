@@ -49,7 +49,8 @@ else:
 
 vp = ctypes.c_void_p
 hs = []
-for path in libs:
+for spec in libs:
+  path, _, tune = spec.partition(":")  # lib.so[:key=value] (hgx_set_tuning)
   L = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
   L.hgx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
   L.hgx_records_set.argtypes = [vp, ctypes.c_int64, ctypes.c_int, vp, vp]
@@ -63,6 +64,10 @@ for path in libs:
                                      ctypes.POINTER(ctypes.c_int64)]
   h = vp()
   assert L.hgx_create(0, ctypes.byref(h)) == 0
+  if tune:
+    key, val = tune.split("=")
+    L.hgx_set_tuning.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
+    assert L.hgx_set_tuning(h, key.encode(), int(val)) == 0
   assert L.hgx_records_set(h, n, K, idx.ctypes.data, tgt.ctypes.data) == 0
   assert L.hgx_model_init(h, d, N + 2, E + 2, 1, None, None) == 0
   hs.append((L, h))
@@ -79,5 +84,5 @@ for rnd in range(6):
     if rnd > 0:
       res[i].append(ms.value * 1e3 / bat.value)
 for path, r in zip(libs, res):
-  print(f"{kind} d={d} {os.path.basename(path):>12s}: us/batch min {min(r):.3f} "
+  print(f"{kind} d={d} {os.path.basename(path):>28s}: us/batch min {min(r):.3f} "
         f"median {np.median(r):.3f}")
