@@ -88,6 +88,8 @@ def main():
   dist = None
   if args.one_device:
     local = 0
+  # library calls without an explicit context (EmbedHg2vAlgDist) use this device
+  os.environ["HGX_DEVICE"] = str(local)
   if world > 1:
     import torch
     import torch.distributed as dist
