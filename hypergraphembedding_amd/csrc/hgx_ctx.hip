@@ -116,6 +116,14 @@ extern "C" int hgx_set_tuning(hgx_ctx *ctx, const char *key, int64_t value) {
   } else if (k == "train_fused") {
     HGX_CHECK(ctx, value == 0 || value == 1, HGX_EINVAL, "train_fused must be 0 or 1");
     t.train_fused = (int)value;
+  } else if (k == "train_lanes") {
+    HGX_CHECK(ctx, value == 0 || value == 32 || value == 64, HGX_EINVAL,
+              "train_lanes must be 0, 32 or 64");
+    t.train_lanes = (int)value;
+  } else if (k == "train_tb") {
+    HGX_CHECK(ctx, value == 0 || value == 128 || value == 256 || value == 512, HGX_EINVAL,
+              "train_tb must be 0, 128, 256 or 512");
+    t.train_tb = (int)value;
   } else if (k == "alg_long") {
     HGX_CHECK(ctx, value == 0 || (value >= 64 && value <= (1 << 20)), HGX_EINVAL,
               "alg_long must be 0 or in [64, 2^20]");

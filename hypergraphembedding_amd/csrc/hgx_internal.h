@@ -43,6 +43,12 @@ struct Tuning {
   // trainer: 1 fused one-launch batch step where a batch packs, 0 the
   // two-kernel step for every batch
   int train_fused = 1;
+  // trainer step at dp = 128: lanes per record (0 auto, 32: float4 per lane,
+  // 64: float2 per lane)
+  int train_lanes = 0;
+  // trainer step workgroup size (0 auto; 128 / 256 at 32 lanes, 256 / 512 at
+  // 64 lanes x float2; other values fall back to the geometry's default)
+  int train_tb = 0;
   // alg-dist: long-row threshold (0: kLongRow) and coordinate row width
   // (0: round_up(k + 1, 4))
   int alg_long = 0;

@@ -564,107 +564,185 @@ __device__ __forceinline__ unsigned long long to_fix(float v) {
 __device__ __forceinline__ float from_fix(long long v) {
   return (float)((double)v * kFixInv);
 }
-// v -> gacc entry (4 consecutive int64 of this lane), fixed point
-__device__ __forceinline__ void fix_add4(long long *dst, float4 v, int &bad) {
-  bad |= !(fabsf(v.x) < kFixLimit) | !(fabsf(v.y) < kFixLimit) |
-         !(fabsf(v.z) < kFixLimit) | !(fabsf(v.w) < kFixLimit);
-  unsigned long long *d = reinterpret_cast<unsigned long long *>(dst);
-  atomicAdd(d + 0, to_fix(v.x));
-  atomicAdd(d + 1, to_fix(v.y));
-  atomicAdd(d + 2, to_fix(v.z));
-  atomicAdd(d + 3, to_fix(v.w));
-}
+// The step's per-lane vector: VW floats of a row (float4: dp = 4L, float2:
+// dp = 2L), the fixed-point view of this lane's part of a gacc entry, and the
+// ops on them
+template <int VW>
+struct SV;
+template <>
+struct SV<4> {
+  using T = float4;
+  struct Fx {
+    longlong2 a, b;
+  };
+  static __device__ __forceinline__ T zero() { return f4(0.f); }
+  static __device__ __forceinline__ T add(T x, T y) { return x + y; }
+  static __device__ __forceinline__ T mul(T x, float m) {
+    return make_float4(x.x * m, x.y * m, x.z * m, x.w * m);
+  }
+  static __device__ __forceinline__ T fma(float s, T v, T c) { return fma4(s, v, c); }
+  static __device__ __forceinline__ float dot(T x, T y) { return dot4(x, y); }
+  static __device__ __forceinline__ void adagrad(T &p, T &ac, T g, float lr, float eps) {
+    adagrad4_hw(p, ac, g, lr, eps);
+  }
+  static __device__ __forceinline__ void pin(T &v) {
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+  }
+  static __device__ __forceinline__ Fx ldfix(const long long *e, int lane) {
+    const longlong2 *g = reinterpret_cast<const longlong2 *>(e) + 2 * lane;
+    return {g[0], g[1]};
+  }
+  static __device__ __forceinline__ T unfix(const Fx &g) {
+    return make_float4(from_fix(g.a.x), from_fix(g.a.y), from_fix(g.b.x), from_fix(g.b.y));
+  }
+  static __device__ __forceinline__ void addfix(long long *e, int lane, T v, int &bad) {
+    bad |= !(fabsf(v.x) < kFixLimit) | !(fabsf(v.y) < kFixLimit) |
+           !(fabsf(v.z) < kFixLimit) | !(fabsf(v.w) < kFixLimit);
+    unsigned long long *d = reinterpret_cast<unsigned long long *>(e) + 4 * lane;
+    atomicAdd(d + 0, to_fix(v.x));
+    atomicAdd(d + 1, to_fix(v.y));
+    atomicAdd(d + 2, to_fix(v.z));
+    atomicAdd(d + 3, to_fix(v.w));
+  }
+  static __device__ __forceinline__ void zerofix(long long *e, int lane) {
+    longlong2 *g = reinterpret_cast<longlong2 *>(e) + 2 * lane;
+    g[0] = g[1] = make_longlong2(0, 0);
+  }
+};
+template <>
+struct SV<2> {
+  using T = float2;
+  struct Fx {
+    longlong2 a;
+  };
+  static __device__ __forceinline__ T zero() { return make_float2(0.f, 0.f); }
+  static __device__ __forceinline__ T add(T x, T y) { return make_float2(x.x + y.x, x.y + y.y); }
+  static __device__ __forceinline__ T mul(T x, float m) { return make_float2(x.x * m, x.y * m); }
+  static __device__ __forceinline__ T fma(float s, T v, T c) {
+    return make_float2(fmaf(s, v.x, c.x), fmaf(s, v.y, c.y));
+  }
+  static __device__ __forceinline__ float dot(T x, T y) { return x.x * y.x + x.y * y.y; }
+  static __device__ __forceinline__ void adagrad(T &p, T &ac, T g, float lr, float eps) {
+    const float *gv = &g.x;
+    float *pp = &p.x, *aa = &ac.x;
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const float na = __fadd_rn(aa[c], __fmul_rn(gv[c], gv[c]));
+      aa[c] = na;
+      const float den = __fadd_rn(__builtin_amdgcn_sqrtf(na), eps);
+      pp[c] = __fsub_rn(pp[c], __fmul_rn(__fmul_rn(lr, gv[c]), __builtin_amdgcn_rcpf(den)));
+    }
+  }
+  static __device__ __forceinline__ void pin(T &v) { asm volatile("" : "+v"(v.x), "+v"(v.y)); }
+  static __device__ __forceinline__ Fx ldfix(const long long *e, int lane) {
+    return {reinterpret_cast<const longlong2 *>(e)[lane]};
+  }
+  static __device__ __forceinline__ T unfix(const Fx &g) {
+    return make_float2(from_fix(g.a.x), from_fix(g.a.y));
+  }
+  static __device__ __forceinline__ void addfix(long long *e, int lane, T v, int &bad) {
+    bad |= !(fabsf(v.x) < kFixLimit) | !(fabsf(v.y) < kFixLimit);
+    unsigned long long *d = reinterpret_cast<unsigned long long *>(e) + 2 * lane;
+    atomicAdd(d + 0, to_fix(v.x));
+    atomicAdd(d + 1, to_fix(v.y));
+  }
+  static __device__ __forceinline__ void zerofix(long long *e, int lane) {
+    reinterpret_cast<longlong2 *>(e)[lane] = make_longlong2(0, 0);
+  }
+};
 // the deferred Adagrad step of the previous batch: (p, a) += sum
-__device__ __forceinline__ void fold4(float4 &p, float4 &ac, longlong2 g01,
-                                      longlong2 g23, float lr, float eps) {
-  const float4 g = make_float4(from_fix(g01.x), from_fix(g01.y), from_fix(g23.x),
-                               from_fix(g23.y));
-  adagrad4_hw(p, ac, g, lr, eps);
+template <int VW>
+__device__ __forceinline__ void fold(typename SV<VW>::T &p, typename SV<VW>::T &ac,
+                                     const typename SV<VW>::Fx &g, float lr, float eps) {
+  SV<VW>::adagrad(p, ac, SV<VW>::unfix(g), lr, eps);
 }
 
-// views of the deferred-row buffers (L lanes x float4 per row: dp = 4L)
-template <int L>
-__device__ __forceinline__ float4 *sh_row(const TrainArgs &a, int par, int m, int which) {
-  return reinterpret_cast<float4 *>(a.shadow) + (((size_t)par * a.MX + m) * 2 + which) * L;
+// views of the deferred-row buffers (L lanes x VW floats per row: dp = VW L)
+template <int L, int VW>
+__device__ __forceinline__ typename SV<VW>::T *sh_row(const TrainArgs &a, int par, int m,
+                                                      int which) {
+  return reinterpret_cast<typename SV<VW>::T *>(a.shadow) +
+         (((size_t)par * a.MX + m) * 2 + which) * L;
 }
-template <int L>
-__device__ __forceinline__ longlong2 *gacc_row(const TrainArgs &a, int par, int m) {
-  return reinterpret_cast<longlong2 *>(a.gacc) + ((size_t)par * a.MX + m) * (2 * L);
+// the dp int64 of gacc entry m
+template <int L, int VW>
+__device__ __forceinline__ long long *gacc_row(const TrainArgs &a, int par, int m) {
+  return a.gacc + ((size_t)par * a.MX + m) * (VW * L);
 }
-template <int L>
-__device__ __forceinline__ float4 *tab_row(const TrainArgs &a, bool edge, int acc, int row) {
+template <int L, int VW>
+__device__ __forceinline__ typename SV<VW>::T *tab_row(const TrainArgs &a, bool edge, int acc,
+                                                       int row) {
   float *t = acc ? (edge ? a.eacc : a.nacc) : (edge ? a.etab : a.ntab);
-  return reinterpret_cast<float4 *>(t) + (size_t)row * L;
+  return reinterpret_cast<typename SV<VW>::T *>(t) + (size_t)row * L;
 }
 
 // one flush entry: the deferred row (table bit 30 | row) of entry m of the
 // previous batch folded and written back
-template <int L>
+template <int L, int VW>
 __device__ __forceinline__ void flush_row(const TrainArgs &a, int par, int key, int m,
                                           int lane) {
   const bool edge = key >> 30;
   const int row = key & 0x3fffffff;
-  float4 p = sh_row<L>(a, par, m, 0)[lane], ac = sh_row<L>(a, par, m, 1)[lane];
-  const longlong2 *g = gacc_row<L>(a, par, m);
-  fold4(p, ac, g[2 * lane], g[2 * lane + 1], a.lr, a.eps);
-  tab_row<L>(a, edge, 0, row)[lane] = p;
-  tab_row<L>(a, edge, 1, row)[lane] = ac;
+  typename SV<VW>::T p = sh_row<L, VW>(a, par, m, 0)[lane], ac = sh_row<L, VW>(a, par, m, 1)[lane];
+  fold<VW>(p, ac, SV<VW>::ldfix(gacc_row<L, VW>(a, par, m), lane), a.lr, a.eps);
+  tab_row<L, VW>(a, edge, 0, row)[lane] = p;
+  tab_row<L, VW>(a, edge, 1, row)[lane] = ac;
 }
 
 // The padding row's partials of the previous batch (np workgroups, at most
 // NBFM: MAXPER = NBFM / TPC loads per thread, index clamped, masked in
 // row0_stage) and its base (shadow of the previous batch, or the table for
 // the first batch of an epoch), issued on the first round trip.
-template <int L, int TB, int NBFM>
+template <int L, int VW, int TB, int NBFM>
 struct Row0Loads {
   static constexpr int NC = 2 * L, TPC = TB / NC, MAXPER = (NBFM + TPC - 1) / TPC;
-  float4 gv[MAXPER];
-  float4 rp, ra;
+  typename SV<VW>::T gv[MAXPER];
+  typename SV<VW>::T rp, ra;
 };
-template <int L, int TB, int NBFM>
+template <int L, int VW, int TB, int NBFM>
 __device__ __forceinline__ void row0_issue(const TrainArgs &a, int q, int np,
-                                           Row0Loads<L, TB, NBFM> &ld) {
-  using RL = Row0Loads<L, TB, NBFM>;
+                                           Row0Loads<L, VW, TB, NBFM> &ld) {
+  using RL = Row0Loads<L, VW, TB, NBFM>;
+  using V = typename SV<VW>::T;
   static_assert(TB % RL::NC == 0, "workgroup covers whole columns");
   const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
   const int tab = col / L, c = col % L, ppar = (q + 2) % 3;
   // the address is selected (q is uniform), not the loaded value
-  ld.rp = (q ? sh_row<L>(a, ppar, tab, 0) : tab_row<L>(a, tab, 0, 0))[c];
-  ld.ra = (q ? sh_row<L>(a, ppar, tab, 1) : tab_row<L>(a, tab, 1, 0))[c];
-  const float4 *gp = reinterpret_cast<const float4 *>(a.gp) +
-                     (size_t)((q + 1) & 1) * NBFM * RL::NC;
+  ld.rp = (q ? sh_row<L, VW>(a, ppar, tab, 0) : tab_row<L, VW>(a, tab, 0, 0))[c];
+  ld.ra = (q ? sh_row<L, VW>(a, ppar, tab, 1) : tab_row<L, VW>(a, tab, 1, 0))[c];
+  const V *gp = reinterpret_cast<const V *>(a.gp) + (size_t)((q + 1) & 1) * NBFM * RL::NC;
   const int last = max(np - 1, 0);
 #pragma unroll
   for (int u = 0; u < RL::MAXPER; u++)
     ld.gv[u] = gp[(size_t)min(sub + u * RL::TPC, last) * RL::NC + col];
 }
 // this thread's fixed-order partial sum of partials [0, np) -> s_red
-template <int L, int TB, int NBFM>
-__device__ __forceinline__ void row0_stage(int np, const Row0Loads<L, TB, NBFM> &ld,
-                                           float4 (*s_red)[2 * L]) {
-  using RL = Row0Loads<L, TB, NBFM>;
+template <int L, int VW, int TB, int NBFM>
+__device__ __forceinline__ void row0_stage(int np, const Row0Loads<L, VW, TB, NBFM> &ld,
+                                           typename SV<VW>::T (*s_red)[2 * L]) {
+  using RL = Row0Loads<L, VW, TB, NBFM>;
+  using S = SV<VW>;
   const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
-  float4 g = f4(0.f);
+  typename S::T g = S::zero();
 #pragma unroll
-  for (int u = 0; u < RL::MAXPER; u++) {
-    const float m = (float)(sub + u * RL::TPC < np);
-    const float4 v = ld.gv[u];
-    g = g + make_float4(v.x * m, v.y * m, v.z * m, v.w * m);
-  }
+  for (int u = 0; u < RL::MAXPER; u++)
+    g = S::add(g, S::mul(ld.gv[u], (float)(sub + u * RL::TPC < np)));
   s_red[sub][col] = g;
 }
 // after a workgroup barrier: column owners (sub == 0) add the TPC staged sums
 // in order and apply the previous batch's row-0 step (zero gradient for the
 // first batch of an epoch: an identity)
-template <int L, int TB, int NBFM>
-__device__ __forceinline__ void row0_finish(const TrainArgs &a, float4 (*s_red)[2 * L],
-                                            float4 &p0, float4 &a0) {
-  using RL = Row0Loads<L, TB, NBFM>;
+template <int L, int VW, int TB, int NBFM>
+__device__ __forceinline__ void row0_finish(const TrainArgs &a,
+                                            typename SV<VW>::T (*s_red)[2 * L],
+                                            typename SV<VW>::T &p0, typename SV<VW>::T &a0) {
+  using RL = Row0Loads<L, VW, TB, NBFM>;
+  using S = SV<VW>;
   const int col = threadIdx.x % RL::NC;
-  float4 gs = f4(0.f);
+  typename S::T gs = S::zero();
 #pragma unroll
-  for (int j = 0; j < RL::TPC; j++) gs = gs + s_red[j][col];
-  adagrad4_hw(p0, a0, gs, a.lr, a.eps);
+  for (int j = 0; j < RL::TPC; j++) gs = S::add(gs, s_red[j][col]);
+  S::adagrad(p0, a0, gs, a.lr, a.eps);
 }
 
 // One launch = one batch. q = the batch's index in the epoch (parities
@@ -672,15 +750,17 @@ __device__ __forceinline__ void row0_finish(const TrainArgs &a, float4 (*s_red)[
 // records per workgroup, ceil(B / RPB) <= NBFM workgroups; records placed by
 // train_place, those without neighbour lists first (whole waves skip the list
 // gathers).
-template <int L, int KMAX, int MODE, int TB, int NBFM, bool MULTI>
+template <int L, int VW, int KMAX, int MODE, int TB, int NBFM, bool MULTI>
 __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, int nb, int q) {
   constexpr int RPB = TB / L, R = 4 + 2 * KMAX, K = KMAX, NC = 2 * L;
+  using S = SV<VW>;
+  using V = typename S::T;
   static_assert(L == 32 || L == 64, "step geometry");
   static_assert(R + kWX <= 32, "slot and batch words fit the first 32 lanes");
-  __shared__ float4 s_z[2][RPB][L];
-  __shared__ float4 s_gl[RPB][R][L];  // gradients of local (one-record) rows
-  __shared__ float4 s_red[TB / NC][NC];
-  __shared__ float4 s_r0[2][L];
+  __shared__ V s_z[2][RPB][L];
+  __shared__ V s_gl[RPB][R][L];  // gradients of local (one-record) rows
+  __shared__ V s_red[TB / NC][NC];
+  __shared__ V s_r0[2][L];
   __shared__ float s_loss[RPB];
   unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (g_trace) ts[0] = __builtin_amdgcn_s_memrealtime();
@@ -711,8 +791,8 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
   // the previous launch was a full batch: its NBF workgroups all stored
   // (none for the first batch of an epoch: row 0 from the table)
   const int np = q ? NBF : 0;
-  Row0Loads<L, TB, NBFM> r0l;
-  row0_issue<L, TB, NBFM>(a, q, np, r0l);
+  Row0Loads<L, VW, TB, NBFM> r0l;
+  row0_issue<L, VW, TB, NBFM>(a, q, np, r0l);
   {
 #pragma unroll
     for (int s = 0; s < R + kFX; s++) {
@@ -755,16 +835,16 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
   if (nval > 0) {
     // staged before the gathers: frees the partials' registers (and waits
     // for round trip 1 before the branchy gather issue)
-    row0_stage<L, TB, NBFM>(np, r0l, s_red);
-    float4 p0 = r0l.rp, a0 = r0l.ra;
-    asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(a0.x),
-                 "+v"(a0.y), "+v"(a0.z), "+v"(a0.w));
+    row0_stage<L, VW, TB, NBFM>(np, r0l, s_red);
+    V p0 = r0l.rp, a0 = r0l.ra;
+    S::pin(p0);
+    S::pin(a0);
     // round trip 2: every slot's table row and the accumulator row where
     // this slot owns the row's update (else the hot row 0; a pending slot's
     // rows are replaced by the previous batch's shadow below). List slots
     // are skipped by a WAVE-uniform branch when no record of the wave has a
     // list.
-    float4 Pv[R], Av[R];
+    V Pv[R], Av[R];
     bool lists = false;
 #pragma unroll
     for (int s = 4; s < R; s++) lists |= row[s] != 0;
@@ -774,8 +854,8 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
     // 0.6 us per batch)
     auto gather = [&](int s) {
       const bool edge = slot_is_edge(s, K);
-      const float4 *T = reinterpret_cast<const float4 *>(edge ? a.etab : a.ntab);
-      const float4 *Ac = reinterpret_cast<const float4 *>(edge ? a.eacc : a.nacc);
+      const V *T = reinterpret_cast<const V *>(edge ? a.etab : a.ntab);
+      const V *Ac = reinterpret_cast<const V *>(edge ? a.eacc : a.nacc);
       const int arow = (code[s] & kSOwn) ? row[s] : 0;
       Pv[s] = T[(size_t)row[s] * L + lane];
       Av[s] = Ac[(size_t)arow * L + lane];
@@ -785,7 +865,7 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
       // at L = 64 (one record per wave, scalar ids) the two padding slots of
       // the first four are skipped: their value comes from s_r0 below
       if (L == 64 && row[s] == 0) {
-        Pv[s] = Av[s] = f4(0.f);
+        Pv[s] = Av[s] = S::zero();
         continue;
       }
       gather(s);
@@ -799,23 +879,21 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
     // (no default values: a conditional assignment over a default makes the
     // compiler copy the loaded registers at the join, i.e. wait for them and
     // drain every gather before the barrier)
-    float4 fp, fa;
-    longlong2 fga, fgb;
+    V fp, fa;
+    typename S::Fx fg;
     if (__any(frow[0] != 0)) {
       const int mf = (fcode[0] >> kDefBits) & kDefMask;
-      fp = sh_row<L>(a, ppar, mf, 0)[lane];
-      fa = sh_row<L>(a, ppar, mf, 1)[lane];
-      const longlong2 *g = gacc_row<L>(a, ppar, mf);
-      fga = g[2 * lane];
-      fgb = g[2 * lane + 1];
+      fp = sh_row<L, VW>(a, ppar, mf, 0)[lane];
+      fa = sh_row<L, VW>(a, ppar, mf, 1)[lane];
+      fg = S::ldfix(gacc_row<L, VW>(a, ppar, mf), lane);
     }
     __syncthreads();  // s_red
     if (sub == 0) {
-      row0_finish<L, TB, NBFM>(a, s_red, p0, a0);
+      row0_finish<L, VW, TB, NBFM>(a, s_red, p0, a0);
       s_r0[tab0][c0] = p0;
       if (blockIdx.x == 0) {
-        sh_row<L>(a, par, tab0, 0)[c0] = p0;
-        sh_row<L>(a, par, tab0, 1)[c0] = a0;
+        sh_row<L, VW>(a, par, tab0, 0)[c0] = p0;
+        sh_row<L, VW>(a, par, tab0, 1)[c0] = a0;
       }
     }
     __syncthreads();  // s_r0
@@ -823,10 +901,10 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
     // flush slot 0: folded and written back now (its registers are free
     // for the forward pass; nothing of this batch reads the row)
     if (has && frow[0] != 0) {
-      fold4(fp, fa, fga, fgb, a.lr, a.eps);
+      fold<VW>(fp, fa, fg, a.lr, a.eps);
       const bool fe = fcode[0] & kFEdge;
-      tab_row<L>(a, fe, 0, frow[0])[lane] = fp;
-      tab_row<L>(a, fe, 1, frow[0])[lane] = fa;
+      tab_row<L, VW>(a, fe, 0, frow[0])[lane] = fp;
+      tab_row<L, VW>(a, fe, 1, frow[0])[lane] = fa;
     }
     // pending slots (rows deferred by the previous batch): base row from the
     // previous batch's shadow, folded with its gacc sum, written to every
@@ -848,9 +926,8 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
       for (int s = 0; s < R; s++)
         if (s == ps) cd = code[s];
       const unsigned mp = (cd >> kDefBits) & kDefMask;
-      const longlong2 *g = gacc_row<L>(a, ppar, mp);
-      const longlong2 ga = g[2 * lane], gb2 = g[2 * lane + 1];
-      float4 pp = sh_row<L>(a, ppar, mp, 0)[lane], aa = sh_row<L>(a, ppar, mp, 1)[lane];
+      const typename S::Fx gg = S::ldfix(gacc_row<L, VW>(a, ppar, mp), lane);
+      V pp = sh_row<L, VW>(a, ppar, mp, 0)[lane], aa = sh_row<L, VW>(a, ppar, mp, 1)[lane];
       // the record's slots naming the same entry (a mask: the write-back
       // below is one bit test per slot)
       unsigned wm = 0;
@@ -858,7 +935,7 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
       for (int s = 0; s < R; s++)
         if (((code[s] >> kDefBits) & kDefMask) == mp) wm |= 1u << s;
       wm &= pm;
-      fold4(pp, aa, ga, gb2, a.lr, a.eps);
+      fold<VW>(pp, aa, gg, a.lr, a.eps);
 #pragma unroll
       for (int s = 0; s < R; s++)
         if ((wm >> s) & 1u) {
@@ -875,10 +952,9 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
         for (int s = 0; s < R; s++) {
           if (!__any((pm >> s) & 1u)) continue;
           const int mp = (code[s] >> kDefBits) & kDefMask;
-          const longlong2 *g = gacc_row<L>(a, ppar, mp);
-          const longlong2 ga = g[2 * lane], gb2 = g[2 * lane + 1];
-          float4 pp = sh_row<L>(a, ppar, mp, 0)[lane], aa = sh_row<L>(a, ppar, mp, 1)[lane];
-          fold4(pp, aa, ga, gb2, a.lr, a.eps);
+          const typename S::Fx gg = S::ldfix(gacc_row<L, VW>(a, ppar, mp), lane);
+          V pp = sh_row<L, VW>(a, ppar, mp, 0)[lane], aa = sh_row<L, VW>(a, ppar, mp, 1)[lane];
+          fold<VW>(pp, aa, gg, a.lr, a.eps);
           if ((pm >> s) & 1u) {
             Pv[s] = pp;
             Av[s] = aa;
@@ -886,20 +962,20 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
         }
       }
     }
-    float4 zN = f4(0.f), zE = f4(0.f);
+    V zN = S::zero(), zE = S::zero();
     float lrec = 0.f;
     if (has) {
 #pragma unroll
       for (int s = 0; s < R; s++)
         if (row[s] == 0) Pv[s] = s_r0[slot_is_edge(s, K) ? 1 : 0][lane];
       const float inv_b = 1.0f / (float)nb;
-      const float4 &Nl = Pv[0], &El = Pv[1], &Nr = Pv[2], &Er = Pv[3];
-      float z1 = group_sum<L>(dot4(Nl, Nr)), z2 = group_sum<L>(dot4(El, Er));
+      const V &Nl = Pv[0], &El = Pv[1], &Nr = Pv[2], &Er = Pv[3];
+      float z1 = group_sum<L>(S::dot(Nl, Nr)), z2 = group_sum<L>(S::dot(El, Er));
       float za[K], zb[K];
 #pragma unroll
       for (int k = 0; k < K; k++) {
-        za[k] = group_sum<L>(dot4(Pv[4 + k], Nl));
-        zb[k] = group_sum<L>(dot4(Pv[4 + K + k], Er));
+        za[k] = group_sum<L>(S::dot(Pv[4 + k], Nl));
+        zb[k] = group_sum<L>(S::dot(Pv[4 + K + k], Er));
       }
       const int act = MODE == 1 ? 0 : 1;
       const int lossk = MODE == 1 ? 0 : 1;
@@ -927,55 +1003,55 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
       const float dz1 = g1 * act_d(act, z1, y1);
       const float dz2 = g2 * act_d(act, z2, y2);
       const float dP = g3 * Q / (float)K, dQ = g3 * P / (float)K;
-      auto emit = [&](int s, float4 g) {
+      auto emit = [&](int s, V g) {
         const unsigned cd = code[s];
         const bool edge = slot_is_edge(s, K);
         if (row[s] == 0) {
-          if (edge) zE = zE + g;
-          else zN = zN + g;
+          if (edge) zE = S::add(zE, g);
+          else zN = S::add(zN, g);
         } else if (cd & kSLocal) {
           // one record's slots of a row, summed in emit order in LDS (the
           // wave's own accesses, in order); the last one (owner) updates
-          float4 *acc = &s_gl[grp][cd & 15u][lane];
+          V *acc = &s_gl[grp][cd & 15u][lane];
           if (cd & kSOwn) {
-            float4 pv = Pv[s], av = Av[s];
-            adagrad4_hw(pv, av, *acc + g, a.lr, a.eps);
-            tab_row<L>(a, edge, 0, row[s])[lane] = pv;
-            tab_row<L>(a, edge, 1, row[s])[lane] = av;
+            V pv = Pv[s], av = Av[s];
+            S::adagrad(pv, av, S::add(*acc, g), a.lr, a.eps);
+            tab_row<L, VW>(a, edge, 0, row[s])[lane] = pv;
+            tab_row<L, VW>(a, edge, 1, row[s])[lane] = av;
           } else {
-            *acc = (cd & kSFirst) ? g : *acc + g;
+            *acc = (cd & kSFirst) ? g : S::add(*acc, g);
           }
         } else if (cd & kSShared) {
           const int m = cd & kDefMask;
           if (g_tab & 1024)  // (debug ablation: plain stores, wrong sums)
-            reinterpret_cast<float4 *>(gacc_row<L>(a, par, m))[lane] = g;
+            reinterpret_cast<V *>(gacc_row<L, VW>(a, par, m))[lane] = g;
           else
-            fix_add4(reinterpret_cast<long long *>(gacc_row<L>(a, par, m) + 2 * lane), g, bad);
+            S::addfix(gacc_row<L, VW>(a, par, m), lane, g, bad);
           if (cd & kSOwn) {
-            sh_row<L>(a, par, m, 0)[lane] = Pv[s];
-            sh_row<L>(a, par, m, 1)[lane] = Av[s];
+            sh_row<L, VW>(a, par, m, 0)[lane] = Pv[s];
+            sh_row<L, VW>(a, par, m, 1)[lane] = Av[s];
           }
         } else {
-          float4 pv = Pv[s], av = Av[s];
-          adagrad4_hw(pv, av, g, a.lr, a.eps);
-          tab_row<L>(a, edge, 0, row[s])[lane] = pv;
-          tab_row<L>(a, edge, 1, row[s])[lane] = av;
+          V pv = Pv[s], av = Av[s];
+          S::adagrad(pv, av, g, a.lr, a.eps);
+          tab_row<L, VW>(a, edge, 0, row[s])[lane] = pv;
+          tab_row<L, VW>(a, edge, 1, row[s])[lane] = av;
         }
       };
-      float4 gln = fma4(dz1, Nr, f4(0.f)), gre = fma4(dz2, El, f4(0.f));
+      V gln = S::fma(dz1, Nr, S::zero()), gre = S::fma(dz2, El, S::zero());
 #pragma unroll
       for (int k = 0; k < K; k++) {
         const float da = dP * act_d(act, za[k], sa[k]);
         const float db = dQ * act_d(act, zb[k], sb[k]);
-        gln = fma4(da, Pv[4 + k], gln);
-        gre = fma4(db, Pv[4 + K + k], gre);
-        emit(4 + k, fma4(da, Nl, f4(0.f)));
-        emit(4 + K + k, fma4(db, Er, f4(0.f)));
+        gln = S::fma(da, Pv[4 + k], gln);
+        gre = S::fma(db, Pv[4 + K + k], gre);
+        emit(4 + k, S::fma(da, Nl, S::zero()));
+        emit(4 + K + k, S::fma(db, Er, S::zero()));
       }
       emit(0, gln);
       emit(3, gre);
-      emit(2, fma4(dz1, Nl, f4(0.f)));
-      emit(1, fma4(dz2, Er, f4(0.f)));
+      emit(2, S::fma(dz1, Nl, S::zero()));
+      emit(1, S::fma(dz2, Er, S::zero()));
       HGX_STAMP(ts[4]);
     }
     s_z[0][grp][lane] = zN;
@@ -984,9 +1060,9 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
     __syncthreads();
     // this batch's row-0 partial: the workgroup's fixed-order sum
     if (threadIdx.x < NC) {
-      float4 sz = f4(0.f);
-      for (int g = 0; g < RPB; g++) sz = sz + s_z[tab0][g][c0];
-      reinterpret_cast<float4 *>(a.gp)[((size_t)(q & 1) * NBFM + blockIdx.x) * NC + col] = sz;
+      V sz = S::zero();
+      for (int g = 0; g < RPB; g++) sz = S::add(sz, s_z[tab0][g][c0]);
+      reinterpret_cast<V *>(a.gp)[((size_t)(q & 1) * NBFM + blockIdx.x) * NC + col] = sz;
     }
     if (threadIdx.x == 0) {
       float sl = 0.f;
@@ -1001,7 +1077,7 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
 #pragma unroll
       for (int f = 1; f < kFX; f++)
         if (frow[f] != 0)
-          flush_row<L>(a, ppar, (fcode[f] & kFEdge ? 1 << 30 : 0) | frow[f],
+          flush_row<L, VW>(a, ppar, (fcode[f] & kFEdge ? 1 << 30 : 0) | frow[f],
                        (fcode[f] >> kDefBits) & kDefMask, lane);
     }
   }
@@ -1009,13 +1085,13 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
   // flush overflow list (rare: more deferred rows than kFX per record)
   for (int e = blockIdx.x * RPB + grp; e < nfo; e += NBF * RPB) {
     const int2 en = a.pfo[(size_t)cb * a.Mmax + e];
-    flush_row<L>(a, ppar, en.x, en.y, lane);
+    flush_row<L, VW>(a, ppar, en.x, en.y, lane);
   }
   // zero the gacc parity the next batch adds into (its deferred entries
   // [2, 2 + zc) were used two batches ago)
   {
-    longlong2 *z = gacc_row<L>(a, zpar, 2);
-    const int tot = zc * 2 * L;
+    longlong2 *z = reinterpret_cast<longlong2 *>(gacc_row<L, VW>(a, zpar, 2));
+    const int tot = zc * (VW / 2) * L;
     for (int i = blockIdx.x * TB + threadIdx.x; i < tot; i += NBF * TB)
       z[i] = make_longlong2(0, 0);
   }
@@ -1047,18 +1123,17 @@ __global__ __launch_bounds__(256) void train_flush(TrainArgs a, const int *keys,
         for (int w = sub; w < np; w += TPC) gs = gs + gp[(size_t)w * 2 * L + lane];
         g = g + gs;
       }
-      float4 p = sh_row<L>(a, par, e, 0)[lane], ac = sh_row<L>(a, par, e, 1)[lane];
+      float4 p = sh_row<L, 4>(a, par, e, 0)[lane], ac = sh_row<L, 4>(a, par, e, 1)[lane];
       adagrad4_hw(p, ac, g, a.lr, a.eps);
-      tab_row<L>(a, e, 0, 0)[lane] = p;
-      tab_row<L>(a, e, 1, 0)[lane] = ac;
+      tab_row<L, 4>(a, e, 0, 0)[lane] = p;
+      tab_row<L, 4>(a, e, 1, 0)[lane] = ac;
       continue;
     }
-    flush_row<L>(a, par, keys[e - 2], e, lane);
-    longlong2 *g = gacc_row<L>(a, par, e);
-    g[2 * lane] = g[2 * lane + 1] = make_longlong2(0, 0);
+    flush_row<L, 4>(a, par, keys[e - 2], e, lane);
+    SV<4>::zerofix(gacc_row<L, 4>(a, par, e), lane);
   }
 
-  longlong2 *z = gacc_row<L>(a, opar, 2);
+  longlong2 *z = reinterpret_cast<longlong2 *>(gacc_row<L, 4>(a, opar, 2));
   for (int i = blockIdx.x * 256 + threadIdx.x; i < zc * 2 * L; i += gridDim.x * 256)
     z[i] = make_longlong2(0, 0);
 }
@@ -1535,34 +1610,46 @@ KFn fwd_for(int K, int loss, int act, int tb1) {
 using KStepFn = void (*)(TrainArgs, int, int, int, int);
 using KFlushFn = void (*)(TrainArgs, const int *, const int *, const int *, int, int);
 
-// deferred-row step: d in (64, 256] (one float4 per lane, L = 32 or 64),
-// K = 5 with the FOBE (sigmoid/KLD) or HOBE (relu/MSE) heads. tb = the
-// workgroup size (records per workgroup = tb / L); nbfm = the workgroup cap
-// of the instantiation (every workgroup loads nbfm / (tb / 2L) row-0
-// partials per thread).
-template <int L, int TB, int NBFM>
+// deferred-row step: d in (64, 256], K = 5 with the FOBE (sigmoid/KLD) or
+// HOBE (relu/MSE) heads. One SL-lane group per record with VW floats per lane
+// (dp = SL VW): float4 x 32 lanes or float2 x 64 lanes for dp = 128, float4 x
+// 64 lanes for dp = 256. tb = the workgroup size (records per workgroup =
+// tb / SL); nbfm = the workgroup cap of the instantiation (every workgroup
+// loads nbfm / (tb / 2 SL) row-0 partials per thread). The flush kernel views
+// rows as float4 and sums the row-0 partials in the step's order (its TPC).
+template <int SL, int VW, int TB, int NBFM>
 void step_fns(int loss, KStepFn *kf, KFlushFn &kfl) {
-  kf[0] = loss == 0 ? train_step<L, 5, 1, TB, NBFM, false> : train_step<L, 5, 2, TB, NBFM, false>;
-  kf[1] = loss == 0 ? train_step<L, 5, 1, TB, NBFM, true> : train_step<L, 5, 2, TB, NBFM, true>;
-  kfl = train_flush<L, NBFM, TB / (2 * L)>;
+  kf[0] = loss == 0 ? train_step<SL, VW, 5, 1, TB, NBFM, false>
+                    : train_step<SL, VW, 5, 2, TB, NBFM, false>;
+  kf[1] = loss == 0 ? train_step<SL, VW, 5, 1, TB, NBFM, true>
+                    : train_step<SL, VW, 5, 2, TB, NBFM, true>;
+  kfl = train_flush<SL * VW / 4, NBFM, TB / (2 * SL)>;
 }
-bool pick_step(int L, int VPL, int K, int loss, int act, int batch, int &tb, int &nbfm,
-               KStepFn *kf, KFlushFn &kfl) {
+// lanes = the tuning (0 auto, 32 or 64 lanes per record where dp = 128);
+// sets sl (the step's lanes per record), tb, nbfm and the kernels
+bool pick_step(int L, int VPL, int K, int loss, int act, int batch, int lanes, int &sl,
+               int &tb, int &nbfm, KStepFn *kf, KFlushFn &kfl) {
   if (VPL != 1 || K != 5 || loss != act) return false;
-  // measured r02 (tools/ab_train.py, interleaved): d=128 L=32 at 128
-  // threads 7.92 / 8.27 us per batch (random / C3 HOBE records) vs 8.33 / 8.75
-  // at 256; d=256 L=64 at 256 threads
-  if (L == 32) tb = tb == 256 ? 256 : 128;
-  else if (L == 64) tb = 256;
-  else return false;
-  const int nbf = (batch + tb / L - 1) / (tb / L);
+  if (L != 32 && L != 64) return false;
+  // dp = 128, measured r02 (tools/ab_train.py, interleaved, us per batch on
+  // random / C3 HOBE records): float2 x 64 lanes at 256 threads 7.63 / 7.79;
+  // float4 x 32 lanes at 128 threads 8.07 / 8.42 (8.33 / 8.75 at 256)
+  const int vw = L == 32 && lanes != 32 ? 2 : 4;
+  sl = L * 4 / vw;
+  if (sl == 32) tb = tb == 256 ? 256 : 128;
+  else if (vw == 2) tb = tb == 512 ? 512 : 256;
+  else tb = 256;
+  const int nbf = (batch + tb / sl - 1) / (tb / sl);
   nbfm = nbf <= 32 ? 32 : 64;
   if (nbf > nbfm) return false;
-  if (L == 32) {
-    if (tb == 128) nbfm == 32 ? step_fns<32, 128, 32>(loss, kf, kfl) : step_fns<32, 128, 64>(loss, kf, kfl);
-    else nbfm == 32 ? step_fns<32, 256, 32>(loss, kf, kfl) : step_fns<32, 256, 64>(loss, kf, kfl);
+  if (sl == 32) {
+    if (tb == 128) nbfm == 32 ? step_fns<32, 4, 128, 32>(loss, kf, kfl) : step_fns<32, 4, 128, 64>(loss, kf, kfl);
+    else nbfm == 32 ? step_fns<32, 4, 256, 32>(loss, kf, kfl) : step_fns<32, 4, 256, 64>(loss, kf, kfl);
+  } else if (vw == 2) {
+    if (tb == 512) nbfm == 32 ? step_fns<64, 2, 512, 32>(loss, kf, kfl) : step_fns<64, 2, 512, 64>(loss, kf, kfl);
+    else nbfm == 32 ? step_fns<64, 2, 256, 32>(loss, kf, kfl) : step_fns<64, 2, 256, 64>(loss, kf, kfl);
   } else {
-    nbfm == 32 ? step_fns<64, 256, 32>(loss, kf, kfl) : step_fns<64, 256, 64>(loss, kf, kfl);
+    nbfm == 32 ? step_fns<64, 4, 256, 32>(loss, kf, kfl) : step_fns<64, 4, 256, 64>(loss, kf, kfl);
   }
   return true;
 }
@@ -1883,12 +1970,13 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   // batch of the run then takes it); else the two-kernel step for every batch
   KStepFn kf[2] = {nullptr, nullptr};  // light / MULTI pending-slot forms
   KFlushFn kfl = nullptr;
-  int tbf = env_int("HGX_STEP_TB", 0);  // workgroup size (debug builds)
-  int NBFM = 0;
+  int tbf = ctx->tune.train_tb;  // workgroup size (0: per geometry)
+  int NBFM = 0, SL = 0;
   const bool fused = ctx->tune.train_fused && env_int("HGX_TRAIN_GENERIC", 0) != 1 &&
                      batch <= kPackB &&
-                     pick_step(L, VPL, K, loss, act, batch, tbf, NBFM, kf, kfl);
-  const int prpb = fused ? tbf / L : 0;
+                     pick_step(L, VPL, K, loss, act, batch, ctx->tune.train_lanes, SL, tbf,
+                               NBFM, kf, kfl);
+  const int prpb = fused ? tbf / SL : 0;
   const int NBF = fused ? (batch + prpb - 1) / prpb : 0;
   const int RW = R + kWX;
   const int Mmax = SB / 2 + 1;        // deferred rows per batch: <= SB / 2

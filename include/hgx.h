@@ -60,6 +60,10 @@ int hgx_synchronize(hgx_ctx *ctx);
  *                      (Karp-Luby), 2 uniform columns
  *   "train_fused"      1 fused one-launch batch step (default), 0 the
  *                      two-kernel step for every batch
+ *   "train_lanes"      fused step at padded d = 128: lanes per record
+ *                      (0 auto = 64, 32 = float4 per lane, 64 = float2)
+ *   "train_tb"         fused step workgroup size (0 auto, 128, 256, 512;
+ *                      a size the geometry has no form for -> its default)
  *   "alg_long"         alg-dist long-row threshold (0 = 512, else >= 64)
  *   "alg_ks"           alg-dist coordinate row width in floats (0 = auto)
  * Unknown keys and out-of-range values -> HGX_EINVAL. */

@@ -55,6 +55,19 @@ def _run_both(ctx, idx, tgt, K, d, loss, act, batch, epochs, seed=0,
   return (ont, oet, olosses), (gnt, get_, glosses), (nt, et)
 
 
+@pytest.fixture(params=[(32, 0), (64, 0), (64, 512)],
+                ids=["lanes32", "lanes64", "lanes64-tb512"])
+def lanes(ctx, request):
+  """The fused step's geometry at padded d = 128: float4 x 32 lanes or float2
+  x 64 lanes per record (tunings train_lanes / train_tb; d = 256 ignores the
+  lanes, takes its 256-thread form)."""
+  ctx.set_tuning("train_lanes", request.param[0])
+  ctx.set_tuning("train_tb", request.param[1])
+  yield request.param
+  ctx.set_tuning("train_lanes", 0)
+  ctx.set_tuning("train_tb", 0)
+
+
 def _check(o, g, init):
   ont, oet, ol = o
   gnt, get_, gl = g
@@ -69,7 +82,7 @@ def _check(o, g, init):
 
 
 @pytest.mark.parametrize("d,batch", [(8, 64), (16, 256), (128, 256), (5, 37)])
-def test_train_hobe_records_vs_oracle(ctx, d, batch):
+def test_train_hobe_records_vs_oracle(ctx, d, batch, lanes):
   z = golden("hobe_small.npz")
   o, g, init = _run_both(ctx, z["idx"], z["tgt"], int(z["K"]), d, O.LOSS_MSE,
                          O.ACT_RELU, batch, epochs=3)
@@ -164,8 +177,7 @@ def _mixed_reuse_records(rs, nb, B, K, hub_batches, wide=20000):
 
 @pytest.mark.parametrize("d,loss,act", [(128, O.LOSS_MSE, O.ACT_RELU),
                                         (256, O.LOSS_KLD, O.ACT_SIGMOID)])
-def test_fused_step_mixed_runs_vs_oracle_and_split(ctx, d, loss, act,
-                                                   monkeypatch):
+def test_fused_step_mixed_runs_vs_oracle_and_split(ctx, d, loss, act, lanes):
   """The one-launch deferred-row step (train_step) against the oracle and
   the two-kernel step. Hub batches (every id from 5 rows) make nearly every
   row of the batch a deferred row; consecutive hub batches chain them
@@ -206,7 +218,7 @@ def test_fused_step_mixed_runs_vs_oracle_and_split(ctx, d, loss, act,
     assert np.abs(a - b).max() < 1e-6
 
 
-def test_fused_step_bitwise_deterministic(ctx):
+def test_fused_step_bitwise_deterministic(ctx, lanes):
   rs = np.random.RandomState(3)
   idx, tgt = _mixed_reuse_records(rs, 20, 256, 5, hub_batches=set())
   ctx.records_set(idx, tgt)
@@ -221,7 +233,7 @@ def test_fused_step_bitwise_deterministic(ctx):
   assert np.array_equal(out[0][1], out[1][1])
 
 
-def test_step_flush_overflow_and_pending_chains_vs_oracle(ctx):
+def test_step_flush_overflow_and_pending_chains_vs_oracle(ctx, lanes):
   """Batch 0: 128 ne records with distinct rows, each twice (1536 rows with
   exactly two slots: all deferred); batch 1 touches none of them, so it
   flushes more rows than its 4 flush slots per record hold (the overflow
