@@ -52,6 +52,9 @@ PMC_TRAIN = os.path.join(ROOT, "profiles", "r02_step_pmc_train.json")
 def parse():
   p = argparse.ArgumentParser()
   p.add_argument("--gpus", type=int, default=1)
+  p.add_argument("--edge-ranges", type=int, default=4,
+                 help="C4 sharded alg-dist: edge ranges the exchange is "
+                      "pipelined over (1 = one all-reduce per iteration)")
   p.add_argument("--steps", type=int, default=3)
   p.add_argument("--warmup", type=int, default=1)
   p.add_argument("--dim", type=int, default=128)
@@ -373,9 +376,12 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
   b_iter4 = 8.0 * big.nnz + (8.0 + 12.0 * k) * (big.N + big.E)
   exch4 = {}
   if world > 1:
-    alg_dist_sharded(ctx, big, bx0, by0, 2)  # warm
+    # exchange pipelined over edge ranges (all-reduce of range r overlaps
+    # the partials of range r + 1)
+    alg_dist_sharded(ctx, big, bx0, by0, 2, edge_ranges=args.edge_ranges)
     ms4 = max_over_ranks(alg_dist_sharded(ctx, big, bx0, by0, args.alg_iters,
-                                          stats=exch4)[2])
+                                          stats=exch4,
+                                          edge_ranges=args.edge_ranges)[2])
     ctx.upload(big)  # HOBE below runs on the whole graph of this rank
   else:
     ctx.alg_set(bx0, by0)

@@ -56,6 +56,8 @@ SIGNATURES = {
     "hgx_alg_shard_edge_final": (_int, [_vp, _int]),
     "hgx_alg_shard_end": (_int, [_vp]),
     "hgx_alg_shard_wire": (_int, [_vp, _vp, _i64, _vp]),
+    "hgx_alg_shard_ranges": (_int, [_vp, _int, _vp]),
+    "hgx_alg_shard_edge_partial_range": (_int, [_vp, _int, _int]),
     "hgx_hobe_probs": (_int, [_vp, _int, _i64, _vp, _vp, _vp]),
     "hgx_incidence_weights": (_int, [_vp, _int, ctypes.c_double, _vp, _vp]),
     "hgx_sample_fobe": (_int, [_vp, _u64, _int, _vp, _vp, _vp, _vp, _pi64]),
@@ -255,6 +257,15 @@ class Context:
 
   def alg_shard_edge_partial(self, it):
     self._chk(lib().hgx_alg_shard_edge_partial(self.h, it))
+
+  def alg_shard_ranges(self, n):
+    """Split the local edge rows into n ranges; returns the n + 1 bounds."""
+    b = np.zeros(n + 1, np.int32)
+    self._chk(lib().hgx_alg_shard_ranges(self.h, n, _ptr(b)))
+    return b
+
+  def alg_shard_edge_partial_range(self, it, r):
+    self._chk(lib().hgx_alg_shard_edge_partial_range(self.h, it, r))
 
   def alg_shard_edge_final(self, it):
     self._chk(lib().hgx_alg_shard_edge_final(self.h, it))

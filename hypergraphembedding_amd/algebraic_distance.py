@@ -75,7 +75,7 @@ def shard_rows(rp, world, rank):
 
 
 def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None,
-                     compact=True, stats=None):
+                     compact=True, stats=None, edge_ranges=1):
   """Node-row-sharded relaxation; the caller's process group does the
   exchange. Every rank must call it with the same inputs. Returns the node
   rows this rank owns (row0, row1, x_own) and all edge coords, already
@@ -87,8 +87,12 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None,
   all-reduce of the min/max words. With `compact` only the edges whose
   incidences sit on two or more ranks are exchanged, as k + 1 floats
   (hgx_alg_shard_wire); an edge private to one rank is finished there and
-  gathered once after the last iteration. `stats` (a dict) receives the
-  exchanged bytes per iteration.
+  gathered once after the last iteration. With `edge_ranges` > 1 the edge
+  partials are computed range by range (hgx_alg_shard_ranges: the same split
+  on every rank) and each range's exchange is issued asynchronously as soon
+  as its partials are queued, so the all-reduce of range r overlaps the
+  partials of range r + 1; edge_final waits for all of them. `stats` (a
+  dict) receives the exchanged bytes per iteration.
 
   `ctx` is a libhgx Context (exchange buffers on its GPU, RCCL) or any
   object with the same alg_shard_* protocol; with device=cpu the exchange
@@ -141,6 +145,15 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None,
     assert ks_lib == ks
     if compact:
       ctx.alg_shard_wire(wire.data_ptr() if n_shared else None, n_shared, slot)
+    segs = [exch]
+    if edge_ranges > 1:
+      b = ctx.alg_shard_ranges(edge_ranges).astype(np.int64)
+      if compact:
+        # wire rows are the shared edges in id order
+        first = np.concatenate([[0], np.cumsum(slot >= 0)])[b] * (k + 1)
+      else:
+        first = b * ks
+      segs = [exch[int(first[r]):int(first[r + 1])] for r in range(edge_ranges)]
     if on_gpu:
       start = torch.cuda.Event(enable_timing=True)
       end = torch.cuda.Event(enable_timing=True)
@@ -149,9 +162,19 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None,
     with torch.cuda.stream(stream) if on_gpu else contextlib.nullcontext():
       for it in range(iterations):
         ctx.alg_shard_node(it)
-        ctx.alg_shard_edge_partial(it)
-        if exch.numel():
-          dist.all_reduce(exch, op=dist.ReduceOp.SUM, group=group)
+        if edge_ranges > 1:
+          works = []
+          for r, seg in enumerate(segs):
+            ctx.alg_shard_edge_partial_range(it, r)
+            if seg.numel():
+              works.append(dist.all_reduce(seg, op=dist.ReduceOp.SUM,
+                                           group=group, async_op=True))
+          for w in works:
+            w.wait()
+        else:
+          ctx.alg_shard_edge_partial(it)
+          if exch.numel():
+            dist.all_reduce(exch, op=dist.ReduceOp.SUM, group=group)
         ctx.alg_shard_edge_final(it)
         dist.all_reduce(mm[it * M:(it + 1) * M], op=dist.ReduceOp.MAX,
                         group=group)
@@ -175,6 +198,7 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None,
     mm_bytes = M * 4
     stats.update(
         exchange="compact" if compact else "dense",
+        edge_ranges=int(edge_ranges),
         shared_edges=int(n_shared) if compact else inc.E,
         partial_bytes_per_iter=int(exch.numel()) * 4,
         dense_partial_bytes_per_iter=inc.E * ks * 4,

@@ -860,14 +860,14 @@ __global__ __launch_bounds__(kBlock) void algdist_edge_final(
 
 // Compact exchange: the shared edges' partial rows [sum w, sum w x_1..k]
 // (k + 1 floats, no padding slot) gathered onto the wire.
-__global__ void algdist_wire_pack(int E, int KS, int k,
+__global__ void algdist_wire_pack(int e0, int E, int KS, int k,
                                   const int *__restrict__ slot,
                                   const float *__restrict__ part,
                                   float *__restrict__ wire) {
   const int64_t total = (int64_t)E * (k + 1);
   for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < total;
        q += (int64_t)gridDim.x * blockDim.x) {
-    const int e = (int)(q / (k + 1)), i = (int)(q % (k + 1));
+    const int e = e0 + (int)(q / (k + 1)), i = (int)(q % (k + 1));
     const int s = slot[e];
     if (s >= 0) wire[(int64_t)s * (k + 1) + i] = part[(int64_t)e * KS + i];
   }
@@ -1466,7 +1466,64 @@ extern "C" int hgx_alg_shard_edge_partial(hgx_ctx *ctx, int it) {
   if (ctx->ext_wire && ctx->n_wire > 0) {
     hipLaunchKernelGGL(algdist_wire_pack,
                        dim3(grid_for((int64_t)ctx->E * (ctx->k + 1), 256)),
-                       dim3(256), 0, ctx->stream, ctx->E, ctx->ks, ctx->k,
+                       dim3(256), 0, ctx->stream, 0, ctx->E, ctx->ks, ctx->k,
+                       ctx->wire_slot.as<int>(), ctx->ext_partial, ctx->ext_wire);
+    HGX_LAUNCH_CHECK(ctx);
+  }
+  return HGX_OK;
+}
+
+// Edge-range pipelining: the caller all-reduces the wire rows of range r
+// while the partials of range r + 1 are computed (both ranges' rows are
+// disjoint in `partial` and on the wire).
+extern "C" int hgx_alg_shard_ranges(hgx_ctx *ctx, int n, int32_t *bounds) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->ext_mm, HGX_ESTATE, "hgx_alg_shard_begin not called");
+  HGX_CHECK(ctx, n >= 1 && n <= hgx_ctx::kMaxEdgeRanges && bounds, HGX_EINVAL,
+            "edge ranges %d outside [1,%d] or null bounds", n,
+            hgx_ctx::kMaxEdgeRanges);
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  std::vector<int> rpl(ctx->E + 1), rpg(ctx->E + 1);
+  HGX_HIP(ctx, hipMemcpy(rpl.data(), ctx->rp_el.p, sizeof(int) * (ctx->E + 1),
+                         hipMemcpyDeviceToHost));
+  HGX_HIP(ctx, hipMemcpy(rpg.data(), ctx->rp_e.p, sizeof(int) * (ctx->E + 1),
+                         hipMemcpyDeviceToHost));
+  // contiguous edge ranges balanced by ALL incidences (the global edge CSR),
+  // so every rank gets the same split and the same wire slices
+  const int64_t tot = rpg[ctx->E];
+  ctx->elr_bound[0] = 0;
+  for (int r = 1; r < n; r++) {
+    const int64_t want = tot * r / n;
+    int e = (int)(std::lower_bound(rpg.begin(), rpg.end(), (int)want) -
+                  rpg.begin());
+    ctx->elr_bound[r] = std::max(ctx->elr_bound[r - 1], std::min(e, ctx->E));
+  }
+  ctx->elr_bound[n] = ctx->E;
+  for (int r = 0; r < n; r++)
+    HGX_TRY(hgx_make_long_rows(ctx, rpl.data(), ctx->elr_bound[r],
+                               ctx->elr_bound[r + 1], ctx->long_elr[r]));
+  ctx->n_elr = n;
+  for (int r = 0; r <= n; r++) bounds[r] = ctx->elr_bound[r];
+  return HGX_OK;
+}
+
+extern "C" int hgx_alg_shard_edge_partial_range(hgx_ctx *ctx, int it, int r) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->ext_mm && it >= 0 && it < ctx->ext_iters, HGX_ESTATE,
+            "shard iteration %d out of order", it);
+  HGX_CHECK(ctx, r >= 0 && r < ctx->n_elr, HGX_EINVAL,
+            "edge range %d outside [0,%d)", r, ctx->n_elr);
+  const int e0 = ctx->elr_bound[r], e1 = ctx->elr_bound[r + 1];
+  float *xn = ctx->X[ctx->xcur ^ 1].as<float>();
+  const double avg = (double)std::max<int64_t>(1, ctx->nnz) / ctx->E;
+  HGX_TRY(launch_half(ctx, MODE_PARTIAL, e0, e1 - e0, ctx->rp_el.as<int>(),
+                      ctx->col_el.as<int>(), nullptr, xn, ctx->ext_partial,
+                      nullptr, 0, nullptr, avg, ctx->blk_el.as<int>(),
+                      ctx->nblk_el, &ctx->long_elr[r]));
+  if (ctx->ext_wire && ctx->n_wire > 0 && e1 > e0) {
+    hipLaunchKernelGGL(algdist_wire_pack,
+                       dim3(grid_for((int64_t)(e1 - e0) * (ctx->k + 1), 256)),
+                       dim3(256), 0, ctx->stream, e0, e1 - e0, ctx->ks, ctx->k,
                        ctx->wire_slot.as<int>(), ctx->ext_partial, ctx->ext_wire);
     HGX_LAUNCH_CHECK(ctx);
   }

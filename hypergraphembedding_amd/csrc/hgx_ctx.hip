@@ -85,6 +85,8 @@ extern "C" int hgx_destroy(hgx_ctx *ctx) {
   for (DevBuf *b : bufs) hgx_release(*b);
   for (LongRows *l : {&ctx->long_n, &ctx->long_e, &ctx->long_sn, &ctx->long_el})
     for (DevBuf *b : {&l->seg, &l->off, &l->rows, &l->part}) hgx_release(*b);
+  for (LongRows &l : ctx->long_elr)
+    for (DevBuf *b : {&l.seg, &l.off, &l.rows, &l.part}) hgx_release(*b);
   if (ctx->ev0) hipEventDestroy(ctx->ev0);
   if (ctx->ev1) hipEventDestroy(ctx->ev1);
   if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);

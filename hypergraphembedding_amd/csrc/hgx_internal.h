@@ -84,6 +84,12 @@ struct hgx_ctx {
   DevBuf rp_el, col_el, blk_sn, blk_el;
   int nblk_sn = 0, nblk_el = 0;
   LongRows long_sn, long_el;
+  // edge-range pipelining of the exchange (hgx_alg_shard_ranges): local edge
+  // rows split into n_elr contiguous ranges, each with its own long rows
+  static constexpr int kMaxEdgeRanges = 16;
+  LongRows long_elr[kMaxEdgeRanges];
+  int32_t elr_bound[kMaxEdgeRanges + 1] = {};
+  int n_elr = 0;
   float *ext_partial = nullptr;  // E x ks
   // compact exchange (hgx_alg_shard_wire): shared edges' [sum w, sum w x]
   // rows of k + 1 floats; per edge its wire row (>= 0), -1 private to this

@@ -122,6 +122,16 @@ int hgx_alg_shard_end(hgx_ctx *ctx);
  * d_partial, which becomes this rank's local scratch. */
 int hgx_alg_shard_wire(hgx_ctx *ctx, void *d_wire, int64_t n_shared,
                        const int32_t *edge_slot);
+/* Exchange pipelining (optional, after begin / wire): split the edge rows
+ * into n (1..16) contiguous ranges balanced by the incidences of the whole
+ * graph, so every rank gets the same split; bounds[n + 1] receives the range
+ * starts. Then per iteration
+ * edge_partial_range(it, r) for r = 0..n-1 in place of edge_partial(it): the
+ * caller may all-reduce range r's rows (of d_partial, or its wire rows) while
+ * range r + 1 is computed, and calls edge_final(it) after all of them. The
+ * reference has one monolithic pass (algebraic_distance.py:77-95). */
+int hgx_alg_shard_ranges(hgx_ctx *ctx, int n, int32_t *bounds);
+int hgx_alg_shard_edge_partial_range(hgx_ctx *ctx, int it, int r);
 
 /* ---- HOBE probabilities ------------------------------------------------ *
  * _same_type_dist_calc (hg2v_sample.py:527-543) and DiffTypeDistanceSample

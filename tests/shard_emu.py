@@ -111,6 +111,29 @@ class ShardEmu:
       sh = self.slot >= 0
       self.wire[self.slot[sh]] = self.part[sh, :self.k + 1]
 
+  def alg_shard_ranges(self, n):
+    """hgx_alg_shard_ranges: edge ranges balanced by all incidences."""
+    rp = np.asarray(self.inc.rp_e, np.int64)
+    b = [0]
+    for r in range(1, n):
+      e = int(np.searchsorted(rp, rp[-1] * r // n, side="left"))
+      b.append(max(b[-1], min(e, self.inc.E)))
+    b.append(self.inc.E)
+    self.bounds = np.array(b, np.int32)
+    return self.bounds
+
+  def alg_shard_edge_partial_range(self, it, r):
+    inc, e0, e1 = self.inc, int(self.bounds[r]), int(self.bounds[r + 1])
+    for e in range(e0, e1):
+      c = inc.col_e[inc.rp_e[e]:inc.rp_e[e + 1]]
+      c = c[(c >= self.row0) & (c < self.row1)]
+      w = 1.0 / self.deg_n[c].astype(np.float64)
+      self.part[e, :] = 0
+      self.part[e, 0] = w.sum()
+      self.part[e, 1:self.k + 1] = (w[:, None] * self.Xn[c]).sum(0)
+      if self.slot is not None and self.slot[e] >= 0:
+        self.wire[self.slot[e]] = self.part[e, :self.k + 1]
+
   def alg_shard_edge_final(self, it):
     m, d = self._affine(it)
     P = self.part[:, :self.k + 1].copy()

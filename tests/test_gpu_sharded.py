@@ -33,7 +33,7 @@ def _graph(name):
   return powerlaw_hypergraph(N=20_000, E=10_000, seed=5)  # long edge rows
 
 
-def _worker(rank, world, port, out_path, iters, graph="tiny"):
+def _worker(rank, world, port, out_path, iters, graph="tiny", edge_ranges=1):
   import torch
   import torch.distributed as dist
   import sys
@@ -50,7 +50,8 @@ def _worker(rank, world, port, out_path, iters, graph="tiny"):
   r = O.Rng(0)
   x0, y0 = r.random((inc.N, 10)), r.random((inc.E, 10))
   ctx = _hgx.Context(0)
-  (r0, r1, xo), y, ms = alg_dist_sharded(ctx, inc, x0, y0, iters)
+  (r0, r1, xo), y, ms = alg_dist_sharded(ctx, inc, x0, y0, iters,
+                                         edge_ranges=edge_ranges)
   np.savez(out_path + f".{rank}.npz", r0=r0, r1=r1, x=xo, y=y)
   dist.barrier()
   dist.destroy_process_group()
@@ -77,11 +78,15 @@ def test_sharded_algdist_matches_reference(tmp_path, world):
   assert np.abs(ys[0] - z["y_20"]).max() <= 1e-4
 
 
-def test_sharded_algdist_powerlaw_long_rows(tmp_path):
+@pytest.mark.parametrize("ranges", [1, 4])
+def test_sharded_algdist_powerlaw_long_rows(tmp_path, ranges):
+  """ranges = 4: edge partials per range (each with its own long rows) and
+  the exchange of each range issued asynchronously."""
   import torch.multiprocessing as mp
   world, iters = 2, 10
   out = str(tmp_path / "shard")
-  mp.start_processes(_worker, args=(world, _free_port(), out, iters, "powerlaw"),
+  mp.start_processes(_worker, args=(world, _free_port(), out, iters, "powerlaw",
+                                    ranges),
                      nprocs=world, join=True, start_method="spawn")
   inc = _graph("powerlaw")
   r = O.Rng(0)
@@ -96,7 +101,7 @@ def test_sharded_algdist_powerlaw_long_rows(tmp_path):
   assert np.abs(y - yr).max() <= 1e-4
 
 
-def _nccl_worker(rank, world, port, out_path):
+def _nccl_worker(rank, world, port, out_path, edge_ranges=1):
   import torch
   import torch.distributed as dist
   import sys
@@ -114,17 +119,20 @@ def _nccl_worker(rank, world, port, out_path):
   r = O.Rng(0)
   x0, y0 = r.random((inc.N, 10)), r.random((inc.E, 10))
   ctx = _hgx.Context(0)
-  (r0, r1, xo), y, ms = alg_dist_sharded(ctx, inc, x0, y0, 20)
+  (r0, r1, xo), y, ms = alg_dist_sharded(ctx, inc, x0, y0, 20,
+                                         edge_ranges=edge_ranges)
   np.savez(out_path, r0=r0, r1=r1, x=xo, y=y)
   dist.destroy_process_group()
 
 
-def test_sharded_algdist_rccl_single_rank(tmp_path):
+@pytest.mark.parametrize("ranges", [1, 3])
+def test_sharded_algdist_rccl_single_rank(tmp_path, ranges):
   """The bench's RCCL path (nccl backend, collectives on the shared torch
-  stream) with one rank: the only RCCL configuration a 1-GPU box can run."""
+  stream; with ranges > 1 asynchronous per-range all-reduces) with one rank:
+  the only RCCL configuration a 1-GPU box can run."""
   import torch.multiprocessing as mp
   out = str(tmp_path / "nccl.npz")
-  mp.start_processes(_nccl_worker, args=(1, _free_port(), out), nprocs=1,
+  mp.start_processes(_nccl_worker, args=(1, _free_port(), out, ranges), nprocs=1,
                      join=True, start_method="spawn")
   z = golden("algdist_tiny.npz")
   d = np.load(out)

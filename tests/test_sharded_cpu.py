@@ -26,7 +26,8 @@ def _free_port():
   return p
 
 
-def _worker(rank, world, port, out_path, iters, compact=True, graph="tiny"):
+def _worker(rank, world, port, out_path, iters, compact=True, graph="tiny",
+            edge_ranges=1):
   import torch
   import torch.distributed as dist
   root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -45,7 +46,8 @@ def _worker(rank, world, port, out_path, iters, compact=True, graph="tiny"):
   st = {}
   (r0, r1, xo), y, _ = alg_dist_sharded(ShardEmu(), inc, x0, y0, iters,
                                         device=torch.device("cpu"),
-                                        compact=compact, stats=st)
+                                        compact=compact, stats=st,
+                                        edge_ranges=edge_ranges)
   np.savez(out_path + f".{rank}.npz", r0=r0, r1=r1, x=xo, y=y,
            wire=st["partial_bytes_per_iter"],
            dense=st["dense_partial_bytes_per_iter"])
@@ -74,12 +76,17 @@ def _local_graph():
   return Incidence(120, 43, rp, cols)
 
 
-@pytest.mark.parametrize("world,compact", [(2, True), (3, True), (2, False)])
-def test_sharded_driver_gloo(tmp_path, world, compact):
+@pytest.mark.parametrize("world,compact,ranges", [(2, True, 1), (3, True, 1),
+                                                  (2, False, 1), (3, True, 4),
+                                                  (2, False, 3)])
+def test_sharded_driver_gloo(tmp_path, world, compact, ranges):
+  """ranges > 1: the exchange pipelined over edge ranges (async all-reduce of
+  range r while range r + 1's partials are computed)."""
   import torch.multiprocessing as mp
   iters = 20
   out = str(tmp_path / "shard")
-  mp.start_processes(_worker, args=(world, _free_port(), out, iters, compact),
+  mp.start_processes(_worker, args=(world, _free_port(), out, iters, compact,
+                                    "tiny", ranges),
                      nprocs=world, join=True, start_method="spawn")
   inc = golden_incidence("csr_tiny.npz")
   z = golden("algdist_tiny.npz")
