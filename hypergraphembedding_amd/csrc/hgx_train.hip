@@ -59,8 +59,17 @@ static constexpr int g_tab = 0;
 // diagnostic phase trace (HGX_TRAIN_TRACE=<file>, timing experiments only):
 // wave 0 of every workgroup stamps s_memrealtime (100 MHz) at phase ends
 // for the first g_trace_nb batches; slots [batch][kernel][block < 1024][8].
+// Diagnostic builds only: in a release build the trace pointer is a
+// compile-time null, so the step's prologue has no dependent scalar load of a
+// device global (GOT entry, then the value) ahead of its kernel-argument
+// loads.
+#ifdef HGX_DEBUG_KNOBS
 __constant__ unsigned long long *g_trace = nullptr;
 __constant__ int g_trace_nb = 0;
+#else
+static constexpr unsigned long long *g_trace = nullptr;
+static constexpr int g_trace_nb = 0;
+#endif
 #define HGX_STAMP(var)                                              \
   do {                                                              \
     if (g_trace) {                                                  \
@@ -1945,8 +1954,10 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     void *p = nullptr;
     ~TraceBuf() {
       if (p) {
+#ifdef HGX_DEBUG_KNOBS
         unsigned long long *z = nullptr;
         hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &z, sizeof(z));
+#endif
         hipFree(p);
       }
     }
@@ -1961,8 +1972,13 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
       tp = (unsigned long long *)tb.p;
       tn = trace_nb;
     }
+#ifdef HGX_DEBUG_KNOBS
     HGX_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &tp, sizeof(tp)));
     HGX_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_trace_nb), &tn, sizeof(tn)));
+#else
+    (void)tp;
+    (void)tn;
+#endif
   }
   const int RPB = tb1 / L;
   const int nblk1 = (batch + RPB - 1) / RPB;
