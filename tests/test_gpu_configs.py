@@ -5,6 +5,9 @@ C1  youtube_tiny FOBE d=16: the reference's record stream (the oracle's
     the device for up to 10 epochs with EarlyStopping on the oracle's batch
     order; per-row cosine vs the CPU restatement (SURVEY §8c tolerance:
     p50 >= 0.9999, p1 >= 0.999) and the same epochs run.
+C1  youtube_tiny HOBE d=16: device alg-dist -> device probabilities on the
+    reference's pair stream -> device training, vs the reference coordinates
+    and the CPU restatement (same tolerance).
 C2  random 100k/50k FOBE d=128: exact per-row counts and pair validity on
     sampled rows, trainer determinism and a decreasing loss.
 C5  the N_E_SUPERVISED combiner on two d=256 embeddings (FOBE, HOBE) of a
@@ -70,6 +73,58 @@ def test_c1_fobe_end_to_end_cosine(ctx, tiny_inc):
   gnt, get_ = ctx.model_get()
   assert len(gl) == len(ol), (gl, ol)  # EarlyStopping stopped at the same epoch
   np.testing.assert_allclose(gl, ol, rtol=1e-4)
+  for g, o in ((gnt[1:], ont[1:]), (get_[1:], oet[1:])):
+    c = _row_cos(g, o)
+    assert np.percentile(c, 50) >= 0.9999 and np.percentile(c, 1) >= 0.999, \
+        (np.percentile(c, 50), np.percentile(c, 1))
+
+
+def test_c1_hobe_end_to_end_cosine(ctx, tiny_inc):
+  """HG2V_ALG_DIST d=16 on youtube_tiny through every device stage: alg-dist
+  (k=10, 20 iterations) from the reference's init vs the reference's own
+  coordinates; the reference's HOBE pair stream (oracle MT19937 replica with
+  the reference's coordinates: 755,267 records, the count measured from the
+  reference) whose nn/ee/ne probabilities the device
+  recomputes from ITS coordinates; then up to 10 epochs + EarlyStopping
+  (MSE / ReLU heads) on the device vs the CPU restatement trained on the
+  reference stream, same init and batch order: same epochs, per-row cosine
+  p50 >= 0.9999, p1 >= 0.999."""
+  from hypergraphembedding_amd import _hgx
+  z = golden("algdist_tiny.npz")
+  inc = tiny_inc
+  r = O.Rng(int(z["seed"]))
+  x0, y0 = r.random((inc.N, 10)), r.random((inc.E, 10))
+  ctx.upload(inc)
+  gx, gy = ctx.alg_dist(x0, y0, 20)  # coordinates stay resident
+  assert np.abs(gx - z["x_20"]).max() <= 1e-4
+  assert np.abs(gy - z["y_20"]).max() <= 1e-4
+  K, S = 5, 200
+  idx, tgt = O.hobe_sample(O.Rng(7), inc, z["x_20"], z["y_20"], S, K)
+  assert idx.shape[0] == 755_267
+  nn = (idx[:, 0] > 0) & (idx[:, 2] > 0)
+  ee = (idx[:, 1] > 0) & (idx[:, 3] > 0)
+  ne = (idx[:, 0] > 0) & (idx[:, 3] > 0)
+  assert (nn.sum(), ee.sum(), ne.sum()) == (718_589, 138, 36_540)
+  gt = np.zeros_like(tgt)
+  gt[nn, 0] = ctx.hobe_probs(_hgx.HOBE_NN, idx[nn, 0] - 1, idx[nn, 2] - 1)
+  gt[ee, 1] = ctx.hobe_probs(_hgx.HOBE_EE, idx[ee, 1] - 1, idx[ee, 3] - 1)
+  gt[ne, 2] = ctx.hobe_probs(_hgx.HOBE_NE, idx[ne, 0] - 1, idx[ne, 3] - 1)
+  assert np.abs(gt - tgt).max() <= 5e-4  # coordinates agree to 1e-4
+  n, d = idx.shape[0], 16
+  rs = np.random.RandomState(11)
+  perms = np.stack([rs.permutation(n) for _ in range(10)])
+  nt = rs.uniform(-0.05, 0.05, (inc.N + 1, d)).astype(np.float32)
+  et = rs.uniform(-0.05, 0.05, (inc.E + 1, d)).astype(np.float32)
+  ont, oet, ol, _, _ = O.train(idx, tgt, K, nt, et, O.LOSS_MSE, O.ACT_RELU,
+                               batch=256, max_epochs=10, perms=perms,
+                               min_delta=1e-3)
+  ctx.records_set(idx, gt)
+  ctx.model_init(d, inc.N + 1, inc.E + 1, node_tab=nt, edge_tab=et)
+  gl = ctx.train(batch=256, max_epochs=10, loss=_hgx.LOSS_MSE,
+                 act=_hgx.ACT_RELU, min_delta=1e-3, perms=perms)
+  gnt, get_ = ctx.model_get()
+  assert len(gl) == len(ol), (gl, ol)  # EarlyStopping stopped at the same epoch
+  np.testing.assert_allclose(gl, ol, rtol=1e-3)
   for g, o in ((gnt[1:], ont[1:]), (get_[1:], oet[1:])):
     c = _row_cos(g, o)
     assert np.percentile(c, 50) >= 0.9999 and np.percentile(c, 1) >= 0.999, \
