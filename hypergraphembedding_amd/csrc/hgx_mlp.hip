@@ -143,6 +143,68 @@ __device__ __forceinline__ float4 src_load4(const Src &s, const Ctx &c, int m,
   return v;
 }
 
+// One operand row resolved once per kernel (the sample ids of a gathered
+// source loaded up front), so the per-chunk loads of that row depend on no
+// other load and several chunks can be in flight.
+struct SrcRow {
+  const float *p0, *p1;  // dense row / table-0 row, table-1 row
+  int64_t pos;
+  bool ok;
+};
+// the rows m and m + off of a tile: rows past M resolve to row 0 of
+// the batch (never read: src_raw4 masks them), and all four id loads are
+// unconditional inside one uniform branch, so they share one round trip
+__device__ __forceinline__ void src_rows2(const Src &s, const Ctx &c, int m,
+                                          SrcRow &a, SrcRow &b, int off = 16) {
+  a.ok = m < c.M;
+  b.ok = m + off < c.M;
+  a.pos = c.pbase + m;
+  b.pos = c.pbase + m + off;
+  a.p0 = a.p1 = b.p0 = b.p1 = nullptr;
+  if (!s.gather) {
+    a.p0 = s.x + (int64_t)(a.ok ? m : 0) * s.ldx;
+    b.p0 = s.x + (int64_t)(b.ok ? m + off : 0) * s.ldx;
+    return;
+  }
+  const int64_t pa = a.ok ? a.pos : c.pbase, pb = b.ok ? b.pos : c.pbase;
+  const int *j0 = s.c1 > 0 ? s.i0 : s.i1;       // a valid id array either way
+  const int *j1 = s.c1 < s.width ? s.i1 : s.i0;
+  const int a0 = j0[pa], a1 = j1[pa], b0 = j0[pb], b1 = j1[pb];
+  const float *t0 = s.c1 > 0 ? s.t0 : s.t1, *t1 = s.c1 < s.width ? s.t1 : s.t0;
+  const int l0 = s.c1 > 0 ? s.ld0 : s.ld1, l1 = s.c1 < s.width ? s.ld1 : s.ld0;
+  a.p0 = t0 + (int64_t)a0 * l0;
+  a.p1 = t1 + (int64_t)a1 * l1;
+  b.p0 = t0 + (int64_t)b0 * l0;
+  b.p1 = t1 + (int64_t)b1 * l1;
+}
+// src_load4 of a resolved row in two steps, so that no lane-divergent
+// branch separates a load from its use (a join over loaded registers makes
+// the compiler wait for them): src_raw4 issues one unconditional load (a
+// valid dummy row when the element is outside the operand), src_fix4 zeroes
+// and applies the dropout mask when the chunk is consumed. Same values as
+// src_load4.
+__device__ __forceinline__ float4 src_raw4(const Src &s, const SrcRow &r,
+                                           int k4) {
+  const bool in = r.ok && k4 < s.width;
+  const float *a = s.gather ? (k4 < s.c1 ? r.p0 + k4 : r.p1 + (k4 - s.c1))
+                            : r.p0 + k4;
+  const float *safe = s.gather ? (s.c1 > 0 ? s.t0 : s.t1) : s.x;
+  return *reinterpret_cast<const float4 *>(in ? a : safe);
+}
+__device__ __forceinline__ float4 src_fix4(const Src &s, const Ctx &c,
+                                           const SrcRow &r, int k4, float4 v,
+                                           bool use_drop) {
+  if (!(r.ok && k4 < s.width)) return make_float4(0.f, 0.f, 0.f, 0.f);
+  if (s.gather && use_drop && s.drop) {
+    const unsigned b = drop_bits4(s, c, r.pos, k4);
+    v.x = (b & 1) ? v.x * 2.0f : 0.0f;
+    v.y = (b & 2) ? v.y * 2.0f : 0.0f;
+    v.z = (b & 4) ? v.z * 2.0f : 0.0f;
+    v.w = (b & 8) ? v.w * 2.0f : 0.0f;
+  }
+  return v;
+}
+
 __device__ __forceinline__ float src_at(const Src &s, const Ctx &c, int m,
                                         int k) {
   if (m >= c.M || k >= s.width) return 0.f;
@@ -242,6 +304,10 @@ __device__ __forceinline__ int find_job(const int *start, int n, int bid) {
   return q;
 }
 
+// NCH > 0: exactly NCH reduction chunks, every chunk's operands loaded up
+// front (straight-line code: no load waits on another, the wait before chunk
+// ch is for chunk ch's loads only); NCH = 0: any K, one chunk ahead.
+template <int NCH>
 __global__ __launch_bounds__(kThreads) void mlp_fwd(Jobs<FwdJob> js, Ctx c) {
   __shared__ __attribute__((aligned(16))) float lds[2][2][32 * 64];
   const int qj = find_job(js.start, js.n, blockIdx.x);
@@ -249,25 +315,50 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd(Jobs<FwdJob> js, Ctx c) {
   const int tile = blockIdx.x - js.start[qj];
   const int m0 = (tile / J.tiles_n) * kTile, n0 = (tile % J.tiles_n) * kTile;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  const int nch = J.K / kChunk;
-  float4 ra0, ra1, rb0, rb1;
-  auto load = [&](int ch) {
-    const int r0 = ch * kChunk;
-    ra0 = src_load4(J.a, c, m0 + (t >> 4), r0 + 4 * (t & 15), true);
-    ra1 = src_load4(J.a, c, m0 + (t >> 4) + 16, r0 + 4 * (t & 15), true);
-    const float *wp = J.W + (int64_t)(r0 + (t >> 3)) * J.ldw + n0 + 4 * (t & 7);
-    rb0 = *reinterpret_cast<const float4 *>(wp);
-    rb1 = *reinterpret_cast<const float4 *>(wp + (int64_t)32 * J.ldw);
-  };
   f32x16 acc = {};
-  load(0);
-  for (int ch = 0; ch < nch; ch++) {
-    float *As = lds[ch & 1][0], *Bs = lds[ch & 1][1];
-    store_R(As, ra0, ra1);
-    store_C(Bs, rb0, rb1);
-    __syncthreads();
-    if (ch + 1 < nch) load(ch + 1);
-    mma_chunk(As, Bs, acc, w, lane);
+  if constexpr (NCH > 0) {
+    SrcRow row0, row1;
+    src_rows2(J.a, c, m0 + (t >> 4), row0, row1);
+    float4 ra0[NCH], ra1[NCH], rb0[NCH], rb1[NCH];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+      const int r0 = ch * kChunk;
+      ra0[ch] = src_raw4(J.a, row0, r0 + 4 * (t & 15));
+      ra1[ch] = src_raw4(J.a, row1, r0 + 4 * (t & 15));
+      const float *wp = J.W + (int64_t)(r0 + (t >> 3)) * J.ldw + n0 + 4 * (t & 7);
+      rb0[ch] = *reinterpret_cast<const float4 *>(wp);
+      rb1[ch] = *reinterpret_cast<const float4 *>(wp + (int64_t)32 * J.ldw);
+    }
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+      float *As = lds[ch & 1][0], *Bs = lds[ch & 1][1];
+      const int k4 = ch * kChunk + 4 * (t & 15);
+      store_R(As, src_fix4(J.a, c, row0, k4, ra0[ch], true),
+              src_fix4(J.a, c, row1, k4, ra1[ch], true));
+      store_C(Bs, rb0[ch], rb1[ch]);
+      __syncthreads();
+      mma_chunk(As, Bs, acc, w, lane);
+    }
+  } else {
+    const int nch = J.K / kChunk;
+    float4 ra0, ra1, rb0, rb1;
+    auto load = [&](int ch) {
+      const int r0 = ch * kChunk;
+      ra0 = src_load4(J.a, c, m0 + (t >> 4), r0 + 4 * (t & 15), true);
+      ra1 = src_load4(J.a, c, m0 + (t >> 4) + 16, r0 + 4 * (t & 15), true);
+      const float *wp = J.W + (int64_t)(r0 + (t >> 3)) * J.ldw + n0 + 4 * (t & 7);
+      rb0 = *reinterpret_cast<const float4 *>(wp);
+      rb1 = *reinterpret_cast<const float4 *>(wp + (int64_t)32 * J.ldw);
+    };
+    load(0);
+    for (int ch = 0; ch < nch; ch++) {
+      float *As = lds[ch & 1][0], *Bs = lds[ch & 1][1];
+      store_R(As, ra0, ra1);
+      store_C(Bs, rb0, rb1);
+      __syncthreads();
+      if (ch + 1 < nch) load(ch + 1);
+      mma_chunk(As, Bs, acc, w, lane);
+    }
   }
   float v[4];
   int i0, j;
@@ -327,29 +418,59 @@ struct HeadJob {
 
 __global__ __launch_bounds__(kThreads) void mlp_head(HeadJob h, Ctx c) {
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int mb = blockIdx.x * 32 + w * 8;  // this wave's 8 rows
   float lsum = 0.f;
-  for (int s = 0; s < 8; s++) {
-    const int m = blockIdx.x * 32 + w * 8 + s;
-    const bool valid = m < c.M;
-    float z = 0.f;
-    if (valid)
-      for (int k = lane; k < h.K; k += 64)
-        z = fmaf(h.H[(int64_t)m * h.ldh + k], h.W[(int64_t)k * h.ldw], z);
-    z = hgx::group_allreduce_sum<64>(z);
-    const float y = act_f(h.act, z + h.b[0]);
-    if (valid && h.y && lane == 0) h.y[m] = y;
-    if (!h.loss) continue;
-    float dz = 0.f;
-    if (valid) {
-      const float diff = y - h.label[c.pbase + m];
-      if (lane == 0) lsum += diff * diff;
-      dz = h.lw * 2.0f * diff / (float)c.M * act_d(h.act, y);
+  // every load of the wave's 8 rows is issued before any of them is used:
+  // the labels and the bias up front, the rows' dot products interleaved
+  // (each row's fma chain in the same k order as one row at a time), the
+  // dZprev rows interleaved; the same arithmetic in the same order per row
+  float lab[8];
+#pragma unroll
+  for (int s = 0; s < 8; s++)
+    lab[s] = h.loss ? h.label[c.pbase + min(mb + s, c.M - 1)] : 0.f;
+  const float bias = h.b[0];
+  float zs[8];
+#pragma unroll
+  for (int s = 0; s < 8; s++) zs[s] = 0.f;
+  for (int k = lane; k < h.K; k += 64) {
+    const float wk = h.W[(int64_t)k * h.ldw];
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+      const int m = mb + s;
+      if (m < c.M) zs[s] = fmaf(h.H[(int64_t)m * h.ldh + k], wk, zs[s]);
     }
-    if (lane == 0) h.dz4[(int64_t)m * h.ld4] = dz;
+  }
+#pragma unroll
+  for (int s = 0; s < 8; s++) zs[s] = hgx::group_allreduce_sum<64>(zs[s]);
+  float dzs[8];
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+    const int m = mb + s;
+    const bool valid = m < c.M;
+    const float y = act_f(h.act, zs[s] + bias);
+    if (valid && h.y && lane == 0) h.y[m] = y;
+    float dz = 0.f;
+    if (h.loss) {
+      if (valid) {
+        const float diff = y - lab[s];
+        if (lane == 0) lsum += diff * diff;
+        dz = h.lw * 2.0f * diff / (float)c.M * act_d(h.act, y);
+      }
+      if (lane == 0) h.dz4[(int64_t)m * h.ld4] = dz;
+    }
+    dzs[s] = dz;
+  }
+  if (h.loss) {
     for (int k = lane; k < h.K; k += 64) {
-      const float hv = valid ? h.H[(int64_t)m * h.ldh + k] : 0.f;
-      h.dZprev[(int64_t)m * h.ldp + k] =
-          valid ? dz * h.W[(int64_t)k * h.ldw] * act_d(h.act_prev, hv) : 0.f;
+      const float wk = h.W[(int64_t)k * h.ldw];
+#pragma unroll
+      for (int s = 0; s < 8; s++) {
+        const int m = mb + s;
+        const bool valid = m < c.M;
+        const float hv = valid ? h.H[(int64_t)m * h.ldh + k] : 0.f;
+        h.dZprev[(int64_t)m * h.ldp + k] =
+            valid ? dzs[s] * wk * act_d(h.act_prev, hv) : 0.f;
+      }
     }
   }
   if (!h.loss) return;
@@ -378,6 +499,7 @@ struct BwdJob {
   int ldo, Kreal, tiles_n;
 };
 
+template <int NCH>
 __global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c) {
   __shared__ __attribute__((aligned(16))) float lds[2][2][32 * 64];
   const int qj = find_job(js.start, js.n, blockIdx.x);
@@ -386,31 +508,61 @@ __global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c) {
   const int m0 = (tile / J.tiles_n) * kTile, k0 = (tile % J.tiles_n) * kTile;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int nch0 = J.tm[0].R / kChunk;
-  const int nch = nch0 + (J.nt > 1 ? J.tm[1].R / kChunk : 0);
-  float4 ra0, ra1, rb0, rb1;
-  auto load = [&](int ch) {
-    const BwdTerm &T = ch < nch0 ? J.tm[0] : J.tm[1];
-    const int r0 = (ch < nch0 ? ch : ch - nch0) * kChunk;
-    const int r4 = r0 + 4 * (t & 15);
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int row = t >> 4, m = m0 + row;
-    ra0 = z4;
-    ra1 = z4;
-    if (m < c.M) ra0 = *reinterpret_cast<const float4 *>(T.dz + (int64_t)m * T.lddz + r4);
-    if (m + 16 < c.M)
-      ra1 = *reinterpret_cast<const float4 *>(T.dz + (int64_t)(m + 16) * T.lddz + r4);
-    rb0 = *reinterpret_cast<const float4 *>(T.W + (int64_t)(k0 + row) * T.ldw + r4);
-    rb1 = *reinterpret_cast<const float4 *>(T.W + (int64_t)(k0 + row + 16) * T.ldw + r4);
-  };
   f32x16 acc = {};
-  load(0);
-  for (int ch = 0; ch < nch; ch++) {
-    float *As = lds[ch & 1][0], *Bs = lds[ch & 1][1];
-    store_R(As, ra0, ra1);
-    store_R(Bs, rb0, rb1);
-    __syncthreads();
-    if (ch + 1 < nch) load(ch + 1);
-    mma_chunk(As, Bs, acc, w, lane);
+  if constexpr (NCH > 0) {
+    // all NCH chunks' loads up front, unconditional (rows past M read row 0
+    // and are zeroed when stored)
+    const int row = t >> 4, ma = m0 + row, mb = ma + 16;
+    const bool oka = ma < c.M, okb = mb < c.M;
+    float4 ra0[NCH], ra1[NCH], rb0[NCH], rb1[NCH];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+      const bool first = ch < nch0;
+      const float *dz = first ? J.tm[0].dz : J.tm[1].dz;
+      const float *W = first ? J.tm[0].W : J.tm[1].W;
+      const int lddz = first ? J.tm[0].lddz : J.tm[1].lddz;
+      const int ldw = first ? J.tm[0].ldw : J.tm[1].ldw;
+      const int r4 = (first ? ch : ch - nch0) * kChunk + 4 * (t & 15);
+      ra0[ch] = *reinterpret_cast<const float4 *>(dz + (int64_t)(oka ? ma : 0) * lddz + r4);
+      ra1[ch] = *reinterpret_cast<const float4 *>(dz + (int64_t)(okb ? mb : 0) * lddz + r4);
+      rb0[ch] = *reinterpret_cast<const float4 *>(W + (int64_t)(k0 + row) * ldw + r4);
+      rb1[ch] = *reinterpret_cast<const float4 *>(W + (int64_t)(k0 + row + 16) * ldw + r4);
+    }
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+      float *As = lds[ch & 1][0], *Bs = lds[ch & 1][1];
+      store_R(As, oka ? ra0[ch] : z4, okb ? ra1[ch] : z4);
+      store_R(Bs, rb0[ch], rb1[ch]);
+      __syncthreads();
+      mma_chunk(As, Bs, acc, w, lane);
+    }
+  } else {
+    const int nch = nch0 + (J.nt > 1 ? J.tm[1].R / kChunk : 0);
+    float4 ra0, ra1, rb0, rb1;
+    auto load = [&](int ch) {
+      const BwdTerm &T = ch < nch0 ? J.tm[0] : J.tm[1];
+      const int r0 = (ch < nch0 ? ch : ch - nch0) * kChunk;
+      const int r4 = r0 + 4 * (t & 15);
+      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int row = t >> 4, m = m0 + row;
+      ra0 = z4;
+      ra1 = z4;
+      if (m < c.M) ra0 = *reinterpret_cast<const float4 *>(T.dz + (int64_t)m * T.lddz + r4);
+      if (m + 16 < c.M)
+        ra1 = *reinterpret_cast<const float4 *>(T.dz + (int64_t)(m + 16) * T.lddz + r4);
+      rb0 = *reinterpret_cast<const float4 *>(T.W + (int64_t)(k0 + row) * T.ldw + r4);
+      rb1 = *reinterpret_cast<const float4 *>(T.W + (int64_t)(k0 + row + 16) * T.ldw + r4);
+    };
+    load(0);
+    for (int ch = 0; ch < nch; ch++) {
+      float *As = lds[ch & 1][0], *Bs = lds[ch & 1][1];
+      store_R(As, ra0, ra1);
+      store_R(Bs, rb0, rb1);
+      __syncthreads();
+      if (ch + 1 < nch) load(ch + 1);
+      mma_chunk(As, Bs, acc, w, lane);
+    }
   }
   float v[4];
   int i0, j;
@@ -434,6 +586,7 @@ struct WgJob {
   int ldw, tiles_n;
 };
 
+template <int NCH>
 __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
   __shared__ __attribute__((aligned(16))) float lds[2][2][32 * 64];
   const int qj = find_job(js.start, js.n, blockIdx.x);
@@ -441,28 +594,59 @@ __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
   const int tile = blockIdx.x - js.start[qj];
   const int k0 = (tile / J.tiles_n) * kTile, n0 = (tile % J.tiles_n) * kTile;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  const int nch = (c.M + kChunk - 1) / kChunk;
-  float4 ra0, ra1, rb0, rb1;
-  auto load = [&](int ch) {
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int m = ch * kChunk + (t >> 3);
-    ra0 = src_load4(J.a, c, m, k0 + 4 * (t & 7), true);
-    ra1 = src_load4(J.a, c, m + 32, k0 + 4 * (t & 7), true);
-    const float *dp = J.dZ + (int64_t)m * J.lddz + n0 + 4 * (t & 7);
-    rb0 = z4;
-    rb1 = z4;
-    if (m < c.M) rb0 = *reinterpret_cast<const float4 *>(dp);
-    if (m + 32 < c.M) rb1 = *reinterpret_cast<const float4 *>(dp + (int64_t)32 * J.lddz);
-  };
   f32x16 acc = {};
-  load(0);
-  for (int ch = 0; ch < nch; ch++) {
-    float *As = lds[ch & 1][0], *Bs = lds[ch & 1][1];
-    store_C(As, ra0, ra1);
-    store_C(Bs, rb0, rb1);
-    __syncthreads();
-    if (ch + 1 < nch) load(ch + 1);
-    mma_chunk(As, Bs, acc, w, lane);
+  if constexpr (NCH > 0) {
+    // the reduction runs over the batch rows: every chunk's input rows
+    // resolved (ids in one round trip), then all chunks' loads up front
+    SrcRow ra[NCH], rb[NCH];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++)
+      src_rows2(J.a, c, ch * kChunk + (t >> 3), ra[ch], rb[ch], 32);
+    const int kk = k0 + 4 * (t & 7);
+    float4 xa0[NCH], xa1[NCH], d0[NCH], d1[NCH];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+      const int m = ch * kChunk + (t >> 3);
+      xa0[ch] = src_raw4(J.a, ra[ch], kk);
+      xa1[ch] = src_raw4(J.a, rb[ch], kk);
+      const float *dp = J.dZ + n0 + 4 * (t & 7);
+      d0[ch] = *reinterpret_cast<const float4 *>(dp + (int64_t)(m < c.M ? m : 0) * J.lddz);
+      d1[ch] = *reinterpret_cast<const float4 *>(dp + (int64_t)(m + 32 < c.M ? m + 32 : 0) * J.lddz);
+    }
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+      const int m = ch * kChunk + (t >> 3);
+      float *As = lds[ch & 1][0], *Bs = lds[ch & 1][1];
+      store_C(As, src_fix4(J.a, c, ra[ch], kk, xa0[ch], true),
+              src_fix4(J.a, c, rb[ch], kk, xa1[ch], true));
+      store_C(Bs, m < c.M ? d0[ch] : z4, m + 32 < c.M ? d1[ch] : z4);
+      __syncthreads();
+      mma_chunk(As, Bs, acc, w, lane);
+    }
+  } else {
+    const int nch = (c.M + kChunk - 1) / kChunk;
+    float4 ra0, ra1, rb0, rb1;
+    auto load = [&](int ch) {
+      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int m = ch * kChunk + (t >> 3);
+      ra0 = src_load4(J.a, c, m, k0 + 4 * (t & 7), true);
+      ra1 = src_load4(J.a, c, m + 32, k0 + 4 * (t & 7), true);
+      const float *dp = J.dZ + (int64_t)m * J.lddz + n0 + 4 * (t & 7);
+      rb0 = z4;
+      rb1 = z4;
+      if (m < c.M) rb0 = *reinterpret_cast<const float4 *>(dp);
+      if (m + 32 < c.M) rb1 = *reinterpret_cast<const float4 *>(dp + (int64_t)32 * J.lddz);
+    };
+    load(0);
+    for (int ch = 0; ch < nch; ch++) {
+      float *As = lds[ch & 1][0], *Bs = lds[ch & 1][1];
+      store_C(As, ra0, ra1);
+      store_C(Bs, rb0, rb1);
+      __syncthreads();
+      if (ch + 1 < nch) load(ch + 1);
+      mma_chunk(As, Bs, acc, w, lane);
+    }
   }
   float v[4];
   int i0, j;
@@ -657,6 +841,59 @@ int launch_jobs(hgx_ctx *ctx, void (*kern)(Jobs<J>, Ctx), const J *jobs,
   return HGX_OK;
 }
 
+// FWD launch: the all-chunks-in-flight instantiation when every job of the
+// launch has the same K of 2..8 chunks, else the generic one (same results:
+// identical chunk order and wave split)
+int launch_fwd(hgx_ctx *ctx, const FwdJob *jobs, const int *tiles, int n,
+               const Ctx &c) {
+  int nch = n > 0 ? jobs[0].K / kChunk : 0;
+  for (int q = 1; q < n; q++)
+    if (jobs[q].K != jobs[0].K) nch = 0;
+  switch (nch) {
+    case 2: return launch_jobs(ctx, mlp_fwd<2>, jobs, tiles, n, c);
+    case 3: return launch_jobs(ctx, mlp_fwd<3>, jobs, tiles, n, c);
+    case 4: return launch_jobs(ctx, mlp_fwd<4>, jobs, tiles, n, c);
+    case 5: return launch_jobs(ctx, mlp_fwd<5>, jobs, tiles, n, c);
+    case 6: return launch_jobs(ctx, mlp_fwd<6>, jobs, tiles, n, c);
+    case 7: return launch_jobs(ctx, mlp_fwd<7>, jobs, tiles, n, c);
+    case 8: return launch_jobs(ctx, mlp_fwd<8>, jobs, tiles, n, c);
+    default: return launch_jobs(ctx, mlp_fwd<0>, jobs, tiles, n, c);
+  }
+}
+
+// BWD: every job of the launch with the same total chunk count (2..8)
+int launch_bwd(hgx_ctx *ctx, const BwdJob *jobs, const int *tiles, int n,
+               const Ctx &c) {
+  auto chunks = [](const BwdJob &j) {
+    return j.tm[0].R / kChunk + (j.nt > 1 ? j.tm[1].R / kChunk : 0);
+  };
+  int nch = n > 0 ? chunks(jobs[0]) : 0;
+  for (int q = 1; q < n; q++)
+    if (chunks(jobs[q]) != nch) nch = 0;
+  switch (nch) {
+    case 2: return launch_jobs(ctx, mlp_bwd<2>, jobs, tiles, n, c);
+    case 3: return launch_jobs(ctx, mlp_bwd<3>, jobs, tiles, n, c);
+    case 4: return launch_jobs(ctx, mlp_bwd<4>, jobs, tiles, n, c);
+    case 5: return launch_jobs(ctx, mlp_bwd<5>, jobs, tiles, n, c);
+    case 6: return launch_jobs(ctx, mlp_bwd<6>, jobs, tiles, n, c);
+    case 7: return launch_jobs(ctx, mlp_bwd<7>, jobs, tiles, n, c);
+    case 8: return launch_jobs(ctx, mlp_bwd<8>, jobs, tiles, n, c);
+    default: return launch_jobs(ctx, mlp_bwd<0>, jobs, tiles, n, c);
+  }
+}
+
+// WGRAD: the reduction is the batch (M rows): 1..4 chunks at batch <= 256
+int launch_wgrad(hgx_ctx *ctx, const WgJob *jobs, const int *tiles, int n,
+                 const Ctx &c) {
+  switch ((c.M + kChunk - 1) / kChunk) {
+    case 1: return launch_jobs(ctx, mlp_wgrad<1>, jobs, tiles, n, c);
+    case 2: return launch_jobs(ctx, mlp_wgrad<2>, jobs, tiles, n, c);
+    case 3: return launch_jobs(ctx, mlp_wgrad<3>, jobs, tiles, n, c);
+    case 4: return launch_jobs(ctx, mlp_wgrad<4>, jobs, tiles, n, c);
+    default: return launch_jobs(ctx, mlp_wgrad<0>, jobs, tiles, n, c);
+  }
+}
+
 FwdJob fwd_job(const hgx_mlp *m, int li, const Src &a, float *Y, int ldy) {
   const MlpLayer &l = m->L[li];
   FwdJob j{};
@@ -717,7 +954,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
     const Src in = gather_src(m, 0, pn, pe, dstream, false);
     FwdJob f = fwd_job(m, l1, in, m->A_hn.as<float>(), L[l1].Np);
     int tl = tiles(l1);
-    HGX_TRY(launch_jobs(ctx, mlp_fwd, &f, &tl, 1, c));
+    HGX_TRY(launch_fwd(ctx, &f, &tl, 1, c));
     HeadJob h{};
     h.H = m->A_hn.as<float>();
     h.ldh = L[l1].Np;
@@ -742,7 +979,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
                    wg_job(m, l2, dense(m->A_hn, L[l1].Np, L[l1].Np), m->D_4, L[l2].Np)};
     int wt[2] = {(L[l1].Kp / kTile) * (L[l1].Np / kTile),
                  (L[l2].Kp / kTile) * (L[l2].Np / kTile)};
-    return launch_jobs(ctx, mlp_wgrad, wj, wt, 2, c);
+    return launch_wgrad(ctx, wj, wt, 2, c);
   }
   // combiners
   const bool ae = m->kind == HGX_MLP_NE_SEMI_SUPERVISED && train;
@@ -763,7 +1000,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
       f[n] = fwd_job(m, b, in_e, m->A_he.as<float>(), L[b].Np);
       tl[n++] = tiles(b);
     }
-    HGX_TRY(launch_jobs(ctx, mlp_fwd, f, tl, n, c));
+    HGX_TRY(launch_fwd(ctx, f, tl, n, c));
     n = 0;
     if (which != 2) {
       f[n] = fwd_job(m, jn, dense(m->A_hn, L[a].Np, L[a].Np), m->A_j.as<float>(), m->ldJ);
@@ -774,7 +1011,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
                      m->ldJ);
       tl[n++] = tiles(je);
     }
-    HGX_TRY(launch_jobs(ctx, mlp_fwd, f, tl, n, c));
+    HGX_TRY(launch_fwd(ctx, f, tl, n, c));
     if (which == 1 || which == 2) return HGX_OK;
   }
   {  // stage 3: merged hidden (+ post layers)
@@ -790,7 +1027,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
                      L[m->post_e].Np);
       tl[n++] = tiles(m->post_e);
     }
-    HGX_TRY(launch_jobs(ctx, mlp_fwd, f, tl, n, c));
+    HGX_TRY(launch_fwd(ctx, f, tl, n, c));
   }
   HeadJob h{};
   h.H = m->A_hm.as<float>();
@@ -829,7 +1066,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
     f[0].part = slot + 8;
     f[1].part = slot + 8 + tiles(rn);
     int tl[2] = {tiles(rn), tiles(re)};
-    HGX_TRY(launch_jobs(ctx, mlp_fwd, f, tl, 2, c));
+    HGX_TRY(launch_fwd(ctx, f, tl, 2, c));
     // dZ of the post layers
     BwdJob bj[2] = {};
     const int po[2] = {m->post_n, m->post_e};
@@ -847,7 +1084,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
       bj[q].tiles_n = L[po[q]].Np / kTile;
       bt[q] = tiles(po[q]);
     }
-    HGX_TRY(launch_jobs(ctx, mlp_bwd, bj, bt, 2, c));
+    HGX_TRY(launch_bwd(ctx, bj, bt, 2, c));
   }
   {  // dZ of the joint layers: from the merged hidden layer (+ post layers)
     BwdJob bj[2] = {};
@@ -870,7 +1107,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
       bj[q].tiles_n = NpJ / kTile;
       bt[q] = tiles(jl[q]);
     }
-    HGX_TRY(launch_jobs(ctx, mlp_bwd, bj, bt, 2, c));
+    HGX_TRY(launch_bwd(ctx, bj, bt, 2, c));
   }
   {  // dZ of the pre layers
     BwdJob bj[2] = {};
@@ -890,7 +1127,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
       bj[q].tiles_n = L[pl[q]].Np / kTile;
       bt[q] = tiles(pl[q]);
     }
-    HGX_TRY(launch_jobs(ctx, mlp_bwd, bj, bt, 2, c));
+    HGX_TRY(launch_bwd(ctx, bj, bt, 2, c));
   }
   // every weight gradient + Adagrad
   std::vector<WgJob> wj;
@@ -911,7 +1148,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
   }
   add(hd, dense(m->A_j, m->ldJ, 2 * NpJ), m->D_hm);
   add(lb, dense(m->A_hm, L[hd].Np, L[hd].Np), m->D_4);
-  return launch_jobs(ctx, mlp_wgrad, wj.data(), wt.data(), (int)wj.size(), c);
+  return launch_wgrad(ctx, wj.data(), wt.data(), (int)wj.size(), c);
 }
 
 int loss_slots(const hgx_mlp *m) {
