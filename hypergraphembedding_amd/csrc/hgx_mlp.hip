@@ -432,12 +432,13 @@ __global__ __launch_bounds__(kThreads) void mlp_head(HeadJob h, Ctx c) {
   float zs[8];
 #pragma unroll
   for (int s = 0; s < 8; s++) zs[s] = 0.f;
+  // (rows past M read the batch's last row: their sums are never used)
   for (int k = lane; k < h.K; k += 64) {
     const float wk = h.W[(int64_t)k * h.ldw];
 #pragma unroll
     for (int s = 0; s < 8; s++) {
-      const int m = mb + s;
-      if (m < c.M) zs[s] = fmaf(h.H[(int64_t)m * h.ldh + k], wk, zs[s]);
+      const int m = min(mb + s, c.M - 1);
+      zs[s] = fmaf(h.H[(int64_t)m * h.ldh + k], wk, zs[s]);
     }
   }
 #pragma unroll
@@ -447,7 +448,7 @@ __global__ __launch_bounds__(kThreads) void mlp_head(HeadJob h, Ctx c) {
   for (int s = 0; s < 8; s++) {
     const int m = mb + s;
     const bool valid = m < c.M;
-    const float y = act_f(h.act, zs[s] + bias);
+    const float y = act_f(h.act, (valid ? zs[s] : 0.f) + bias);
     if (valid && h.y && lane == 0) h.y[m] = y;
     float dz = 0.f;
     if (h.loss) {
@@ -467,7 +468,7 @@ __global__ __launch_bounds__(kThreads) void mlp_head(HeadJob h, Ctx c) {
       for (int s = 0; s < 8; s++) {
         const int m = mb + s;
         const bool valid = m < c.M;
-        const float hv = valid ? h.H[(int64_t)m * h.ldh + k] : 0.f;
+        const float hv = h.H[(int64_t)min(m, c.M - 1) * h.ldh + k];
         h.dZprev[(int64_t)m * h.ldp + k] =
             valid ? dzs[s] * wk * act_d(h.act_prev, hv) : 0.f;
       }
@@ -571,8 +572,10 @@ __global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c) {
 #pragma unroll
   for (int e = 0; e < 4; e++) {
     const int m = m0 + i0 + e;
-    float d = 0.f;
-    if (m < c.M && k < J.Kreal) d = v[e] * act_d(J.act, J.Y[(int64_t)m * J.ldy + k]);
+    // unconditional load (clamped), so the four rows' loads are in flight
+    // together; the value is used only where the original read it
+    const float yv = J.Y[(int64_t)min(m, c.M - 1) * J.ldy + min(k, J.Kreal - 1)];
+    const float d = (m < c.M && k < J.Kreal) ? v[e] * act_d(J.act, yv) : 0.f;
     J.dZ[(int64_t)m * J.ldo + k] = d;
   }
 }
@@ -672,8 +675,17 @@ __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
   float *bs = &lds[0][0][0];
   {
     const int col = t & 31, grp = t >> 5;
+    // rows grp, grp + 8, ... summed in that order; 8 loads in flight
     float s = 0.f;
-    for (int m = grp; m < c.M; m += 8) s += J.dZ[(int64_t)m * J.lddz + n0 + col];
+    int m = grp;
+    for (; m + 56 < c.M; m += 64) {
+      float dv[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) dv[u] = J.dZ[(int64_t)(m + 8 * u) * J.lddz + n0 + col];
+#pragma unroll
+      for (int u = 0; u < 8; u++) s += dv[u];
+    }
+    for (; m < c.M; m += 8) s += J.dZ[(int64_t)m * J.lddz + n0 + col];
     bs[grp * 32 + col] = s;
   }
   __syncthreads();
