@@ -268,6 +268,15 @@ __device__ __forceinline__ void store_R(float *S, float4 v0, float4 v1) {
   store_R1(S, v0, t >> 4, r4);
   store_R1(S, v1, (t >> 4) + 16, r4);
 }
+// pattern R2 (the NCH-instantiated kernels): thread t holds tile row
+// i = t & 31 at reduction r4 = 4*(t>>5) and r4 + 32, so one ds_write_b32 of
+// a wave spans all 32 rows (2-way bank conflicts instead of pattern R's
+// 16-way); the LDS image is the same
+__device__ __forceinline__ void store_R2(float *S, float4 v0, float4 v1) {
+  const int t = threadIdx.x, i = t & 31, r4 = 4 * (t >> 5);
+  store_R1(S, v0, i, r4);
+  store_R1(S, v1, i, r4 + 32);
+}
 __device__ __forceinline__ void store_C(float *S, float4 v0, float4 v1) {
   const int t = threadIdx.x, j4 = 4 * (t & 7);
   *reinterpret_cast<float4 *>(S + lds_at(j4, t >> 3)) = v0;
@@ -317,14 +326,15 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd(Jobs<FwdJob> js, Ctx c) {
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   f32x16 acc = {};
   if constexpr (NCH > 0) {
-    SrcRow row0, row1;
-    src_rows2(J.a, c, m0 + (t >> 4), row0, row1);
+    SrcRow row0, unused;
+    src_rows2(J.a, c, m0 + (t & 31), row0, unused, 0);
+    const int q4 = 4 * (t >> 5);  // pattern R2
     float4 ra0[NCH], ra1[NCH], rb0[NCH], rb1[NCH];
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
       const int r0 = ch * kChunk;
-      ra0[ch] = src_raw4(J.a, row0, r0 + 4 * (t & 15));
-      ra1[ch] = src_raw4(J.a, row1, r0 + 4 * (t & 15));
+      ra0[ch] = src_raw4(J.a, row0, r0 + q4);
+      ra1[ch] = src_raw4(J.a, row0, r0 + q4 + 32);
       const float *wp = J.W + (int64_t)(r0 + (t >> 3)) * J.ldw + n0 + 4 * (t & 7);
       rb0[ch] = *reinterpret_cast<const float4 *>(wp);
       rb1[ch] = *reinterpret_cast<const float4 *>(wp + (int64_t)32 * J.ldw);
@@ -332,9 +342,9 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd(Jobs<FwdJob> js, Ctx c) {
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
       float *As = lds[ch & 1][0], *Bs = lds[ch & 1][1];
-      const int k4 = ch * kChunk + 4 * (t & 15);
-      store_R(As, src_fix4(J.a, c, row0, k4, ra0[ch], true),
-              src_fix4(J.a, c, row1, k4, ra1[ch], true));
+      const int k4 = ch * kChunk + q4;
+      store_R2(As, src_fix4(J.a, c, row0, k4, ra0[ch], true),
+               src_fix4(J.a, c, row0, k4 + 32, ra1[ch], true));
       store_C(Bs, rb0[ch], rb1[ch]);
       __syncthreads();
       mma_chunk(As, Bs, acc, w, lane);
@@ -513,8 +523,9 @@ __global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c) {
   if constexpr (NCH > 0) {
     // all NCH chunks' loads up front, unconditional (rows past M read row 0
     // and are zeroed when stored)
-    const int row = t >> 4, ma = m0 + row, mb = ma + 16;
-    const bool oka = ma < c.M, okb = mb < c.M;
+    // pattern R2 for both operands: row i = t & 31, reduction r4, r4 + 32
+    const int row = t & 31, ma = m0 + row, q4 = 4 * (t >> 5);
+    const bool oka = ma < c.M;
     float4 ra0[NCH], ra1[NCH], rb0[NCH], rb1[NCH];
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
@@ -523,18 +534,20 @@ __global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c) {
       const float *W = first ? J.tm[0].W : J.tm[1].W;
       const int lddz = first ? J.tm[0].lddz : J.tm[1].lddz;
       const int ldw = first ? J.tm[0].ldw : J.tm[1].ldw;
-      const int r4 = (first ? ch : ch - nch0) * kChunk + 4 * (t & 15);
-      ra0[ch] = *reinterpret_cast<const float4 *>(dz + (int64_t)(oka ? ma : 0) * lddz + r4);
-      ra1[ch] = *reinterpret_cast<const float4 *>(dz + (int64_t)(okb ? mb : 0) * lddz + r4);
-      rb0[ch] = *reinterpret_cast<const float4 *>(W + (int64_t)(k0 + row) * ldw + r4);
-      rb1[ch] = *reinterpret_cast<const float4 *>(W + (int64_t)(k0 + row + 16) * ldw + r4);
+      const int r4 = (first ? ch : ch - nch0) * kChunk + q4;
+      const float *dr = dz + (int64_t)(oka ? ma : 0) * lddz + r4;
+      const float *wr = W + (int64_t)(k0 + row) * ldw + r4;
+      ra0[ch] = *reinterpret_cast<const float4 *>(dr);
+      ra1[ch] = *reinterpret_cast<const float4 *>(dr + 32);
+      rb0[ch] = *reinterpret_cast<const float4 *>(wr);
+      rb1[ch] = *reinterpret_cast<const float4 *>(wr + 32);
     }
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
       float *As = lds[ch & 1][0], *Bs = lds[ch & 1][1];
-      store_R(As, oka ? ra0[ch] : z4, okb ? ra1[ch] : z4);
-      store_R(Bs, rb0[ch], rb1[ch]);
+      store_R2(As, oka ? ra0[ch] : z4, oka ? ra1[ch] : z4);
+      store_R2(Bs, rb0[ch], rb1[ch]);
       __syncthreads();
       mma_chunk(As, Bs, acc, w, lane);
     }
