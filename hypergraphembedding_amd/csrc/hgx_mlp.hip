@@ -610,6 +610,18 @@ __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
   const int tile = blockIdx.x - js.start[qj];
   const int k0 = (tile / J.tiles_n) * kTile, n0 = (tile % J.tiles_n) * kTile;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  // the Adagrad operands of the 4 elements this thread updates (reduce_tile's
+  // mapping), loaded before the GEMM so the update needs no further round trip
+  float pW[4], pA[4];
+  {
+    const int e0 = 8 * w + 4 * (lane >> 5), jn = n0 + (lane & 31);
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int64_t q = (int64_t)(k0 + e0 + e) * J.ldw + jn;
+      pW[e] = J.W[q];
+      pA[e] = J.aW[q];
+    }
+  }
   f32x16 acc = {};
   if constexpr (NCH > 0) {
     // the reduction runs over the batch rows: every chunk's input rows
@@ -678,9 +690,9 @@ __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
     }
     // plain sqrtf is correctly rounded on gfx950 (__fsqrt_rn is not: 15% of
     // 1M inputs off by an ulp, tools/fp_check.hip), as the CPU side's is
-    const float na = J.aW[q] + g * g;
+    const float na = pA[e] + g * g;
     J.aW[q] = na;
-    J.W[q] = J.W[q] - (c.lr * g) / (sqrtf(na) + c.eps);
+    J.W[q] = pW[e] - (c.lr * g) / (sqrtf(na) + c.eps);
   }
   if (k0 != 0) return;
   // bias: column sums of dZ over the batch rows (8 row groups per column)
