@@ -426,61 +426,101 @@ struct HeadJob {
   float *part;         // one partial per workgroup
 };
 
+// HEAD_KH: inputs of up to 64 * HEAD_KH columns are kept in registers
+constexpr int kHeadKH = 8;
+
 __global__ __launch_bounds__(kThreads) void mlp_head(HeadJob h, Ctx c) {
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int mb = blockIdx.x * 32 + w * 8;  // this wave's 8 rows
   float lsum = 0.f;
-  // every load of the wave's 8 rows is issued before any of them is used:
-  // the labels and the bias up front, the rows' dot products interleaved
-  // (each row's fma chain in the same k order as one row at a time), the
-  // dZprev rows interleaved; the same arithmetic in the same order per row
+  // Every load is issued, and consumed, before the first store: on this
+  // architecture the vector-memory counter also counts stores, so a load
+  // waited for after a store waits for that store too. The same arithmetic
+  // in the same order per row as one row at a time: each row's fma chain in
+  // k order, the loss summed over the wave's rows in order. Rows past M read
+  // the batch's last row (their sums are never used).
   float lab[8];
 #pragma unroll
   for (int s = 0; s < 8; s++)
     lab[s] = h.loss ? h.label[c.pbase + min(mb + s, c.M - 1)] : 0.f;
   const float bias = h.b[0];
-  float zs[8];
+  const bool regs = h.K <= 64 * kHeadKH;
+  float zs[8], wv[kHeadKH], hv[kHeadKH][8];
 #pragma unroll
   for (int s = 0; s < 8; s++) zs[s] = 0.f;
-  // (rows past M read the batch's last row: their sums are never used)
-  for (int k = lane; k < h.K; k += 64) {
-    const float wk = h.W[(int64_t)k * h.ldw];
+  if (regs) {
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
-      const int m = min(mb + s, c.M - 1);
-      zs[s] = fmaf(h.H[(int64_t)m * h.ldh + k], wk, zs[s]);
+    for (int kk = 0; kk < kHeadKH; kk++) {
+      const int k = min(lane + 64 * kk, h.K - 1);
+      wv[kk] = h.W[(int64_t)k * h.ldw];
+#pragma unroll
+      for (int s = 0; s < 8; s++)
+        hv[kk][s] = h.H[(int64_t)min(mb + s, c.M - 1) * h.ldh + k];
     }
-  }
 #pragma unroll
-  for (int s = 0; s < 8; s++) zs[s] = hgx::group_allreduce_sum<64>(zs[s]);
-  float dzs[8];
+    for (int kk = 0; kk < kHeadKH; kk++) {
+      const bool in = lane + 64 * kk < h.K;
 #pragma unroll
-  for (int s = 0; s < 8; s++) {
-    const int m = mb + s;
-    const bool valid = m < c.M;
-    const float y = act_f(h.act, (valid ? zs[s] : 0.f) + bias);
-    if (valid && h.y && lane == 0) h.y[m] = y;
-    float dz = 0.f;
-    if (h.loss) {
-      if (valid) {
-        const float diff = y - lab[s];
-        if (lane == 0) lsum += diff * diff;
-        dz = h.lw * 2.0f * diff / (float)c.M * act_d(h.act, y);
-      }
-      if (lane == 0) h.dz4[(int64_t)m * h.ld4] = dz;
+      for (int s = 0; s < 8; s++)
+        zs[s] = in ? fmaf(hv[kk][s], wv[kk], zs[s]) : zs[s];
     }
-    dzs[s] = dz;
-  }
-  if (h.loss) {
+  } else {
     for (int k = lane; k < h.K; k += 64) {
       const float wk = h.W[(int64_t)k * h.ldw];
 #pragma unroll
       for (int s = 0; s < 8; s++) {
-        const int m = mb + s;
-        const bool valid = m < c.M;
-        const float hv = h.H[(int64_t)min(m, c.M - 1) * h.ldh + k];
-        h.dZprev[(int64_t)m * h.ldp + k] =
-            valid ? dzs[s] * wk * act_d(h.act_prev, hv) : 0.f;
+        const int m = min(mb + s, c.M - 1);
+        zs[s] = fmaf(h.H[(int64_t)m * h.ldh + k], wk, zs[s]);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 8; s++) zs[s] = hgx::group_allreduce_sum<64>(zs[s]);
+  float ys[8], dzs[8];
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+    const bool valid = mb + s < c.M;
+    ys[s] = act_f(h.act, (valid ? zs[s] : 0.f) + bias);
+    float dz = 0.f;
+    if (h.loss && valid) {
+      const float diff = ys[s] - lab[s];
+      if (lane == 0) lsum += diff * diff;
+      dz = h.lw * 2.0f * diff / (float)c.M * act_d(h.act, ys[s]);
+    }
+    dzs[s] = dz;
+  }
+  // stores
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+    const int m = mb + s;
+    if (m < c.M && h.y && lane == 0) h.y[m] = ys[s];
+    if (h.loss && lane == 0) h.dz4[(int64_t)m * h.ld4] = dzs[s];
+  }
+  if (h.loss) {
+    if (regs) {
+#pragma unroll
+      for (int kk = 0; kk < kHeadKH; kk++) {
+        const int k = lane + 64 * kk;
+        if (k < h.K) {
+#pragma unroll
+          for (int s = 0; s < 8; s++) {
+            const int m = mb + s;
+            h.dZprev[(int64_t)m * h.ldp + k] =
+                m < c.M ? dzs[s] * wv[kk] * act_d(h.act_prev, hv[kk][s]) : 0.f;
+          }
+        }
+      }
+    } else {
+      for (int k = lane; k < h.K; k += 64) {
+        const float wk = h.W[(int64_t)k * h.ldw];
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+          const int m = mb + s;
+          const bool valid = m < c.M;
+          const float hvv = h.H[(int64_t)min(m, c.M - 1) * h.ldh + k];
+          h.dZprev[(int64_t)m * h.ldp + k] =
+              valid ? dzs[s] * wk * act_d(h.act_prev, hvv) : 0.f;
+        }
       }
     }
   }
