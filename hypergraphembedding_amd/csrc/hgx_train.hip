@@ -567,8 +567,9 @@ constexpr double kFixScale = 17592186044416.0;  // 2^44
 constexpr double kFixInv = 1.0 / 17592186044416.0;
 constexpr float kFixLimit = 32.f;
 
+// rounded to the nearest 2^-44 unit (not truncated toward zero)
 __device__ __forceinline__ unsigned long long to_fix(float v) {
-  return (unsigned long long)(long long)((double)v * kFixScale);
+  return (unsigned long long)__double2ll_rn((double)v * kFixScale);
 }
 __device__ __forceinline__ float from_fix(long long v) {
   return (float)((double)v * kFixInv);

@@ -137,6 +137,8 @@ def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
   else:
     inc = Incidence.from_hypergraph(hypergraph)  # CompressRange + CSR
   budget = RECORDS_BUDGET if records_budget is None else records_budget
+  if callable(bound_per_row):  # a bound that depends on the incidence
+    bound_per_row = bound_per_row(inc)
   if chunk_sampler_fn is not None and bound_per_row * (inc.N + inc.E) > budget:
     # the stream does not fit: sample and train row-range chunks in turn
     chunks = _row_chunks(inc, bound_per_row, budget)
@@ -185,16 +187,19 @@ def EmbedHg2vBoolean(hypergraph, dimension, num_neighbors=5, num_samples=200,
     return chunk
 
   # per row at most q nn (or ee) and q node-edge records, q = int(w * S)
-  # (hg2v_sample.py:138-194), plus 3 negative blocks of int(w * neg_samples)
-  inc0 = hypergraph if isinstance(hypergraph, Incidence) else None
-  wmax = 1.0 if inc0 is None else float(max(inc0.node_weight.max(initial=1),
-                                            inc0.edge_weight.max(initial=1)))
+  # (hg2v_sample.py:138-194), plus 3 negative blocks of int(w * neg_samples),
+  # w the largest node / edge weight of the compressed incidence (any float
+  # in the proto, default 1)
+  def bound_per_row(inc):
+    wmax = float(max(np.max(inc.node_weight, initial=0.0),
+                     np.max(inc.edge_weight, initial=0.0), 0.0))
+    return int(wmax * 2 * num_samples) + int(wmax * 3 * neg_samples) + 2
+
   emb = _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors,
                                  sampler_fn, _hgx.LOSS_KLD, _hgx.ACT_SIGMOID,
                                  batch_size, epochs, debug_summary_path,
                                  disable_pbar, chunk_sampler_fn=chunk_sampler_fn,
-                                 bound_per_row=int(wmax * (2 * num_samples +
-                                                           3 * neg_samples)),
+                                 bound_per_row=bound_per_row,
                                  records_budget=records_budget)
   emb.method_name = "HG2V_BOOLEAN"
   return emb

@@ -107,22 +107,25 @@ def shard_range(n, world, rank):
 
 def sample_sharded(inc, num_neighbors, num_samples, ctx=None, seed=0,
                    kind="hobe", node_quota=None, edge_quota=None, group=None,
-                   gather=True, device=None):
+                   gather=True, device=None, rows=None):
   """Row-sharded sampling over the ranks of a torch.distributed group
   (sampling shards by row with no data-path collective).
 
-  Rank g samples only its node rows [n0, n1) and edge rows [e0, e1)
-  (kind "hobe": AlgebraicDistanceSamples, quota S per row unless quotas are
-  given; kind "fobe": BooleanSamples with the given per-row quotas): the
-  other rows' quotas are 0. Every draw is keyed by (seed, pattern, row), so with the same seed
-  on every rank the ranks' rows are exactly the rows a single process would
-  draw. A count all-gather gives every rank the kind-block sizes of every
-  rank. With `gather`, the per-rank streams are then all-gathered and laid
-  out kind block by kind block, ranks in row order inside each block: the
-  reference's record order (nn, ee, ne node rows, ne edge rows, ...), the
-  stream every training replica needs. The K neighbour draws of node-edge
-  records are keyed by the record's position, so only they differ from a
-  single-process run (same distribution).
+  `rows` = ((n_lo, n_hi), (e_lo, e_hi)) restricts the call to one row-range
+  chunk of the graph (fit_streaming, default: every row). Rank g samples
+  only its share of those rows (node rows [n0, n1), edge rows [e0, e1),
+  contiguous splits of the chunk; kind "hobe": AlgebraicDistanceSamples,
+  quota S per row unless quotas are given; kind "fobe": BooleanSamples with
+  the given per-row quotas): the other rows' quotas are 0. Every draw,
+  including the K neighbour draws of node-edge records, is keyed by (seed,
+  pattern or block, row, rank in the row), so with the same seed on every
+  rank the ranks' rows are exactly the rows a single process would draw. A
+  count all-gather gives every rank the kind-block sizes of every rank.
+  With `gather`, the per-rank streams are then all-gathered and laid out
+  kind block by kind block, ranks in row order inside each block: the
+  reference's record order (nn, ee, ne node rows, ne edge rows, ...) of the
+  chunk, the stream every training replica needs, identical to a
+  single-process call on the same rows.
 
   Collectives: RCCL on device buffers for a GPU device (the records never
   leave HBM), gloo through host arrays otherwise. Returns
@@ -133,8 +136,10 @@ def sample_sharded(inc, num_neighbors, num_samples, ctx=None, seed=0,
   ctx = ctx or get_context()
   world, rank = dist.get_world_size(group), dist.get_rank(group)
   K = num_neighbors
-  n0, n1 = shard_range(inc.N, world, rank)
-  e0, e1 = shard_range(inc.E, world, rank)
+  (nl, nh), (el, eh) = rows if rows is not None else ((0, inc.N), (0, inc.E))
+  assert 0 <= nl <= nh <= inc.N and 0 <= el <= eh <= inc.E
+  n0, n1 = (nl + x for x in shard_range(nh - nl, world, rank))
+  e0, e1 = (el + x for x in shard_range(eh - el, world, rank))
   if node_quota is None:  # HOBE: S per row (hg2v_sample.py:659-703)
     assert kind == "hobe"
     node_quota = np.full(inc.N, num_samples, np.int32)
@@ -168,16 +173,21 @@ def sample_sharded(inc, num_neighbors, num_samples, ctx=None, seed=0,
       [np.zeros((1, allsz.shape[1]), np.int64), np.cumsum(allsz, 0)[:-1]], 0)
   src = np.concatenate([np.zeros((world, 1), np.int64),
                         np.cumsum(allsz, 1)[:, :-1]], 1)
-  li = torch.zeros((max(maxn, 1), R), dtype=torch.int32, device=dev)
-  lt = torch.zeros((max(maxn, 1), 3), dtype=torch.float32, device=dev)
-  nl = int(n_loc[rank])
+  # rows past a rank's count are never read: no fill is needed
+  li = torch.empty((max(maxn, 1), R), dtype=torch.int32, device=dev)
+  lt = torch.empty((max(maxn, 1), 3), dtype=torch.float32, device=dev)
+  nl_ = int(n_loc[rank])
   if gpu:
-    if nl:
+    if nl_:
+      # the export runs on the context's stream: torch's stream (which owns
+      # li / lt and may still be using their memory) must be done first;
+      # records_export returns after its copies completed
+      torch.cuda.current_stream(dev).synchronize()
       ctx.records_export(li.data_ptr(), lt.data_ptr())
   else:
     hi, ht = ctx.records_get()
-    li[:nl] = torch.from_numpy(hi)
-    lt[:nl] = torch.from_numpy(ht)
+    li[:nl_] = torch.from_numpy(hi)
+    lt[:nl_] = torch.from_numpy(ht)
   gi = [torch.empty_like(li) for _ in range(world)]
   gt = [torch.empty_like(lt) for _ in range(world)]
   dist.all_gather(gi, li, group=group)
@@ -191,12 +201,34 @@ def sample_sharded(inc, num_neighbors, num_samples, ctx=None, seed=0,
         d, s0 = int(dst[r, j]), int(src[r, j])
         fi[d:d + c] = gi[r][s0:s0 + c]
         ft[d:d + c] = gt[r][s0:s0 + c]
+  del gi, gt, li, lt
   if gpu:
     torch.cuda.synchronize(dev)
     ctx.records_import(total, K, fi.data_ptr(), ft.data_ptr(), gbounds)
   else:
     ctx.records_set(fi[:total].numpy(), ft[:total].numpy())
   return total, allsz
+
+
+def sharded_chunk_fn(inc, num_neighbors, num_samples, chunks, ctx=None,
+                     seed=0, kind="hobe", node_quota=None, edge_quota=None,
+                     group=None, device=None):
+  """chunk_fn for Hg2vModel.fit_streaming over row-sharded sampling: chunk c
+  (((n_lo, n_hi), (e_lo, e_hi)) = chunks[c]) is sampled by every rank on its
+  share of the chunk's rows and all-gathered, so each training replica holds
+  only one chunk's stream at a time (the reference materialises
+  the whole stream in host RAM, embedding.py:277-284). Returns the records
+  of the chunk now resident on ctx, identical to a single-process
+  sample of the same rows (sample_sharded)."""
+  ctx = ctx or get_context()
+
+  def chunk(c):
+    total, _ = sample_sharded(inc, num_neighbors, num_samples, ctx=ctx,
+                              seed=seed, kind=kind, node_quota=node_quota,
+                              edge_quota=edge_quota, group=group,
+                              device=device, rows=chunks[c])
+    return total
+  return chunk
 
 
 def BooleanSamples(hypergraph, num_neighbors, num_samples, neg_samples=0,
@@ -359,4 +391,5 @@ def ModelInputToArrays(features, targets):
 __all__ = ["SimilarityRecord", "BooleanSamples", "AlgebraicDistanceSamples",
            "WeightedJaccardSamples", "sample_jaccard",
            "SamplesToModelInput", "ModelInputToArrays", "DeviceRecords",
+           "sample_sharded", "sharded_chunk_fn", "shard_range",
            "sample_fobe", "sample_hobe", "records_from_arrays"]

@@ -6,11 +6,16 @@
  * thread-compatible: use one per thread) and no global state.
  *
  * Every call returns 0 on success or a negative HGX_E* code; the message is
- * in hgx_last_error(ctx). The Python host package (hypergraphembedding_amd)
- * maps HGX_EINVAL -> AssertionError (the reference's precondition style,
- * e.g. embedding.py:83-85, hg2v_sample.py:646-647), HGX_EZERODIV ->
- * ZeroDivisionError (algebraic_distance.py:49 on an isolated row) and the
- * rest -> RuntimeError.
+ * in hgx_last_error(ctx). The Python host package (hypergraphembedding_amd,
+ * _hgx._raise) maps
+ *   HGX_EINVAL   -> AssertionError (the reference's precondition style,
+ *                   e.g. embedding.py:83-85, hg2v_sample.py:646-647)
+ *   HGX_EZERODIV -> ZeroDivisionError (algebraic_distance.py:49 on an
+ *                   isolated row)
+ *   HGX_EVALUE   -> ValueError (np.random.choice on an empty row,
+ *                   hg2v_sample.py:49-51)
+ *   HGX_ENUMERIC -> FloatingPointError (trainer fixed-point range left)
+ *   the rest (EHIP, ENOMEM, ESTATE, EUNSUP) -> RuntimeError.
  *
  * Each entry point names the reference interface it replaces
  * (JSybrandt/HypergraphEmbedding, hypergraph_embedding/<file>:<line>).
@@ -245,8 +250,13 @@ int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
  * applied by the next launch, the padding row likewise) and batches that
  * took the two-kernel step (train_fwd_bwd + train_update; tuning
  * "train_fused" 0 forces it). Same Keras semantics either way
- * (embedding.py:269-305, hg2v_model.py:51-203); the two differ only in the
- * summation order of a row's slot gradients. */
+ * (embedding.py:269-305, hg2v_model.py:51-203). They differ in how a row's
+ * slot gradients are summed: the two-kernel step adds them in fp32, the
+ * deferred-row step rounds each slot gradient (after the 1/batch factor) to
+ * the nearest multiple of 2^-44 and adds them exactly as 64-bit integers
+ * (order-free, bitwise reproducible): a quantisation of 2^-45 absolute per
+ * slot, so values below 2^-45 (~2.8e-14) vanish. A slot gradient of
+ * magnitude >= 32 fails the call with HGX_ENUMERIC. */
 int hgx_train_path_stats(hgx_ctx *ctx, int64_t *fused_batches,
                          int64_t *split_batches);
 /* Of the last hgx_train: step batches launched in the MULTI pending-slot form

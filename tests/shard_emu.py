@@ -156,3 +156,73 @@ class ShardEmu:
 
   def alg_get(self):
     return self.X, self.Y
+
+
+class SampleEmu:
+  """Test double of the row-keyed device samplers for the row-sharded
+  sampling driver (hg2v_sample.sample_sharded / sharded_chunk_fn): the same
+  contract as hgx_sample_hobe_rows / hgx_sample_fobe -- kind blocks nn, ee,
+  ne node rows, ne edge rows, each in row order; every draw keyed by (seed,
+  block, row, rank in row) -- on a small incidence with numpy. Records are
+  host arrays; records_blocks / records_get / records_set as the Context."""
+  device = None
+
+  def upload(self, inc):
+    self.inc = inc
+    A = np.zeros((inc.N, inc.E), bool)
+    A[np.repeat(np.arange(inc.N), np.diff(inc.rp_n)), inc.col_n] = True
+    self.pat = [A.astype(int) @ A.T.astype(int) > 0,       # nn  (A A^T)
+                A.T.astype(int) @ A.astype(int) > 0,       # ee  (A^T A)
+                (A.astype(int) @ A.T.astype(int) @ A.astype(int)) > 0,  # ne
+                (A.T.astype(int) @ A.astype(int) @ A.T.astype(int)) > 0]
+
+  def _rows(self, blk, q, seed, K):
+    inc, out = self.inc, []
+    for r in np.flatnonzero(q):
+      cols = np.flatnonzero(self.pat[blk][r])
+      rs = np.random.RandomState([seed & 0xFFFFFFFF, blk, int(r)])
+      pick = np.sort(rs.choice(cols, min(int(q[r]), cols.size), replace=False))
+      for j, c in enumerate(pick):
+        rec = np.zeros(4 + 2 * K, np.int32)
+        t = np.zeros(3, np.float32)
+        v, e = (r, c) if blk == 2 else (c, r)
+        if blk == 0:
+          rec[0], rec[2] = r + 1, c + 1
+        elif blk == 1:
+          rec[1], rec[3] = r + 1, c + 1
+        else:
+          rec[0], rec[3] = v + 1, e + 1
+          ns = np.random.RandomState([seed & 0xFFFFFFFF, 16 + blk, int(r), j])
+          nodes_e = inc.col_e[inc.rp_e[e]:inc.rp_e[e + 1]]
+          edges_v = inc.col_n[inc.rp_n[v]:inc.rp_n[v + 1]]
+          rec[4:4 + K] = ns.choice(nodes_e, K) + 1
+          rec[4 + K:] = ns.choice(edges_v, K) + 1
+        t[min(blk, 2)] = ((r * 131 + c * 7 + blk) % 97) / 97.0
+        out.append((rec, t))
+    return out
+
+  def sample_hobe(self, seed, K, S, node_q=None, edge_q=None):
+    inc = self.inc
+    nq = np.full(inc.N, S) if node_q is None else np.asarray(node_q)
+    eq = np.full(inc.E, S) if edge_q is None else np.asarray(edge_q)
+    blocks = [self._rows(0, nq, seed, K), self._rows(1, eq, seed, K),
+              self._rows(2, nq, seed, K), self._rows(3, eq, seed, K)]
+    self.K = K
+    self.bounds = np.concatenate([[0], np.cumsum([len(b) for b in blocks])])
+    recs = [x for b in blocks for x in b]
+    self.idx = (np.stack([r for r, _ in recs]) if recs
+                else np.zeros((0, 4 + 2 * K), np.int32))
+    self.tgt = (np.stack([t for _, t in recs]) if recs
+                else np.zeros((0, 3), np.float32))
+    return self.idx.shape[0]
+
+  def records_blocks(self):
+    return self.bounds.astype(np.int64)
+
+  def records_get(self):
+    return self.idx.copy(), self.tgt.copy()
+
+  def records_set(self, idx, tgt):
+    self.idx = np.asarray(idx, np.int32).copy()
+    self.tgt = np.asarray(tgt, np.float32).copy()
+    self.bounds = np.array([0, self.idx.shape[0]], np.int64)

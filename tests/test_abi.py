@@ -57,3 +57,37 @@ def test_build_outputs_gfx950_code_object(lib_path):
     pytest.skip("no llvm-objdump")
   data = open(lib_path, "rb").read()
   assert b"gfx950" in data
+
+
+def _header_error_codes():
+  import re
+  with open(_hgx.HEADER) as f:
+    text = f.read()
+  return {m.group(1): int(m.group(2))
+          for m in re.finditer(r"#define (HGX_E[A-Z]+) (-\d+)", text)}
+
+
+# the exception each HGX_E* code becomes (include/hgx.h:8-19)
+EXPECTED_EXC = {"HGX_EINVAL": AssertionError, "HGX_EZERODIV": ZeroDivisionError,
+                "HGX_EVALUE": ValueError, "HGX_ENUMERIC": FloatingPointError,
+                "HGX_EHIP": RuntimeError, "HGX_ENOMEM": RuntimeError,
+                "HGX_ESTATE": RuntimeError, "HGX_EUNSUP": RuntimeError}
+
+
+def test_every_error_code_has_a_mapping():
+  """Every HGX_E* the header defines maps to the documented exception in
+  _hgx._raise, the module constants agree with the header, and the
+  reference-side ctypes stub in INTEGRATION.md maps the same codes."""
+  codes = _header_error_codes()
+  assert set(codes) == set(EXPECTED_EXC), set(codes) ^ set(EXPECTED_EXC)
+  for name, rc in codes.items():
+    assert getattr(_hgx, name) == rc, name
+    with pytest.raises(EXPECTED_EXC[name]) as ei:
+      _hgx._raise(rc, "x")
+    if EXPECTED_EXC[name] is RuntimeError:  # not a narrower mapping
+      assert type(ei.value) is _hgx.HgxError
+  doc = open(os.path.join(os.path.dirname(_hgx.HEADER), "..",
+                          "INTEGRATION.md")).read()
+  for name, exc in EXPECTED_EXC.items():
+    if exc is not RuntimeError:
+      assert f"{codes[name]}: {exc.__name__}" in doc, name

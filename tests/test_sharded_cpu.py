@@ -150,3 +150,72 @@ def test_sharded_compact_exchange_local_edges(tmp_path):
     assert int(d["wire"]) == 3 * 11 * 4  # the 3 bridge edges, k + 1 floats
     assert int(d["dense"]) == inc.E * 12 * 4
   assert np.abs(x - xr).max() <= 1e-4
+
+
+# ---- row-sharded sampling in row-range chunks (fit_streaming) --------------
+def _chunks(inc, n):
+  from hypergraphembedding_amd.embedding import _row_chunks
+  per_row = 40
+  budget = -(-per_row * (inc.N + inc.E) // n)
+  return _row_chunks(inc, per_row, budget)
+
+
+def _chunk_worker(rank, world, port, out_path, n_chunks):
+  import torch.distributed as dist
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  sys.path[:0] = [root, os.path.join(root, "oracle"),
+                  os.path.join(root, "tests")]
+  from conftest import golden_incidence as gi
+  from shard_emu import SampleEmu
+  from test_sharded_cpu import _chunks
+  from hypergraphembedding_amd.hg2v_sample import sharded_chunk_fn
+  os.environ["MASTER_ADDR"] = "127.0.0.1"
+  os.environ["MASTER_PORT"] = str(port)
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  inc = gi("csr_small.npz")
+  emu = SampleEmu()
+  emu.upload(inc)
+  chunks = _chunks(inc, n_chunks)
+  fn = sharded_chunk_fn(inc, 3, 6, chunks, ctx=emu, seed=77, kind="hobe",
+                        device="cpu")
+  out = {}
+  for c in (2, 0, 1):  # any chunk order (fit_streaming shuffles it)
+    n = fn(c)
+    idx, tgt = emu.records_get()
+    assert idx.shape[0] == n
+    out[f"idx{c}"], out[f"tgt{c}"] = idx, tgt
+  np.savez(out_path + f".{rank}.npz", **out)
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_chunked_sharded_sampling_equals_single_process(tmp_path, world):
+  """Row-range chunks sampled row-sharded over gloo ranks and all-gathered:
+  every rank holds, chunk by chunk, exactly the stream (ids, neighbour
+  lists, targets, kind-block order) a single process samples for that
+  chunk's rows -- so a replica never holds more than one chunk."""
+  import torch.multiprocessing as mp
+  sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+  from shard_emu import SampleEmu
+  out = str(tmp_path / "chunk")
+  mp.start_processes(_chunk_worker, args=(world, _free_port(), out, 3),
+                     nprocs=world, join=True, start_method="spawn")
+  inc = golden_incidence("csr_small.npz")
+  chunks = _chunks(inc, 3)
+  assert len(chunks) == 3
+  emu = SampleEmu()
+  emu.upload(inc)
+  seen = 0
+  for c, ((n0, n1), (e0, e1)) in enumerate(chunks):
+    nq = np.zeros(inc.N, np.int32)
+    eq = np.zeros(inc.E, np.int32)
+    nq[n0:n1], eq[e0:e1] = 6, 6
+    n = emu.sample_hobe(77, 3, 6, node_q=nq, edge_q=eq)
+    ridx, rtgt = emu.records_get()
+    seen += n
+    for r in range(world):
+      d = np.load(out + f".{r}.npz")
+      assert np.array_equal(d[f"idx{c}"], ridx), (c, r)
+      assert np.array_equal(d[f"tgt{c}"], rtgt), (c, r)
+  assert seen == emu.sample_hobe(77, 3, 6)  # the chunks tile the stream
