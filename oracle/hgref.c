@@ -217,24 +217,31 @@ int64_t hgref_spgemm(int64_t nrowA, const int32_t *Ap, const int32_t *Aj,
 static int algdist_half(int64_t R, int k, const int32_t *rp, const int32_t *col,
                         const int32_t *rp_src, const double *self_in,
                         const double *src, double *out) {
-  double *acc = (double *)malloc(sizeof(double) * k);
-  for (int64_t a = 0; a < R; a++) {
-    if (rp[a + 1] == rp[a]) { free(acc); return -1; }
-    for (int d = 0; d < k; d++) acc[d] = 0.0;
-    double wsum = 0.0;
-    for (int32_t t = rp[a]; t < rp[a + 1]; t++) {
-      int32_t b = col[t];
-      double w = 1.0 / (double)(rp_src[b + 1] - rp_src[b]);
-      for (int d = 0; d < k; d++) acc[d] = acc[d] + src[(int64_t)b * k + d] * w;
-      wsum = wsum + w;
+  /* rows are independent and each row sums in CSR order, so the OpenMP
+   * split changes nothing in the result (checker speed at C4 only) */
+  int bad = 0;
+#pragma omp parallel
+  {
+    double *acc = (double *)malloc(sizeof(double) * k);
+#pragma omp for schedule(dynamic, 4096) reduction(|: bad)
+    for (int64_t a = 0; a < R; a++) {
+      if (rp[a + 1] == rp[a]) { bad = 1; continue; }
+      for (int d = 0; d < k; d++) acc[d] = 0.0;
+      double wsum = 0.0;
+      for (int32_t t = rp[a]; t < rp[a + 1]; t++) {
+        int32_t b = col[t];
+        double w = 1.0 / (double)(rp_src[b + 1] - rp_src[b]);
+        for (int d = 0; d < k; d++) acc[d] = acc[d] + src[(int64_t)b * k + d] * w;
+        wsum = wsum + w;
+      }
+      for (int d = 0; d < k; d++) {
+        double bd = acc[d] / wsum;
+        out[a * k + d] = (self_in[a * k + d] + bd) / 2.0;
+      }
     }
-    for (int d = 0; d < k; d++) {
-      double bd = acc[d] / wsum;
-      out[a * k + d] = (self_in[a * k + d] + bd) / 2.0;
-    }
+    free(acc);
   }
-  free(acc);
-  return 0;
+  return bad ? -1 : 0;
 }
 
 int hgref_algdist(int64_t N, int64_t E, int k, int iters, const int32_t *rp_n,
@@ -471,15 +478,33 @@ float hgref_dist_weight(const float *a, const float *b, int k) {
   return dist_weight(a, b, k);
 }
 
-/* sorted-list intersection of rows i and j of P; src/tgt coords */
+/* first position in [lo, hi) of col with col[pos] >= v (galloping then
+ * binary search) */
+static int32_t seek(const int32_t *col, int32_t lo, int32_t hi, int32_t v) {
+  int32_t step = 1, b = lo;
+  while (b < hi && col[b] < v) { lo = b + 1; b += step; step <<= 1; }
+  if (b > hi) b = hi;
+  while (lo < b) {
+    int32_t m = lo + (b - lo) / 2;
+    if (col[m] < v) lo = m + 1; else b = m;
+  }
+  return lo;
+}
+
+/* sorted-list intersection of rows i and j of P; src/tgt coords. The
+ * reference takes the max over the shared targets of min(w_it, w_jt)
+ * (hg2v_sample.py:527-543); max and min are exact, so visiting the shared
+ * targets by merge or by galloping from the shorter row gives the same
+ * float. Galloping keeps the checker usable on power-law hub rows. */
 static float same_type_prob(const int32_t *rp, const int32_t *col, int32_t i,
                             int32_t j, const float *src, const float *tgt,
                             int k) {
   int32_t a = rp[i], ae = rp[i + 1], b = rp[j], be = rp[j + 1];
   float prob = 0.0f;  /* prob = 0; prob = max(prob, min(w_ik, w_jk)) */
+  const int gallop = (ae - a) * 16 < (be - b) || (be - b) * 16 < (ae - a);
   while (a < ae && b < be) {
-    if (col[a] < col[b]) a++;
-    else if (col[a] > col[b]) b++;
+    if (col[a] < col[b]) a = gallop ? seek(col, a, ae, col[b]) : a + 1;
+    else if (col[a] > col[b]) b = gallop ? seek(col, b, be, col[a]) : b + 1;
     else {
       int32_t t = col[a];
       float wi = dist_weight(src + (int64_t)i * k, tgt + (int64_t)t * k, k);
@@ -500,6 +525,8 @@ void hgref_hobe_probs(int kind, int64_t n, const int32_t *pa, const int32_t *pb,
                       const int32_t *rp_e, const int32_t *col_e,
                       const float *alg_node, const float *alg_edge, int k,
                       float *out) {
+  /* pairs are independent: OpenMP only for checker speed at C4 */
+#pragma omp parallel for schedule(dynamic, 16) if (n > 64)
   for (int64_t t = 0; t < n; t++) {
     float p = 0.0f;
     if (kind == 0) {

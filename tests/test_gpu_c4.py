@@ -1,0 +1,246 @@
+"""BASELINE.json configs[3] (C4) and configs[4] (C5) at full size on the GPU:
+the power-law hypergraph of 10M nodes / 5M edges (nnz 2.0e8, largest edge
+1.7M nodes), through checks whose cost does not grow with the
+record stream.
+
+C4  HG2V_ALG_DIST d=256 (hg2v_sample.py:632-717, embedding.py:389-416):
+    * alg-dist, 3 iterations on the whole graph, vs the float64 oracle
+      (max-abs 1e-4);
+    * HOBE on a seeded 0.5% of node rows and of edge rows (quota S = 200,
+      the rest 0): the rejection and uniform-column paths are taken; exact
+      per-row counts min(S, |pattern row|) and pair validity on sampled rows
+      of all four kind blocks (2-hop nn / ee, 3-hop ne from node and edge
+      rows); nn / ee / ne probabilities of 5,000 records per kind bit-exact
+      vs the oracle on the device's own coordinates;
+    * one d=256 epoch on full-size tables (10M+1 and 5M+1 rows) is bitwise
+      deterministic, and the loss falls over two epochs.
+C5  CombineEmbeddings N_E_SUPERVISED (combine_embeddings_util.py:78-174) on
+    full-size 10M x 512 / 5M x 512 [FOBE | HOBE] tables of this graph: a
+    ~2M-sample slice drawn over the whole graph (random incidences labelled
+    1, five times as many missing pairs labelled 0), bit-exact vs
+    oracle/mlpref.c on 1,200 of them, then one epoch with a finite loss.
+"""
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+S, K, D, QFRAC = 200, 5, 256, 0.005
+_cache = {}
+
+
+@pytest.fixture(scope="module")
+def g():
+  from hypergraphembedding_amd.synthetic import powerlaw_hypergraph
+  inc = powerlaw_hypergraph(seed=0)
+  assert inc.N == 10_000_000 and inc.nnz > 1.9e8
+  assert inc.edge_size().max() > 1_000_000  # power-law hub edges
+  return inc
+
+
+@pytest.fixture(scope="module")
+def ctx(g):
+  from hypergraphembedding_amd import _hgx
+  c = _hgx.Context(0)
+  c.upload(g)
+  yield c
+  c.close()
+
+
+def _init(inc):
+  r = O.Rng(7)
+  return r.random((inc.N, 10)), r.random((inc.E, 10))
+
+
+def _quotas(inc):
+  rs = np.random.RandomState(2)
+  nq = np.where(rs.random_sample(inc.N) < QFRAC, S, 0).astype(np.int32)
+  eq = np.where(rs.random_sample(inc.E) < QFRAC, S, 0).astype(np.int32)
+  return nq, eq
+
+
+def _gather(rp, col, rows):
+  """Concatenated CSR rows `rows` (vectorised)."""
+  rows = np.asarray(rows, np.int64)
+  starts = rp[rows].astype(np.int64)
+  lens = rp[rows + 1].astype(np.int64) - starts
+  off = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens)
+  return col[off + np.arange(int(lens.sum()), dtype=np.int64)]
+
+
+def _mask(n, ids):
+  m = np.zeros(n, bool)
+  m[ids] = True
+  return m
+
+
+def test_c4_algdist_3_iterations_vs_oracle(ctx, g):
+  x0, y0 = _init(g)
+  x, y = ctx.alg_dist(x0, y0, 3)
+  xr, yr = O.algdist(g, x0, y0, 3)
+  assert np.abs(x - xr).max() <= 1e-4
+  assert np.abs(y - yr).max() <= 1e-4
+
+
+def _sample(ctx, g, seed=41):
+  x0, y0 = _init(g)
+  ctx.alg_set(x0, y0)
+  ctx.alg_run(20)  # HOBE's k = 10, 20 iterations (embedding.py:401-402)
+  nq, eq = _quotas(g)
+  n = ctx.sample_hobe(seed, K, S, node_q=nq, edge_q=eq)
+  return n, nq, eq
+
+
+def test_c4_hobe_counts_validity_and_probabilities(ctx, g):
+  from hypergraphembedding_amd import _hgx
+  n, nq, eq = _sample(ctx, g)
+  union_rows, fallback_rows = ctx.sample_stats()
+  assert union_rows > 0 and ctx.sample_uniform_rows() > 0  # power-law paths
+  ax, ay = ctx.alg_get()
+  idx, tgt = ctx.records_get()
+  b = ctx.records_blocks()
+  assert b.size == 5 and b[-1] == n == idx.shape[0]
+  nn, ee, nen, nee = (slice(int(b[i]), int(b[i + 1])) for i in range(4))
+  assert (b[1] - b[0]) <= int(nq.sum()) and (b[2] - b[1]) <= int(eq.sum())
+  rs = np.random.RandomState(5)
+  # --- per-row counts and validity on sampled rows of every block ---
+  def rows_of(block, col, r):
+    c = idx[block, col] - 1
+    lo, hi = np.searchsorted(c, r), np.searchsorted(c, r, side="right")
+    return idx[block][lo:hi]
+
+  for v in rs.choice(np.flatnonzero(nq), 8, replace=False):
+    edges_v = g.col_n[g.rp_n[v]:g.rp_n[v + 1]]
+    n2 = _mask(g.N, _gather(g.rp_e, g.col_e, edges_v))  # A A^T row (2-hop)
+    got = rows_of(nn, 0, v)[:, 2] - 1
+    assert got.size == min(S, int(n2.sum()))
+    assert np.unique(got).size == got.size and n2[got].all()
+    e3 = _mask(g.E, _gather(g.rp_n, g.col_n, np.flatnonzero(n2)))  # A A^T A
+    got = rows_of(nen, 0, v)[:, 3] - 1
+    assert got.size == min(S, int(e3.sum()))
+    assert np.unique(got).size == got.size and e3[got].all()
+  for e in rs.choice(np.flatnonzero(eq), 8, replace=False):
+    nodes_e = g.col_e[g.rp_e[e]:g.rp_e[e + 1]]
+    e2 = _mask(g.E, _gather(g.rp_n, g.col_n, nodes_e))  # A^T A row (2-hop)
+    got = rows_of(ee, 1, e)[:, 3] - 1
+    assert got.size == min(S, int(e2.sum()))
+    assert np.unique(got).size == got.size and e2[got].all()
+    got = rows_of(nee, 3, e)[:, 0] - 1  # A^T A A^T row: nodes of e2's edges
+    e2_ids = np.flatnonzero(e2)
+    big = int(np.diff(g.rp_e)[e2_ids].max())
+    n3 = (int(_mask(g.N, _gather(g.rp_e, g.col_e, e2_ids)).sum())
+          if big < S else big)  # |row| >= the largest member edge
+    assert got.size == min(S, n3)
+    assert np.unique(got).size == got.size
+    for u in got:
+      assert e2[g.col_n[g.rp_n[u]:g.rp_n[u + 1]]].any()
+  # neighbour lists of node-edge records come from the right rows
+  ne_all = np.arange(int(b[2]), int(b[4]))
+  for i in rs.choice(ne_all, 500, replace=False):
+    v, e = idx[i, 0] - 1, idx[i, 3] - 1
+    assert np.isin(idx[i, 4:4 + K] - 1, g.col_e[g.rp_e[e]:g.rp_e[e + 1]]).all()
+    assert np.isin(idx[i, 4 + K:] - 1, g.col_n[g.rp_n[v]:g.rp_n[v + 1]]).all()
+  # --- probabilities bit-exact vs the oracle on the device's coordinates ---
+  for kind, lo, hi, a_col, b_col, t_col in (
+      (_hgx.HOBE_NN, b[0], b[1], 0, 2, 0), (_hgx.HOBE_EE, b[1], b[2], 1, 3, 1),
+      (_hgx.HOBE_NE, b[2], b[4], 0, 3, 2)):
+    sel = np.sort(rs.choice(np.arange(int(lo), int(hi)), 5000, replace=False))
+    ref = O.hobe_probs(kind, idx[sel, a_col] - 1, idx[sel, b_col] - 1, g, ax, ay)
+    assert np.array_equal(tgt[sel, t_col], ref), kind
+    others = [c for c in range(3) if c != t_col]
+    assert np.all(tgt[sel][:, others] == 0)
+  assert tgt.min() >= 0 and tgt.max() <= 1
+
+
+def test_c4_hobe_d256_epoch_deterministic_and_learning(ctx, g):
+  from hypergraphembedding_amd import _hgx
+  n, _, _ = _sample(ctx, g)
+  assert n > 10_000_000
+  tabs = []
+  for _ in range(2):
+    ctx.model_init(D, g.N + 1, g.E + 1, seed=3)
+    ctx.train(batch=256, max_epochs=1, loss=_hgx.LOSS_MSE, act=_hgx.ACT_RELU,
+              min_delta=-1e30, shuffle_seed=11)
+    tabs.append(ctx.model_get())
+  assert np.array_equal(tabs[0][0], tabs[1][0])
+  assert np.array_equal(tabs[0][1], tabs[1][1])
+  del tabs
+  ctx.model_init(D, g.N + 1, g.E + 1, seed=3)
+  losses = ctx.train(batch=256, max_epochs=2, loss=_hgx.LOSS_MSE,
+                     act=_hgx.ACT_RELU, min_delta=-1e30, shuffle_seed=11)
+  assert len(losses) == 2 and np.all(np.isfinite(losses))
+  assert losses[1] < losses[0]
+  _cache["hobe"] = ctx.model_get()
+
+
+def test_c5_combiner_full_size_tables(ctx, g):
+  """N_E_SUPERVISED on [FOBE | HOBE] d=256 tables of every node and edge of
+  the 10M/5M graph (one epoch of each embedder on the 0.5% row quota)."""
+  from hypergraphembedding_amd import _hgx
+  nq, eq = _quotas(g)
+  if "hobe" not in _cache:
+    _sample(ctx, g)
+    ctx.model_init(D, g.N + 1, g.E + 1, seed=3)
+    ctx.train(batch=256, max_epochs=1, loss=_hgx.LOSS_MSE, act=_hgx.ACT_RELU,
+              min_delta=-1e30, shuffle_seed=11)
+    _cache["hobe"] = ctx.model_get()
+  ctx.sample_fobe(43, K, nq, eq)
+  ctx.model_init(D, g.N + 1, g.E + 1, seed=4)
+  ctx.train(batch=256, max_epochs=1, loss=_hgx.LOSS_KLD, act=_hgx.ACT_SIGMOID,
+            min_delta=-1e30, shuffle_seed=12)
+  fobe = ctx.model_get()
+  hobe = _cache.pop("hobe")
+  # _concatenate_embeddings (combine_embeddings_util.py:15-24): rows idx + 1
+  nt = np.concatenate([fobe[0][1:], hobe[0][1:]], 1)
+  et = np.concatenate([fobe[1][1:], hobe[1][1:]], 1)
+  del fobe, hobe
+  assert nt.shape == (g.N, 2 * D) and et.shape == (g.E, 2 * D)
+  # ~2M samples over the whole graph (_sample_hypergraph, :46-67): random
+  # incidences labelled 1 and five times as many missing pairs labelled 0
+  rs = np.random.RandomState(6)
+  npos = 340_000
+  pick = np.sort(rs.choice(g.nnz, npos, replace=False))
+  pos_n = (np.searchsorted(g.rp_n, pick, side="right") - 1).astype(np.int32)
+  pos_e = g.col_n[pick].astype(np.int32)
+  m = 5 * npos
+  cand_n = rs.randint(0, g.N, 2 * m).astype(np.int64)
+  cand_e = rs.randint(0, g.E, 2 * m).astype(np.int64)
+  key = np.repeat(np.arange(g.N, dtype=np.int64), np.diff(g.rp_n)) * g.E + g.col_n
+  cand = cand_n * g.E + cand_e  # key is sorted (CSR rows, sorted columns)
+  at = np.minimum(np.searchsorted(key, cand), key.size - 1)
+  keep = key[at] != cand
+  del key
+  neg_n = cand_n[keep][:m].astype(np.int32)
+  neg_e = cand_e[keep][:m].astype(np.int32)
+  node_row = np.concatenate([pos_n, neg_n])
+  edge_row = np.concatenate([pos_e, neg_e])
+  label = np.concatenate([np.ones(npos, np.float32), np.zeros(m, np.float32)])
+  assert label.size > 2_000_000
+  mlp = _hgx.Mlp(ctx, _hgx.MLP_NE_SUPERVISED, 2 * D, D)
+  lims = [np.sqrt(6.0 / (k + n)) for k, n in mlp.shapes]
+  w0 = np.concatenate([np.concatenate([rs.uniform(-l, l, k * n), np.zeros(n)])
+                       for l, (k, n) in zip(lims, mlp.shapes)]).astype(np.float32)
+  mlp.set_weights(w0)
+  mlp.set_tables(nt, et)
+  # (1) bit-exact vs the CPU restatement on 1,200 of the samples
+  sel = rs.choice(label.size, 1200, replace=False)
+  mlp.set_samples(node_row[sel], edge_row[sel], label[sel])
+  perms = rs.permutation(sel.size)[None, :]
+  mlp.fit(batch=256, max_epochs=1, min_delta=-1e30, seed=7, perms=perms)
+  wc, _ = O.mlp_fit(_hgx.MLP_NE_SUPERVISED, 2 * D, D, w0, nt, et,
+                    node_row[sel], edge_row[sel], label[sel], perms,
+                    batch=256, min_delta=-1e30, seed=7)
+  assert np.abs(mlp.get_weights() - wc).max() == 0.0
+  # (2) one epoch over the whole slice on the device
+  mlp.set_weights(w0)
+  mlp.set_samples(node_row, edge_row, label)
+  losses = mlp.fit(batch=256, max_epochs=1, min_delta=-1e30, seed=8)
+  assert len(losses) == 1 and np.isfinite(losses[0]) and 0 <= losses[0] <= 0.25
+  st = mlp.stats()
+  assert st["samples"] == label.size
+  jn = mlp.predict(1, rs.randint(0, g.N, 4096).astype(np.int32), None)
+  assert jn.shape == (4096, D) and np.isfinite(jn).all()
+  mlp.close()

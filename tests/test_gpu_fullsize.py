@@ -3,6 +3,8 @@ edges, nnz 2.0e6), through checks whose cost does not grow with the stream:
   * alg-dist, 20 iterations, against the float64 oracle (max-abs 1e-4);
   * HOBE stream: exact per-row counts min(S, |pattern row|) and pair
     validity on a random sample of rows, total count = the sum over all rows;
+    every record of those rows (nn, ee and their node-edge rows) carries the
+    oracle's probability bit for bit, computed from the device coordinates;
   * trainer: bitwise determinism of a full epoch (same init, same shuffle
     seed -> identical tables) and a decreasing epoch loss.
 """
@@ -56,7 +58,9 @@ def test_c3_hobe_stream_counts_and_pairs(ctx, c3):
   ctx.alg_set(x0, y0)
   ctx.alg_run(20)
   n = ctx.sample_hobe(99, K, S)
+  ax, ay = ctx.alg_get()  # the coordinates the device probabilities used
   idx, tgt = ctx.records_get()
+  bnd = ctx.records_blocks()
   assert idx.shape == (n, 4 + 2 * K)
   ln, le, rn, re = (idx[:, i] for i in range(4))
   nn = (ln > 0) & (rn > 0)
@@ -66,16 +70,34 @@ def test_c3_hobe_stream_counts_and_pairs(ctx, c3):
   cnt_nn = np.bincount(ln[nn] - 1, minlength=inc.N)
   cnt_ee = np.bincount(le[ee] - 1, minlength=inc.E)
   rs = np.random.RandomState(0)
-  for v in rs.choice(inc.N, 64, replace=False):
+  checked = np.zeros(n, bool)
+  ne_n_blk = np.zeros(n, bool)
+  ne_n_blk[int(bnd[2]):int(bnd[3])] = True
+  ne_e_blk = np.zeros(n, bool)
+  ne_e_blk[int(bnd[3]):int(bnd[4])] = True
+  sel_v = rs.choice(inc.N, 64, replace=False)
+  for v in sel_v:
     row = _two_hop(inc.rp_n, inc.col_n, inc.rp_e, inc.col_e, v)  # A A^T
     assert cnt_nn[v] == min(S, row.size)
     got = rn[nn][ln[nn] - 1 == v] - 1
     assert np.unique(got).size == got.size and np.isin(got, row).all()
-  for e in rs.choice(inc.E, 64, replace=False):
+  sel_e = rs.choice(inc.E, 64, replace=False)
+  for e in sel_e:
     row = _two_hop(inc.rp_e, inc.col_e, inc.rp_n, inc.col_n, e)  # A^T A
     assert cnt_ee[e] == min(S, row.size)
     got = re[ee][le[ee] - 1 == e] - 1
     assert np.unique(got).size == got.size and np.isin(got, row).all()
+  # every record of those rows: probability bit-exact vs the oracle
+  rows_v, rows_e = np.isin(ln - 1, sel_v), np.isin(le - 1, sel_e)
+  for kind, m, a, b_, col in (
+      (O.HOBE_NN, nn & rows_v, ln, rn, 0), (O.HOBE_EE, ee & rows_e, le, re, 1),
+      (O.HOBE_NE, ne_n_blk & rows_v, ln, re, 2),
+      (O.HOBE_NE, ne_e_blk & np.isin(re - 1, sel_e), ln, re, 2)):
+    assert m.sum() >= 64
+    ref = O.hobe_probs(kind, a[m] - 1, b_[m] - 1, inc, ax, ay)
+    assert np.array_equal(tgt[m, col], ref), kind
+    checked |= m
+  assert checked.sum() > 4 * 64 * 100
   # probabilities are in [0, 1]; the targets not of a record's kind are 0
   assert tgt.min() >= 0 and tgt.max() <= 1
   assert np.all(tgt[nn, 1:] == 0) and np.all(tgt[ee][:, [0, 2]] == 0)
