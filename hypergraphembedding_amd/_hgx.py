@@ -95,6 +95,13 @@ SIGNATURES = {
     "hgx_proto_write_embedding": (_int, [_i64, _vp, _vp, _i64, _vp, _vp, _int,
                                          ctypes.c_char_p, _vp, _i64, _pi64]),
     "hgx_host_last_error": (ctypes.c_char_p, []),
+    "hgx_proto_parse_embedding": (_int, [_vp, _i64, ctypes.POINTER(_vp), _pi64,
+                                         _pi64, _pi64,
+                                         ctypes.POINTER(_i32)]),
+    "hgx_proto_embedding_fill": (_int, [_vp, _vp, _vp, _vp, _vp,
+                                        ctypes.c_char_p, _i64]),
+    "hgx_proto_embedding_method_len": (_i64, [_vp]),
+    "hgx_proto_embedding_free": (None, [_vp]),
     "hgx_proto_write_hypergraph": (_int, [_i32, _i32, _vp, _vp, _vp, _vp, _vp,
                                           _vp, _vp, _i64, _pi64]),
     "hgx_mlp_create": (_int, [_vp, _int, _int, _int, ctypes.POINTER(_vp)]),
@@ -628,6 +635,41 @@ def write_embedding_bytes(node_ids, node_tab, edge_ids, edge_tab, method_name):
                                        ctypes.byref(ln))
   if rc != HGX_OK:
     _host_raise(rc)
+  return out
+
+
+def parse_embedding(buf):
+  """Serialized HypergraphEmbedding bytes (one message or concatenated
+  shards; bytes / memoryview / uint8 array / mmap) -> dict(node_ids,
+  node_tab, edge_ids, edge_tab, dim, width, method_name)
+  (hgx_proto_parse_embedding)."""
+  a = np.frombuffer(buf, dtype=np.uint8)
+  h = _vp()
+  nn, ne, w = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+  dim = ctypes.c_int32()
+  rc = lib().hgx_proto_parse_embedding(_ptr(a) if a.size else None, a.size,
+                                       ctypes.byref(h), ctypes.byref(nn),
+                                       ctypes.byref(ne), ctypes.byref(w),
+                                       ctypes.byref(dim))
+  if rc != HGX_OK:
+    _host_raise(rc)
+  try:
+    W = w.value
+    out = {"node_ids": np.empty(nn.value, np.int64),
+           "node_tab": np.empty((nn.value, W), np.float32),
+           "edge_ids": np.empty(ne.value, np.int64),
+           "edge_tab": np.empty((ne.value, W), np.float32),
+           "dim": dim.value, "width": W}
+    mlen = lib().hgx_proto_embedding_method_len(h)
+    name = ctypes.create_string_buffer(mlen + 1)
+    rc = lib().hgx_proto_embedding_fill(
+        h, _ptr(out["node_ids"]), _ptr(out["node_tab"]), _ptr(out["edge_ids"]),
+        _ptr(out["edge_tab"]), name, mlen + 1)
+    if rc != HGX_OK:
+      _host_raise(rc)
+    out["method_name"] = name.value.decode()
+  finally:
+    lib().hgx_proto_embedding_free(h)
   return out
 
 

@@ -52,10 +52,18 @@ def coords_to_embedding(inc, x, y, dimension, method_name):
   """HypergraphEmbedding keyed by the original ids (KerasModelToEmbedding,
   hg2v_model.py:31-48 / algebraic_distance.py:166-174): serialized by the
   native writer and parsed once, instead of filling the maps field by field
-  in Python (same message; map entries in ascending id order)."""
+  in Python (same message; map entries in ascending id order). A message
+  beyond protobuf's 2 GiB limit (C4 at d=256: ~10 GB) cannot exist as one
+  HypergraphEmbedding: a proto_native.ShardedEmbedding (the same message
+  surface, written as shards of complete messages) is returned instead."""
   from . import _hgx
+  from .proto_native import PROTO_LIMIT, ShardedEmbedding, message_bytes
   x = np.ascontiguousarray(x, np.float32).reshape(inc.N, dimension)
   y = np.ascontiguousarray(y, np.float32).reshape(inc.E, dimension)
+  if message_bytes(inc.node_ids, inc.edge_ids, dimension,
+                   method_name) > PROTO_LIMIT:
+    return ShardedEmbedding(inc.node_ids, x, inc.edge_ids, y, dimension,
+                            method_name)
   emb = HypergraphEmbedding()
   emb.ParseFromString(_hgx.write_embedding_bytes(inc.node_ids, x, inc.edge_ids,
                                                  y, method_name).tobytes())

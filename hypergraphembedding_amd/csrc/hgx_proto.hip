@@ -443,3 +443,200 @@ extern "C" int hgx_proto_write_hypergraph(
   return (size_t)(p - out) == total ? HGX_OK
                                     : host_fail(HGX_EINVAL, "internal size mismatch");
 }
+
+// HypergraphEmbedding reader (hypergraph.proto:26-35): the merged message of
+// one serialized buffer -- a single message, or shards concatenated (the
+// wire format merges them: map entries union, last key wins, last dim /
+// method_name wins). Pass 1 walks the top-level fields (length prefixes
+// only); pass 2 decodes the map entries on threads. `values` may be packed
+// or unpacked; every entry must carry the same number of values.
+namespace {
+struct EmbEntry {
+  int32_t key;
+  int32_t field;  // 1 node, 2 edge
+  const uint8_t *p, *end;
+};
+}  // namespace
+
+struct hgx_emb {
+  int64_t width = 0;
+  int32_t dim = 0;
+  std::string method;
+  std::vector<int64_t> node_ids, edge_ids;
+  std::vector<float> node_tab, edge_tab;
+};
+
+extern "C" int hgx_proto_parse_embedding(const uint8_t *buf, int64_t len,
+                                         hgx_emb **out, int64_t *n_nodes,
+                                         int64_t *n_edges, int64_t *width,
+                                         int32_t *dim) {
+  if (!out || (len > 0 && !buf) || len < 0)
+    return host_fail(HGX_EINVAL, "null buffer or handle");
+  *out = nullptr;
+  auto *h = new hgx_emb();
+  std::vector<EmbEntry> ents;
+  Reader r{buf, buf + len};
+  while (r.ok && r.p < r.end) {
+    const uint64_t tag = r.varint();
+    const int field = (int)(tag >> 3), wt = (int)(tag & 7);
+    if ((field == 1 || field == 2) && wt == 2) {
+      Reader e = r.sub();
+      ents.push_back({0, field, e.p, e.end});
+    } else if (field == 3 && wt == 0) {
+      h->dim = (int32_t)r.varint();
+    } else if (field == 4 && wt == 2) {
+      Reader s = r.sub();
+      h->method.assign((const char *)s.p, (size_t)(s.end - s.p));
+    } else {
+      r.skip(wt);
+    }
+  }
+  if (!r.ok) {
+    delete h;
+    return host_fail(HGX_EINVAL, "malformed HypergraphEmbedding message");
+  }
+  // pass 2: key and value range of every entry, in parallel
+  const int64_t n = (int64_t)ents.size();
+  std::vector<int64_t> cnt((size_t)n, -1);
+  std::vector<const uint8_t *> vbeg((size_t)n), vend((size_t)n);
+  const int64_t per = (n + kChunksP - 1) / kChunksP;
+  std::vector<int> badc(kChunksP, 0);
+  run_chunks(kChunksP, [&](int c) {
+    const int64_t i0 = std::min(n, c * per), i1 = std::min(n, i0 + per);
+    for (int64_t i = i0; i < i1; i++) {
+      Reader e{ents[i].p, ents[i].end};
+      int64_t m = 0;
+      const uint8_t *vb = nullptr, *ve = nullptr;
+      bool ok = true;
+      while (e.ok && e.p < e.end && ok) {
+        const uint64_t t = e.varint();
+        const int f = (int)(t >> 3), w = (int)(t & 7);
+        if (f == 1 && w == 0) {
+          ents[i].key = (int32_t)e.varint();
+        } else if (f == 2 && w == 2) {  // Embedding{ repeated float values = 1 }
+          Reader v = e.sub();
+          if (vb) ok = false;  // a split value field: not written by anyone
+          vb = v.p;
+          ve = v.end;
+          while (v.ok && v.p < v.end) {
+            const uint64_t tv = v.varint();
+            const int fv = (int)(tv >> 3), wv = (int)(tv & 7);
+            if (fv == 1 && wv == 5) {
+              v.fixed32();
+              m++;
+            } else if (fv == 1 && wv == 2) {
+              Reader q = v.sub();
+              if ((q.end - q.p) % 4) ok = false;
+              m += (q.end - q.p) / 4;
+            } else {
+              v.skip(wv);
+            }
+          }
+          if (!v.ok) ok = false;
+        } else {
+          e.skip(w);
+        }
+      }
+      if (!e.ok || !ok) {
+        badc[c] = 1;
+        return;
+      }
+      cnt[i] = m;
+      vbeg[i] = vb;
+      vend[i] = ve;
+    }
+  });
+  for (int b : badc)
+    if (b) {
+      delete h;
+      return host_fail(HGX_EINVAL, "malformed HypergraphEmbedding entry");
+    }
+  h->width = n ? cnt[0] : (int64_t)h->dim;
+  for (int64_t i = 0; i < n; i++)
+    if (cnt[i] != h->width) {
+      delete h;
+      return host_fail(HGX_EINVAL, "embedding entries of different lengths (" +
+                                       std::to_string(cnt[i]) + " vs " +
+                                       std::to_string(h->width) + ")");
+    }
+  // last entry per key wins; ascending keys
+  std::vector<int64_t> order((size_t)n);
+  for (int64_t i = 0; i < n; i++) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+    if (ents[a].field != ents[b].field) return ents[a].field < ents[b].field;
+    return ents[a].key < ents[b].key;
+  });
+  std::vector<int64_t> keep;
+  keep.reserve((size_t)n);
+  for (int64_t t = 0; t < n; t++) {
+    const int64_t i = order[t];
+    if (t + 1 < n && ents[order[t + 1]].field == ents[i].field &&
+        ents[order[t + 1]].key == ents[i].key)
+      continue;
+    keep.push_back(i);
+  }
+  int64_t nn = 0;
+  while (nn < (int64_t)keep.size() && ents[keep[nn]].field == 1) nn++;
+  const int64_t ne = (int64_t)keep.size() - nn, W = h->width;
+  h->node_ids.resize((size_t)nn);
+  h->edge_ids.resize((size_t)ne);
+  h->node_tab.resize((size_t)(nn * W));
+  h->edge_tab.resize((size_t)(ne * W));
+  const int64_t nk = (int64_t)keep.size(), perk = (nk + kChunksP - 1) / kChunksP;
+  run_chunks(kChunksP, [&](int c) {
+    const int64_t t0 = std::min(nk, c * perk), t1 = std::min(nk, t0 + perk);
+    for (int64_t t = t0; t < t1; t++) {
+      const int64_t i = keep[t];
+      const bool isn = t < nn;
+      const int64_t row = isn ? t : t - nn;
+      (isn ? h->node_ids : h->edge_ids)[row] = ents[i].key;
+      float *dst = (isn ? h->node_tab.data() : h->edge_tab.data()) + row * W;
+      Reader v{vbeg[i], vend[i]};
+      int64_t m = 0;
+      while (v.p < v.end && m < W) {
+        const uint64_t tv = v.varint();
+        const int fv = (int)(tv >> 3), wv = (int)(tv & 7);
+        if (fv == 1 && wv == 5) {
+          const uint32_t bits = v.fixed32();
+          memcpy(dst + m++, &bits, 4);
+        } else if (fv == 1 && wv == 2) {
+          Reader q = v.sub();
+          const int64_t k = (q.end - q.p) / 4;
+          memcpy(dst + m, q.p, (size_t)k * 4);
+          m += k;
+        } else {
+          v.skip(wv);
+        }
+      }
+    }
+  });
+  *out = h;
+  if (n_nodes) *n_nodes = nn;
+  if (n_edges) *n_edges = ne;
+  if (width) *width = W;
+  if (dim) *dim = h->dim;
+  return HGX_OK;
+}
+
+extern "C" int hgx_proto_embedding_fill(const hgx_emb *h, int64_t *node_ids,
+                                        float *node_tab, int64_t *edge_ids,
+                                        float *edge_tab, char *method_name,
+                                        int64_t cap) {
+  if (!h) return host_fail(HGX_EINVAL, "null embedding handle");
+  if (node_ids) std::copy(h->node_ids.begin(), h->node_ids.end(), node_ids);
+  if (edge_ids) std::copy(h->edge_ids.begin(), h->edge_ids.end(), edge_ids);
+  if (node_tab) std::copy(h->node_tab.begin(), h->node_tab.end(), node_tab);
+  if (edge_tab) std::copy(h->edge_tab.begin(), h->edge_tab.end(), edge_tab);
+  if (method_name) {
+    if (cap < (int64_t)h->method.size() + 1)
+      return host_fail(HGX_EINVAL, "method_name buffer too small");
+    memcpy(method_name, h->method.c_str(), h->method.size() + 1);
+  }
+  return HGX_OK;
+}
+
+extern "C" int64_t hgx_proto_embedding_method_len(const hgx_emb *h) {
+  return h ? (int64_t)h->method.size() : -1;
+}
+
+extern "C" void hgx_proto_embedding_free(hgx_emb *h) { delete h; }

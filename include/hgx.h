@@ -357,6 +357,25 @@ int hgx_proto_write_embedding(int64_t n_nodes, const int64_t *node_ids,
                               const int64_t *edge_ids, const float *edge_tab,
                               int d, const char *method_name, uint8_t *out,
                               int64_t cap, int64_t *len);
+/* Native HypergraphEmbedding reader (hypergraph.proto:26-35): one buffer
+ * holding one message, or several shards of one embedding concatenated
+ * (protobuf's wire format merges them: map entries union, a repeated key
+ * keeps its last entry, the last dim / method_name wins). Any size, no
+ * 2 GiB message limit. Parse -> sizes (entries per map, `width` = values per
+ * entry, the same for every entry, and the dim field, 0 if unset); fill
+ * (ids ascending, tables n x width row-major; any pointer may be NULL;
+ * method_name NUL-terminated, cap >= hgx_proto_embedding_method_len + 1);
+ * free. Replaces HypergraphEmbedding.ParseFromString for embeddings
+ * written by runner.py:363-364 or by write_embedding's shards. */
+typedef struct hgx_emb hgx_emb;
+int hgx_proto_parse_embedding(const uint8_t *buf, int64_t len, hgx_emb **out,
+                              int64_t *n_nodes, int64_t *n_edges,
+                              int64_t *width, int32_t *dim);
+int hgx_proto_embedding_fill(const hgx_emb *h, int64_t *node_ids,
+                             float *node_tab, int64_t *edge_ids,
+                             float *edge_tab, char *method_name, int64_t cap);
+int64_t hgx_proto_embedding_method_len(const hgx_emb *h);
+void hgx_proto_embedding_free(hgx_emb *h);
 /* Hypergraph writer (test / bench data): compressed incidence + original
  * ids -> wire bytes (repeated fields unpacked, proto2's default). */
 int hgx_proto_write_hypergraph(int32_t N, int32_t E, const int32_t *rowptr_n,

@@ -176,6 +176,61 @@ def test_c4_hobe_d256_epoch_deterministic_and_learning(ctx, g):
   _cache["hobe"] = ctx.model_get()
 
 
+def test_c4_sharded_embedding_output(ctx, g, tmp_path):
+  """The C4 HOBE d=256 embedding (15M rows, ~19 GB of wire bytes: far past
+  protobuf's 2 GiB message limit) is written as shards of complete
+  HypergraphEmbedding messages (hypergraph.proto:26-35, runner.py:363-364):
+  every shard parses with HypergraphEmbedding.ParseFromString with the same
+  dim and method_name, each id is in exactly one shard, and both the native
+  merge and the shards' rows equal the tables at 10k sampled ids."""
+  import os
+  import shutil
+  from hypergraphembedding_amd.proto import HypergraphEmbedding
+  from hypergraphembedding_amd.proto_native import (read_embedding,
+                                                    write_embedding)
+  if shutil.disk_usage(str(tmp_path)).free < 60 * 2**30:
+    pytest.skip("needs ~20 GB of free disk for the shards")
+  from hypergraphembedding_amd import _hgx
+  if "hobe" not in _cache:
+    _sample(ctx, g)
+    ctx.model_init(D, g.N + 1, g.E + 1, seed=3)
+    ctx.train(batch=256, max_epochs=1, loss=_hgx.LOSS_MSE, act=_hgx.ACT_RELU,
+              min_delta=-1e30, shuffle_seed=11)
+    _cache["hobe"] = ctx.model_get()
+  nt, et = _cache["hobe"]
+  path = str(tmp_path / "c4_hobe.pb")
+  files = write_embedding(path, g, nt[1:], et[1:], "HG2V_ALG_DIST")
+  assert len(files) >= 9 and all(os.path.getsize(f) < 2**31 for f in files)
+  rs = np.random.RandomState(8)
+  sel_n = np.sort(rs.choice(g.N, 10_000, replace=False))
+  sel_e = np.sort(rs.choice(g.E, 10_000, replace=False))
+  back = read_embedding(path)  # native, all shards merged
+  assert back.dim == D and back.method_name == "HG2V_ALG_DIST"
+  assert np.array_equal(back.node_ids, g.node_ids)
+  assert np.array_equal(back.node_tab[sel_n], nt[1:][sel_n])
+  assert np.array_equal(back.edge_tab[sel_e], et[1:][sel_e])
+  del back
+  want_n = dict(zip(g.node_ids[sel_n].tolist(), sel_n.tolist()))
+  want_e = dict(zip(g.edge_ids[sel_e].tolist(), sel_e.tolist()))
+  n_node = n_edge = 0
+  for f in files:
+    m = HypergraphEmbedding()
+    with open(f, "rb") as fh:
+      m.ParseFromString(fh.read())
+    assert m.dim == D and m.method_name == "HG2V_ALG_DIST"
+    n_node += len(m.node)
+    n_edge += len(m.edge)
+    for k, r in want_n.items():
+      if k in m.node:
+        assert np.array_equal(np.array(m.node[k].values, np.float32), nt[1 + r])
+    for k, r in want_e.items():
+      if k in m.edge:
+        assert np.array_equal(np.array(m.edge[k].values, np.float32), et[1 + r])
+    del m
+    os.remove(f)
+  assert (n_node, n_edge) == (g.N, g.E)  # every id in exactly one shard
+
+
 def test_c5_combiner_full_size_tables(ctx, g):
   """N_E_SUPERVISED on [FOBE | HOBE] d=256 tables of every node and edge of
   the 10M/5M graph (one epoch of each embedder on the 0.5% row quota)."""

@@ -170,3 +170,47 @@ def test_weighted_jaccard_samples_api():
     p = [x for x in (r.node_node_prob, r.edge_edge_prob, r.node_edge_prob)
          if x is not None]
     assert len(p) == 1 and 0.0 <= p[0] <= 1.0
+
+
+def test_embed_beyond_proto_limit_returns_shards(tmp_path):
+  """EmbedHg2vAlgDist on an Incidence whose embedding message exceeds
+  protobuf's 2 GiB limit (1.1M rows x 512 floats, ~2.8 GB): the embedder
+  returns a ShardedEmbedding with the message surface, written as shards
+  that each parse as a HypergraphEmbedding; rows equal the trained tables
+  (proto_native.read_embedding, native and per-shard protobuf)."""
+  import os
+  from hypergraphembedding_amd.embedding import EmbedHg2vAlgDist
+  from hypergraphembedding_amd.proto import HypergraphEmbedding
+  from hypergraphembedding_amd.proto_native import (PROTO_LIMIT,
+                                                    ShardedEmbedding,
+                                                    read_embedding)
+  from hypergraphembedding_amd.synthetic import random_hypergraph
+  inc = random_hypergraph(N=1_000_000, E=100_000, seed=3)
+  np.random.seed(0)
+  emb = EmbedHg2vAlgDist(inc, 512, num_samples=2, epochs=1)
+  assert isinstance(emb, ShardedEmbedding) and emb.ByteSize() > PROTO_LIMIT
+  assert emb.dim == 512 and emb.method_name == "HG2V_ALG_DIST"
+  assert len(emb.node) == inc.N and len(emb.edge) == inc.E
+  assert np.isfinite(emb.node_tab).all() and np.abs(emb.node_tab).max() > 0
+  files = emb.write(str(tmp_path / "big.pb"))
+  assert len(files) == 2
+  rs = np.random.RandomState(1)
+  sel = rs.choice(inc.N, 2000, replace=False)
+  total = 0
+  for f in files:
+    m = HypergraphEmbedding()
+    with open(f, "rb") as fh:
+      m.ParseFromString(fh.read())
+    assert m.dim == 512 and m.method_name == "HG2V_ALG_DIST"
+    total += len(m.node) + len(m.edge)
+    for r in sel:
+      k = int(inc.node_ids[r])
+      if k in m.node:
+        assert np.array_equal(np.array(m.node[k].values, np.float32),
+                              emb.node_tab[r])
+  assert total == inc.N + inc.E
+  back = read_embedding(str(tmp_path / "big.pb"))
+  assert np.array_equal(back.node_tab, emb.node_tab)  # ids ascending = rows
+  assert np.array_equal(back.edge_tab, emb.edge_tab)
+  for f in files:
+    os.remove(f)

@@ -113,8 +113,7 @@ def test_write_embedding_matches_protobuf(tmp_path):
   got.ParseFromString(embedding_bytes(inc, x, y, "HG2V_ALG_DIST").tobytes())
   assert got == want
   p = tmp_path / "e.pb"
-  n = write_embedding(str(p), inc, x, y, "X")
-  assert p.stat().st_size == n
+  assert write_embedding(str(p), inc, x, y, "X") == [str(p)]  # one message
   back = HypergraphEmbedding()
   back.ParseFromString(p.read_bytes())
   assert back.method_name == "X" and back.dim == d
@@ -148,3 +147,117 @@ def test_write_hypergraph_roundtrip():
   _same_incidence(read_incidence(buf), Incidence.from_hypergraph(hg))
   got = read_incidence(buf)
   assert np.array_equal(got.col_n, inc.col_n) and np.array_equal(got.node_ids, inc.node_ids)
+
+
+def _emb_case(n_nodes, n_edges, d, seed):
+  rs = np.random.RandomState(seed)
+  # distinct ids over the int32 range (randint, not choice: a legacy
+  # choice without replacement permutes the whole range)
+  nid = rs.permutation(np.unique(rs.randint(-2**31, 2**31 - 1, 3 * n_nodes,
+                                            dtype=np.int64)))[:n_nodes]
+  eid = rs.permutation(np.unique(rs.randint(0, 10**9, 3 * n_edges,
+                                            dtype=np.int64)))[:n_edges]
+  return (nid, rs.standard_normal((n_nodes, d)).astype(np.float32),
+          eid, rs.standard_normal((n_edges, d)).astype(np.float32))
+
+
+def test_embedding_shards_each_parse_and_merge(tmp_path):
+  """Shards of complete messages under the size cap (here 64 KB, 2 GiB in
+  use): every shard parses with protobuf with the same dim / method_name,
+  the shards hold every id once, both readers merge them back to the
+  tables, and the concatenated shards are the one message's encoding."""
+  from hypergraphembedding_amd.proto_native import (ShardedEmbedding,
+                                                    read_embedding,
+                                                    message_bytes)
+  nid, nt, eid, et = _emb_case(700, 300, 24, 0)
+  emb = ShardedEmbedding(nid, nt, eid, et, 24, "HG2V_ALG_DIST",
+                         shard_bytes=64 * 1024)
+  files = emb.write(str(tmp_path / "emb.pb"))
+  assert len(files) == -(-message_bytes(nid, eid, 24, "HG2V_ALG_DIST") //
+                         (64 * 1024 - 64)) or len(files) > 1
+  seen_n, seen_e = [], []
+  for f in files:
+    assert os.path.getsize(f) <= 64 * 1024
+    m = HypergraphEmbedding()
+    m.ParseFromString(open(f, "rb").read())
+    assert m.dim == 24 and m.method_name == "HG2V_ALG_DIST"
+    seen_n += list(m.node.keys())
+    seen_e += list(m.edge.keys())
+  assert sorted(seen_n) == sorted(nid.tolist())
+  assert sorted(seen_e) == sorted(eid.tolist())
+  for native in (True, False):
+    back = read_embedding(str(tmp_path / "emb.pb"), native=native)
+    assert back.dim == 24 and back.method_name == "HG2V_ALG_DIST"
+    o = np.argsort(nid)
+    assert np.array_equal(back.node_ids, nid[o])
+    assert np.array_equal(back.node_tab, nt[o])
+    o = np.argsort(eid)
+    assert np.array_equal(back.edge_ids, eid[o])
+    assert np.array_equal(back.edge_tab, et[o])
+  whole = HypergraphEmbedding()
+  whole.ParseFromString(emb.SerializeToString())
+  assert len(whole.node) == 700 and len(whole.edge) == 300
+  k = int(nid[5])
+  assert np.array_equal(np.array(whole.node[k].values, np.float32), nt[5])
+  assert list(emb.node[k].values) == nt[5].tolist() and len(emb.edge) == 300
+
+
+def test_native_embedding_reader_packed_and_last_key_wins():
+  from google.protobuf.internal import encoder
+  import struct
+  from hypergraphembedding_amd import _hgx
+
+  def ld(field, payload):
+    return (encoder._VarintBytes(field << 3 | 2) +
+            encoder._VarintBytes(len(payload)) + payload)
+
+  def entry(field, key, vals, packed):
+    if packed:
+      emb = ld(1, b"".join(struct.pack("<f", v) for v in vals))
+    else:
+      emb = b"".join(b"\x0d" + struct.pack("<f", v) for v in vals)
+    return ld(field, b"\x08" + encoder._VarintBytes(key & (2**64 - 1)) +
+              ld(2, emb))
+  buf = (entry(1, 5, [1, 2], True) + entry(2, -3, [3, 4], False) +
+         b"\x18\x02" + ld(4, b"A") + entry(1, 5, [7, 8], False) +
+         entry(1, -9, [5, 6], True) + ld(4, b"BB"))
+  want = HypergraphEmbedding()
+  want.ParseFromString(buf)
+  got = _hgx.parse_embedding(buf)
+  assert got["method_name"] == want.method_name == "BB" and got["dim"] == 2
+  assert got["node_ids"].tolist() == sorted(want.node.keys()) == [-9, 5]
+  assert got["node_tab"].tolist() == [list(want.node[-9].values),
+                                      list(want.node[5].values)] == [[5, 6], [7, 8]]
+  assert got["edge_ids"].tolist() == [-3] and got["edge_tab"].tolist() == [[3, 4]]
+  with pytest.raises(AssertionError):  # entries of different widths
+    _hgx.parse_embedding(entry(1, 1, [1], True) + entry(1, 2, [1, 2], True))
+  with pytest.raises(AssertionError):
+    _hgx.parse_embedding(b"\x0a\xff\xff")
+
+
+def test_oversize_embedding_returns_shards(monkeypatch):
+  """coords_to_embedding past the message limit returns a ShardedEmbedding
+  with the message surface (limit lowered here; 2 GiB in use)."""
+  from hypergraphembedding_amd import algebraic_distance as ad
+  from hypergraphembedding_amd import proto_native as pn
+  hg = CreateRandomHyperGraph(60, 30, 0.3)
+  inc = Incidence.from_hypergraph(hg)
+  rs = np.random.RandomState(1)
+  x = rs.standard_normal((inc.N, 8)).astype(np.float32)
+  y = rs.standard_normal((inc.E, 8)).astype(np.float32)
+  small = ad.coords_to_embedding(inc, x, y, 8, "M")
+  assert isinstance(small, HypergraphEmbedding)
+  monkeypatch.setattr(pn, "PROTO_LIMIT", 512)
+  monkeypatch.setattr(pn, "SHARD_BYTES", 400)
+  big = ad.coords_to_embedding(inc, x, y, 8, "M")
+  assert isinstance(big, pn.ShardedEmbedding)
+  assert big.shard_bytes == 400
+  assert len(big.node) == len(small.node) and set(big.node) == set(small.node)
+  for k in small.node:
+    assert list(big.node[k].values) == list(small.node[k].values)
+  msgs = list(big.shards())
+  assert len(msgs) > 1
+  merged = HypergraphEmbedding()
+  for m in msgs:
+    merged.MergeFrom(m)
+  assert merged == small
