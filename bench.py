@@ -38,6 +38,11 @@ import os
 import sys
 import time
 
+# CPU-baseline legs: OpenMP threads pinned to cores (set before any OpenMP
+# runtime loads), so the box-to-box spread of the CPU numbers is the CPUs'
+os.environ.setdefault("OMP_PROC_BIND", "close")
+os.environ.setdefault("OMP_PLACES", "cores")
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -69,6 +74,10 @@ def parse():
                  help="skip the power-law 10M/5M measurements")
   p.add_argument("--no-extra", action="store_true",
                  help="skip the C2 FOBE and end-to-end measurements")
+  p.add_argument("--c4-chunks", type=int, default=2,
+                 help="--gpus > 1: row-range chunks of the C4 HOBE stream")
+  p.add_argument("--c4-cpu-records", type=int, default=10_000_000,
+                 help="records of the C4 CPU trainer-port slice")
   p.add_argument("--c4-frac", type=float, default=0.02,
                  help="fraction of C4 rows sampled for the HOBE d=256 line")
   p.add_argument("--dist-backend", default="nccl",
@@ -81,6 +90,27 @@ def parse():
 
 def cpu_threads():
   return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def cpu_model():
+  try:
+    with open("/proc/cpuinfo") as f:
+      for line in f:
+        if line.startswith("model name"):
+          return line.split(":", 1)[1].strip()
+  except OSError:
+    pass
+  return "unknown"
+
+
+def timed_runs(fn, reps):
+  """[seconds] of `reps` calls of fn()."""
+  out = []
+  for _ in range(reps):
+    t = time.perf_counter()
+    fn()
+    out.append(time.perf_counter() - t)
+  return out
 
 
 def main():
@@ -240,24 +270,50 @@ def main():
     init = np.random.RandomState(1)
     nt = init.uniform(-0.05, 0.05, (inc.N + 1, args.dim)).astype(np.float32)
     et = init.uniform(-0.05, 0.05, (inc.E + 1, args.dim)).astype(np.float32)
-    t = time.perf_counter()
-    O.train_mt(cidx, ctgt, args.num_neighbors, nt, et, O.LOSS_MSE, O.ACT_RELU,
-               batch=args.batch, epochs=1, threads=threads)
-    cpu_s = time.perf_counter() - t
+    # three runs of the same slice (fresh tables each): median and spread
+    runs = timed_runs(lambda: O.train_mt(cidx, ctgt, args.num_neighbors, nt, et,
+                                         O.LOSS_MSE, O.ACT_RELU,
+                                         batch=args.batch, epochs=1,
+                                         threads=threads), 3)
+    cpu_s = float(np.median(runs))
     m1 = min(m, 500_000)
     t = time.perf_counter()
     O.train(cidx[:m1], ctgt[:m1], args.num_neighbors, nt, et, O.LOSS_MSE,
             O.ACT_RELU, batch=args.batch, max_epochs=1, min_delta=-1e30)
     cpu1_s = time.perf_counter() - t
     cpu = {"value": round(m / cpu_s, 1), "unit": "records/s", "cores": threads,
-           "kind": "port",
+           "kind": "port", "cpu_model": cpu_model(),
+           "omp": {"OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"),
+                   "OMP_PLACES": os.environ.get("OMP_PLACES")},
            "sample": f"{m} HOBE records (random slice of this run's stream), "
                      f"1 epoch, d={args.dim}, batch {args.batch}, "
                      f"oracle/cpu_train_mt.c on {threads} OpenMP threads, "
-                     f"{cpu_s:.1f} s",
+                     f"median of 3 runs ({cpu_s:.1f} s)",
+           "runs_records_per_s": [round(m / r, 1) for r in runs],
            "single_thread_value": round(m1 / cpu1_s, 1),
            "single_thread_sample": f"first {m1} of those records, "
                                    f"oracle/hgref.c hgref_train, {cpu1_s:.1f} s"}
+    # HOBE sampling on the CPU: the same algorithm (exact per-row expansion,
+    # uniform distinct draws, the reference's probabilities) on a seeded 10%
+    # of C3's node rows and edge rows, OpenMP over rows, on this run's
+    # coordinates (oracle/cpu_sample_mt.c)
+    ax, ay = ctx.alg_get()
+    rsq = np.random.RandomState(5)
+    nq = np.where(rsq.random_sample(inc.N) < 0.1, args.num_samples, 0).astype(np.int32)
+    eq = np.where(rsq.random_sample(inc.E) < 0.1, args.num_samples, 0).astype(np.int32)
+    t = time.perf_counter()
+    sidx, _, _ = O.cpu_hobe_sample_mt(inc, ax, ay, nq, eq, args.num_neighbors,
+                                      seed=1, threads=threads)
+    cs_s = time.perf_counter() - t
+    n_cs = int(sidx.shape[0])
+    del sidx
+    cpu["hobe_sampling"] = {
+        "value": round(n_cs / cs_s, 1), "unit": "records/s", "cores": threads,
+        "kind": "port",
+        "sample": f"AlgebraicDistanceSamples on a seeded 10% of C3's node and "
+                  f"edge rows (S={args.num_samples}, K={args.num_neighbors}): "
+                  f"{n_cs} records in {cs_s:.1f} s, oracle/cpu_sample_mt.c",
+        "gpu_records_per_s": round(n / sample_s, 1) if sample_s > 0 else None}
 
   # ---- C2: FOBE d=128 on the same graph (BASELINE configs[1]) ----
   c2 = e2e = None
@@ -411,31 +467,59 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
   rsq = np.random.RandomState(2)
   nq4 = np.where(rsq.random_sample(big.N) < args.c4_frac, S4, 0).astype(np.int32)
   eq4 = np.where(rsq.random_sample(big.E) < args.c4_frac, S4, 0).astype(np.int32)
-  sync()
-  t = time.perf_counter()
-  if world > 1:
-    from hypergraphembedding_amd.hg2v_sample import sample_sharded
-    n4, _ = sample_sharded(big, K4, S4, ctx=ctx, seed=4000, kind="hobe",
-                           node_quota=nq4, edge_quota=eq4,
-                           device=None if args.dist_backend == "nccl" else "cpu")
-  else:
-    n4 = ctx.sample_hobe(4000, K4, S4, node_q=nq4, edge_q=eq4)
-  sync()
-  hobe_sample_s = max_over_ranks(time.perf_counter() - t)
-  rej_rows, fb_rows = ctx.sample_stats()
   ctx.model_init(d4, big.N + 1, big.E + 1, seed=11 + rank)
-  sync()
-  t = time.perf_counter()
-  ctx.train(batch=args.batch, max_epochs=1, loss=_hgx.LOSS_MSE,
-            act=_hgx.ACT_RELU, min_delta=-1e30, shuffle_seed=2)
-  sync()
-  t4 = time.perf_counter() - t
-  ms4t, rec4, bat4 = ctx.train_stats()
-  fz4, sp4 = ctx.train_path_stats()
+  if world > 1:
+    # row-range chunks, each sampled row-sharded over the ranks and
+    # all-gathered (hg2v_sample.sharded_chunk_fn): a replica holds one
+    # chunk's stream at a time, the form the full 5.9e9-record epoch takes
+    from hypergraphembedding_amd.embedding import _row_chunks
+    from hypergraphembedding_amd.hg2v_sample import sharded_chunk_fn
+    bound = 2 * S4
+    chunks = _row_chunks(big, bound, -(-bound * (big.N + big.E) // args.c4_chunks))
+    fn = sharded_chunk_fn(big, K4, S4, chunks, ctx=ctx, seed=4000, kind="hobe",
+                          node_quota=nq4, edge_quota=eq4,
+                          device=None if args.dist_backend == "nccl" else "cpu")
+    n4 = 0
+    hobe_sample_s = t4 = 0.0
+    ms4t = 0.0
+    rec4 = bat4 = fz4 = sp4 = 0
+    for c in range(len(chunks)):
+      sync()
+      t = time.perf_counter()
+      n4 += fn(c)
+      sync()
+      hobe_sample_s += max_over_ranks(time.perf_counter() - t)
+      t = time.perf_counter()
+      ctx.train(batch=args.batch, max_epochs=1, loss=_hgx.LOSS_MSE,
+                act=_hgx.ACT_RELU, min_delta=-1e30, shuffle_seed=2 + c)
+      sync()
+      t4 += time.perf_counter() - t
+      ms_c, rec_c, bat_c = ctx.train_stats()
+      fz_c, sp_c = ctx.train_path_stats()
+      ms4t, rec4, bat4 = ms4t + ms_c, rec4 + rec_c, bat4 + bat_c
+      fz4, sp4 = fz4 + fz_c, sp4 + sp_c
+    rej_rows, fb_rows = ctx.sample_stats()  # of the last chunk
+  else:
+    sync()
+    t = time.perf_counter()
+    n4 = ctx.sample_hobe(4000, K4, S4, node_q=nq4, edge_q=eq4)
+    sync()
+    hobe_sample_s = time.perf_counter() - t
+    rej_rows, fb_rows = ctx.sample_stats()
+    sync()
+    t = time.perf_counter()
+    ctx.train(batch=args.batch, max_epochs=1, loss=_hgx.LOSS_MSE,
+              act=_hgx.ACT_RELU, min_delta=-1e30, shuffle_seed=2)
+    sync()
+    t4 = time.perf_counter() - t
+    ms4t, rec4, bat4 = ctx.train_stats()
+    fz4, sp4 = ctx.train_path_stats()
   hobe4 = {"workload": "HG2V_ALG_DIST (HOBE) dim=256 on the 10M/5M power-law "
                        f"graph, rows sampled: a seeded {args.c4_frac:.0%} of "
                        "node rows and edge rows (quota S=200, K=5), 1 epoch",
            "records": n4,
+           "chunks": (f"{args.c4_chunks} row-range chunks, row-sharded sampling "
+                      "+ all-gather per chunk" if world > 1 else "one stream"),
            "rows_sampled": int((nq4 > 0).sum() + (eq4 > 0).sum()),
            "rejection_rows": rej_rows, "expansion_fallback_rows": fb_rows,
            "uniform_column_rows": ctx.sample_uniform_rows(),
@@ -447,13 +531,13 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
            "multi_pending_batches": ctx.train_multi_pending(),
            "loss": "MSE", "act": "relu"}
   if rank == 0 and world == 1 and not args.no_cpu:
-    # CPU port on 1M records of the same stream, tables of the same size
-    # (10M+1 and 5M+1 rows x 256; only the rows the slice touches are
-    # initialised, the rest stays untouched memory)
+    # CPU port on 1e7 records of the same stream (BASELINE.md's planned
+    # slice), tables of the same size (10M+1 and 5M+1 rows x 256; only the
+    # rows the slice touches are initialised, the rest stays untouched)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     idx4, tgt4 = ctx.records_get()
-    m4 = min(1_000_000, n4)
+    m4 = min(args.c4_cpu_records, n4)
     sel = np.random.RandomState(3).permutation(n4)[:m4]
     ci, ct = idx4[sel].copy(), tgt4[sel].copy()
     del idx4, tgt4
@@ -479,7 +563,22 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
                                 f"threads, {cpu4_s:.1f} s")
     hobe4["vs_cpu_port"] = round(hobe4["train_records_per_s"] /
                                  hobe4["cpu_port_records_per_s"], 1)
-    del nt4, et4
+    del nt4, et4, ci, ct
+    # alg-dist on the CPU: the reference's float64 relaxation restated
+    # (oracle/hgref.c hgref_algdist, OpenMP over rows), 3 iterations of the
+    # whole 10M/5M graph from the same init
+    t = time.perf_counter()
+    O.algdist(big, bx0, by0, 3)
+    ca_s = time.perf_counter() - t
+    c4["cpu_algdist"] = {
+        "ms_per_iter": round(ca_s / 3 * 1e3, 1),
+        "gbps": round(b_iter4 * 3 / ca_s / 1e9, 2),
+        "cores": threads, "kind": "port", "dtype": "f64",
+        "sample": "3 iterations on the whole power-law 10M/5M graph, "
+                  "oracle/hgref.c hgref_algdist (float64 like the reference, "
+                  f"OpenMP over rows), {ca_s:.1f} s; gbps in the fp32 "
+                  "algorithmic bytes of the GPU line",
+        "vs_gpu": round((ca_s / 3 * 1e3) / (ms4 / args.alg_iters), 1)}
   c4["hobe_d256"] = hobe4
   return c4
 

@@ -369,3 +369,40 @@ def mlp_predict(kind, in_dim, out_dim, weights, node_tab, edge_tab, output,
                             None if nr is None else nr.ctypes.data,
                             None if er is None else er.ctypes.data, out)
   return out if output == 0 else out.reshape(n, out_dim)
+
+
+_smp = None
+
+
+def cpu_hobe_sample_mt(inc, alg_node, alg_edge, node_q, edge_q, K, seed=0,
+                       threads=0):
+  """Multi-threaded CPU HOBE sampler (cpu_sample_mt.c; bench baseline, exact
+  expansion per row). Returns (idx, tgt, block bounds[5])."""
+  global _smp
+  if _smp is None:
+    path = os.path.join(_HERE, "libcpusample.so")
+    src = os.path.join(_HERE, "cpu_sample_mt.c")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+      subprocess.run(["make", "-C", _HERE, "-s", "libcpusample.so"], check=True)
+    _smp = ctypes.CDLL(path)
+    _smp.cpu_hobe_sample_mt.restype = _i64
+    _smp.cpu_hobe_sample_mt.argtypes = [ctypes.c_int32, ctypes.c_int32, _i32p,
+                                        _i32p, _i32p, _i32p, _f32p, _f32p, _int,
+                                        _i32p, _i32p, _int, ctypes.c_uint64,
+                                        _int, _i32p, _f32p, _i64p]
+  nq = np.ascontiguousarray(node_q, np.int32)
+  eq = np.ascontiguousarray(edge_q, np.int32)
+  an = np.ascontiguousarray(alg_node, np.float32)
+  ae = np.ascontiguousarray(alg_edge, np.float32)
+  cap = 2 * (int(nq.sum()) + int(eq.sum())) + 1
+  idx = np.empty((cap, 4 + 2 * K), np.int32)
+  tgt = np.empty((cap, 3), np.float32)
+  b = np.zeros(5, np.int64)
+  n = _smp.cpu_hobe_sample_mt(inc.N, inc.E, np.ascontiguousarray(inc.rp_n, np.int32),
+                              np.ascontiguousarray(inc.col_n, np.int32),
+                              np.ascontiguousarray(inc.rp_e, np.int32),
+                              np.ascontiguousarray(inc.col_e, np.int32), an, ae,
+                              an.shape[1], nq, eq, K, seed & (2**64 - 1),
+                              threads, idx, tgt, b)
+  assert n >= 0
+  return idx[:n], tgt[:n], b

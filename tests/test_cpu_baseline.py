@@ -31,3 +31,43 @@ def test_train_mt_matches_oracle():
                                threads=4)
     assert np.abs(a_nt - b_nt).max() < 1e-5
     assert np.abs(a_et - b_et).max() < 1e-5
+
+
+def test_cpu_hobe_sampler_baseline_computes_the_reference_quantities(small_inc):
+  """The timed CPU sampler baseline (oracle/cpu_sample_mt.c) samples what
+  AlgebraicDistanceSamples samples: per row min(S, |pattern row|) distinct
+  valid columns in the four kind blocks, probabilities equal to the oracle's
+  (bit-exact, same float formula), neighbours from the right rows."""
+  inc, S, K = small_inc, 6, 3
+  r = O.Rng(3)
+  ax, ay = O.algdist(inc, r.random((inc.N, 10)), r.random((inc.E, 10)), 5)
+  ax, ay = ax.astype(np.float32), ay.astype(np.float32)
+  nq = np.full(inc.N, S, np.int32)
+  eq = np.full(inc.E, S, np.int32)
+  nq[::3] = 0
+  idx, tgt, b = O.cpu_hobe_sample_mt(inc, ax, ay, nq, eq, K, seed=5, threads=2)
+  A = np.zeros((inc.N, inc.E), int)
+  A[np.repeat(np.arange(inc.N), np.diff(inc.rp_n)), inc.col_n] = 1
+  pats = [A @ A.T > 0, A.T @ A > 0, A @ A.T @ A > 0, A.T @ A @ A.T > 0]
+  cols = [(0, 2), (1, 3), (0, 3), (3, 0)]
+  for blk in range(4):
+    rec = idx[b[blk]:b[blk + 1]]
+    q = nq if blk in (0, 2) else eq
+    rc, cc = cols[blk]
+    rows, cnt = np.unique(rec[:, rc] - 1, return_counts=True)
+    want = np.minimum(q, pats[blk].sum(1))
+    assert np.array_equal(np.bincount(rows, cnt, minlength=q.size), want)
+    assert pats[blk][rec[:, rc] - 1, rec[:, cc] - 1].all()
+  nn = slice(b[0], b[1])
+  ee = slice(b[1], b[2])
+  ne = slice(b[2], b[4])
+  assert np.array_equal(tgt[nn, 0], O.hobe_probs(O.HOBE_NN, idx[nn, 0] - 1,
+                                                 idx[nn, 2] - 1, inc, ax, ay))
+  assert np.array_equal(tgt[ee, 1], O.hobe_probs(O.HOBE_EE, idx[ee, 1] - 1,
+                                                 idx[ee, 3] - 1, inc, ax, ay))
+  assert np.array_equal(tgt[ne, 2], O.hobe_probs(O.HOBE_NE, idx[ne, 0] - 1,
+                                                 idx[ne, 3] - 1, inc, ax, ay))
+  for i in range(int(b[2]), int(b[4])):
+    v, e = idx[i, 0] - 1, idx[i, 3] - 1
+    assert np.isin(idx[i, 4:4 + K] - 1, inc.col_e[inc.rp_e[e]:inc.rp_e[e + 1]]).all()
+    assert np.isin(idx[i, 4 + K:] - 1, inc.col_n[inc.rp_n[v]:inc.rp_n[v + 1]]).all()

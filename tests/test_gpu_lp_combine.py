@@ -151,25 +151,28 @@ def test_link_prediction_quality_gpu_vs_cpu_oracle(tiny_hypergraph):
   """snap_youtube_tiny: remove 10% of the connections, embed the rest with
   FOBE d=16 on the GPU and with the CPU oracle, and score both with the
   LP_NODE_EDGE_CLASSIFIER experiment against as many missing links. The RNG
-  streams differ, so the bar is statistical: both well above chance, and
-  the GPU embedding no worse than the oracle's by more than 0.05."""
+  streams differ, so the bar is statistical: every run well above chance,
+  and the GPU embeddings' mean accuracy over three seeds no worse than the
+  oracle's mean by more than 0.04 (one run's accuracy on 238 test pairs has
+  a standard deviation of ~0.02)."""
   random.seed(11)
   np.random.seed(11)
   hg = tiny_hypergraph
   sub, removed = RemoveRandomConnections(hg, 0.1)
   assert len(removed) > 100
   bad = SampleMissingConnections(hg, len(removed))
-  gpu_emb = EmbedHg2vBoolean(sub, 16)
-  cpu_emb = _oracle_fobe_embedding(sub, 16, 11)
-  res = {}
-  for name, emb in (("gpu", gpu_emb), ("cpu_oracle", cpu_emb)):
-    np.random.seed(5)
-    random.seed(5)
-    m = RunLinkPredictionExperiment(
-        LinkPredictionData(sub, emb, removed, bad, 0.1),
-        "LP_NODE_EDGE_CLASSIFIER")
-    res[name] = m
-  print({k: (round(v.accuracy, 3), round(v.f1, 3)) for k, v in res.items()})
-  for m in res.values():
-    assert m.accuracy > 0.6
-  assert res["gpu"].accuracy >= res["cpu_oracle"].accuracy - 0.05
+  res = {"gpu": [], "cpu_oracle": []}
+  for seed in (11, 12, 13):
+    np.random.seed(seed)
+    embs = (("gpu", EmbedHg2vBoolean(sub, 16)),
+            ("cpu_oracle", _oracle_fobe_embedding(sub, 16, seed)))
+    for name, emb in embs:
+      np.random.seed(5)
+      random.seed(5)
+      m = RunLinkPredictionExperiment(
+          LinkPredictionData(sub, emb, removed, bad, 0.1),
+          "LP_NODE_EDGE_CLASSIFIER")
+      assert m.accuracy > 0.6
+      res[name].append(m.accuracy)
+  print({k: np.round(v, 3).tolist() for k, v in res.items()})
+  assert np.mean(res["gpu"]) >= np.mean(res["cpu_oracle"]) - 0.04
