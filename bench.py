@@ -88,8 +88,22 @@ def parse():
   return p.parse_args()
 
 
+# the process's CPU share, read before any OpenMP runtime binds this thread:
+# with OMP_PROC_BIND the runtime pins the calling (main) thread to its first
+# place, which would shrink sched_getaffinity for everything after
+_AFFINITY = frozenset(os.sched_getaffinity(0))
+
+
 def cpu_threads():
-  return max(1, min(16, len(os.sched_getaffinity(0))))
+  return max(1, min(16, len(_AFFINITY)))
+
+
+def restore_affinity():
+  """Give the main thread its whole CPU share back after an OpenMP leg."""
+  try:
+    os.sched_setaffinity(0, _AFFINITY)
+  except OSError:
+    pass
 
 
 def cpu_model():
@@ -281,6 +295,7 @@ def main():
     O.train(cidx[:m1], ctgt[:m1], args.num_neighbors, nt, et, O.LOSS_MSE,
             O.ACT_RELU, batch=args.batch, max_epochs=1, min_delta=-1e30)
     cpu1_s = time.perf_counter() - t
+    restore_affinity()
     cpu = {"value": round(m / cpu_s, 1), "unit": "records/s", "cores": threads,
            "kind": "port", "cpu_model": cpu_model(),
            "omp": {"OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"),
@@ -305,6 +320,7 @@ def main():
     sidx, _, _ = O.cpu_hobe_sample_mt(inc, ax, ay, nq, eq, args.num_neighbors,
                                       seed=1, threads=threads)
     cs_s = time.perf_counter() - t
+    restore_affinity()
     n_cs = int(sidx.shape[0])
     del sidx
     cpu["hobe_sampling"] = {
@@ -555,6 +571,7 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
     O.train_mt(ci, ct, K4, nt4, et4, O.LOSS_MSE, O.ACT_RELU, batch=args.batch,
                epochs=1, threads=threads, copy=False)
     cpu4_s = time.perf_counter() - t
+    restore_affinity()
     hobe4["cpu_port_records_per_s"] = round(m4 / cpu4_s, 1)
     hobe4["cpu_port_cores"] = threads
     hobe4["cpu_port_sample"] = (f"{m4} random records of this stream, d={d4}, "
@@ -570,6 +587,7 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
     t = time.perf_counter()
     O.algdist(big, bx0, by0, 3)
     ca_s = time.perf_counter() - t
+    restore_affinity()
     c4["cpu_algdist"] = {
         "ms_per_iter": round(ca_s / 3 * 1e3, 1),
         "gbps": round(b_iter4 * 3 / ca_s / 1e9, 2),

@@ -30,6 +30,8 @@
 #include <cstring>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "hgx_internal.h"
 
 using hgx::f2ord;
@@ -315,13 +317,25 @@ __device__ __forceinline__ float4 nt_load4(const float4 *p) {
   return make_float4(v.x, v.y, v.z, v.w);
 }
 
-template <int KS, int G, int MODE, int M>
+// Push form of the edge half (tuning alg_push, single GPU): the node half
+// (PM_PUSH) also writes every incidence's contribution row [w_v, w_v * x_v]
+// (w_v = 1/deg v, x_v its NEW raw coords: what the edge half would gather)
+// to contrib[tpos[t]], tpos = the incidence's position in the edge-major
+// CSR; the edge half (PM_STREAM) then reads its rows' contributions
+// sequentially in CSR order instead of gathering node rows (the gathers of
+// the 480 MB node table hit L2 2.6% of the time at C4). Scattered stores do
+// not stall the wave; the stream is coalesced.
+enum { PM_GATHER = 0, PM_STREAM = 1, PM_PUSH = 2 };
+
+template <int KS, int G, int MODE, int M, int PM = PM_GATHER>
 __global__ __launch_bounds__(kBlock) void algdist_half_quad(
     int row0, int R, const int *__restrict__ rp, const int *__restrict__ col,
     const float *__restrict__ self_in, const float *__restrict__ src,
     float *__restrict__ out, const int *__restrict__ mm_prev, int src_affine,
-    int *__restrict__ mm_cur, int k, int long_thresh) {
+    int *__restrict__ mm_cur, int k, int long_thresh,
+    const int *__restrict__ tpos, float *__restrict__ contrib) {
   HGX_FLUSH_SEL(k);
+  static_assert(PM == PM_GATHER || MODE == MODE_FULL, "push / stream: full rows");
   constexpr int NV = KS / 4, Q = G / 4;
   static_assert(NV >= 1 && NV <= 4 && G >= 4, "one float4 per lane");
   __shared__ float s_m[KS], s_d[KS];
@@ -343,7 +357,9 @@ __global__ __launch_bounds__(kBlock) void algdist_half_quad(
     const int beg = rp[r], end = rp[r + 1];
     if (end - beg > long_thresh) continue;  // seg_partial + long_finish
     float4 self = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (MODE == MODE_FULL && qi == 0 && vl)
+    // push: every quad finishes the row (it writes a share of the
+    // contributions); the same self row, from L2
+    if (MODE == MODE_FULL && (qi == 0 || PM == PM_PUSH) && vl)
       self = reinterpret_cast<const float4 *>(self_in)[(size_t)r * NV + p];
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     float wsum = 0.f;
@@ -352,7 +368,8 @@ __global__ __launch_bounds__(kBlock) void algdist_half_quad(
 #pragma unroll
       for (int m = 0; m < M; m++) {
         const int t = base + Q * m;
-        c[m] = t < end ? ((g_ablate & 2) ? -2 : col[t]) : -1;
+        // stream: the source row is the incidence's own contribution row
+        c[m] = t < end ? (PM == PM_STREAM ? t : (g_ablate & 2) ? -2 : col[t]) : -1;
       }
       float4 v[M];
 #pragma unroll
@@ -369,7 +386,14 @@ __global__ __launch_bounds__(kBlock) void algdist_half_quad(
         const float w = hgx::dpp_f<0x00>(v[m].x);  // quad_perm [0,0,0,0]
         if (c[m] >= 0) {
           wsum += w;
-          acc = f4fma(w, v[m], acc);
+          if (PM == PM_STREAM) {  // pre-multiplied [w, w*x]
+            acc.x += v[m].x;
+            acc.y += v[m].y;
+            acc.z += v[m].z;
+            acc.w += v[m].w;
+          } else {
+            acc = f4fma(w, v[m], acc);
+          }
         }
       }
     }
@@ -378,7 +402,7 @@ __global__ __launch_bounds__(kBlock) void algdist_half_quad(
     acc.y = quad_stride_sum<G>(acc.y);
     acc.z = quad_stride_sum<G>(acc.z);
     acc.w = quad_stride_sum<G>(acc.w);
-    if (qi == 0 && vl) {
+    if ((qi == 0 || PM == PM_PUSH) && vl) {
       float4 *op = reinterpret_cast<float4 *>(out) + (size_t)r * NV + p;
       if (MODE == MODE_PARTIAL) {
         if (p == 0) acc.x = wsum;
@@ -404,7 +428,16 @@ __global__ __launch_bounds__(kBlock) void algdist_half_quad(
           }
           f4set(o, c, v);
         }
-        *op = o;
+        if (qi == 0) *op = o;
+        if (PM == PM_PUSH) {
+          // contribution rows [w, w*x_1..k, 0] of this quad's incidences
+          const float w = 1.0f / (float)(end - beg);
+          float4 cv = make_float4(w * o.x, w * o.y, w * o.z, w * o.w);
+          if (p == 0) cv.x = w;
+          float4 *c4 = reinterpret_cast<float4 *>(contrib);
+          for (int t = beg + qi; t < end; t += Q)
+            c4[(size_t)tpos[t] * NV + p] = cv;
+        }
       }
     }
   }
@@ -424,7 +457,9 @@ __global__ __launch_bounds__(kBlock) void algdist_half_quad(
 // (LongRows): part[piece] = [sum w, sum w*src] over the piece, raw sums (the
 // affine of a scaled source commutes with the weighted mean; long_finish
 // applies it).
-template <int KS, int M>
+// PRE (push form): src holds the pre-multiplied contribution rows [w, w*x]
+// in CSR order, read in sequence instead of gathered through col.
+template <int KS, int M, bool PRE = false>
 __global__ __launch_bounds__(kBlock) void algdist_seg_partial(
     int nseg, const int2 *__restrict__ seg, int T, const int *__restrict__ rp,
     const int *__restrict__ col, const float *__restrict__ src,
@@ -446,7 +481,7 @@ __global__ __launch_bounds__(kBlock) void algdist_seg_partial(
 #pragma unroll
       for (int m = 0; m < M; m++) {
         const int t = base + 64 * m;
-        c[m] = t < end ? col[t] : -1;
+        c[m] = t < end ? (PRE ? t : col[t]) : -1;
       }
       float4 v[M][NV];
 #pragma unroll
@@ -461,7 +496,16 @@ __global__ __launch_bounds__(kBlock) void algdist_seg_partial(
           const float w = v[m][0].x;
           wsum += w;
 #pragma unroll
-          for (int j = 0; j < NV; j++) acc[j] = f4fma(w, v[m][j], acc[j]);
+          for (int j = 0; j < NV; j++) {
+            if (PRE) {
+              acc[j].x += v[m][j].x;
+              acc[j].y += v[m][j].y;
+              acc[j].z += v[m][j].z;
+              acc[j].w += v[m][j].w;
+            } else {
+              acc[j] = f4fma(w, v[m][j], acc[j]);
+            }
+          }
         }
     }
     wsum = hgx::group_allreduce_sum<64>(wsum);
@@ -1010,12 +1054,12 @@ using FinFn = void (*)(int, const int *, const int *, const float *,
                        const int *, const float *, float *, const int *, int,
                        int *, int);
 
-template <int MODE>
+template <int MODE, bool PRE = false>
 bool long_fns(int ks, SegFn &seg, FinFn &fin) {
   switch (ks) {
 #define HGX_LCASE(KSV)                                   \
     case KSV:                                            \
-      seg = algdist_seg_partial<KSV, 4>;                 \
+      seg = algdist_seg_partial<KSV, 4, PRE>;            \
       fin = algdist_long_finish<KSV, MODE>;              \
       return true;
     HGX_LCASE(4) HGX_LCASE(8) HGX_LCASE(12) HGX_LCASE(16) HGX_LCASE(20)
@@ -1064,46 +1108,50 @@ HalfFn narrow_for_g(int g) {
                          : narrow_for_gm<KS, MODE, 2>(g);
 }
 
-template <int KS, int MODE, int M>
-HalfFn quad_for_gm(int g) {
+using QuadFn = void (*)(int, int, const int *, const int *, const float *,
+                        const float *, float *, const int *, int, int *, int,
+                        int, const int *, float *);
+
+template <int KS, int MODE, int M, int PM>
+QuadFn quad_for_gm(int g) {
   switch (g) {
-    case 4: return algdist_half_quad<KS, 4, MODE, M>;
-    case 8: return algdist_half_quad<KS, 8, MODE, M>;
-    case 16: return algdist_half_quad<KS, 16, MODE, M>;
-    case 32: return algdist_half_quad<KS, 32, MODE, M>;
-    default: return algdist_half_quad<KS, 64, MODE, M>;
+    case 4: return algdist_half_quad<KS, 4, MODE, M, PM>;
+    case 8: return algdist_half_quad<KS, 8, MODE, M, PM>;
+    case 16: return algdist_half_quad<KS, 16, MODE, M, PM>;
+    case 32: return algdist_half_quad<KS, 32, MODE, M, PM>;
+    default: return algdist_half_quad<KS, 64, MODE, M, PM>;
   }
 }
 
 // HGX_ALG_QM: incidences in flight per quad (2 or 4, default 4)
-template <int KS, int MODE>
-HalfFn quad_for_g(int g) {
+template <int KS, int MODE, int PM>
+QuadFn quad_for_g(int g) {
   static const int m = [] {
     return hgx_debug_env("HGX_ALG_QM", 4);
   }();
-  return m <= 2 ? quad_for_gm<KS, MODE, 2>(g) : quad_for_gm<KS, MODE, 4>(g);
+  return m <= 2 ? quad_for_gm<KS, MODE, 2, PM>(g) : quad_for_gm<KS, MODE, 4, PM>(g);
 }
 
 // quad-split rows (algdist_half_quad) for KS <= 16; HGX_ALG_QUAD=0 selects
 // algdist_half_narrow. G = 4 lanes per quad x Q quads, Q doubling while a
 // quad would stride more than HGX_ALG_QLPI (default 8) incidences.
-template <int MODE>
-HalfFn quad_fn(int ks, double avg, int &g) {
+template <int MODE, int PM = PM_GATHER>
+QuadFn quad_fn(int ks, double avg, int &g) {
   static const int on = [] {
     return hgx_debug_env("HGX_ALG_QUAD", 1);
   }();
   static const int qlpi = [] {
     return std::max(1, hgx_debug_env("HGX_ALG_QLPI", 8));
   }();
-  if (!on || ks > 16) return nullptr;
+  if ((!on && PM == PM_GATHER) || ks > 16) return nullptr;
   int q = 1;
   while (q < 16 && q * qlpi < avg) q *= 2;
   g = 4 * q;
   switch (ks) {
-    case 4: return quad_for_g<4, MODE>(g);
-    case 8: return quad_for_g<8, MODE>(g);
-    case 12: return quad_for_g<12, MODE>(g);
-    case 16: return quad_for_g<16, MODE>(g);
+    case 4: return quad_for_g<4, MODE, PM>(g);
+    case 8: return quad_for_g<8, MODE, PM>(g);
+    case 12: return quad_for_g<12, MODE, PM>(g);
+    case 16: return quad_for_g<16, MODE, PM>(g);
     default: return nullptr;
   }
 }
@@ -1120,13 +1168,50 @@ HalfFn narrow_fn(int ks, int g) {
   }
 }
 
+// pm: PM_GATHER (every sharded / partial sweep), or the single-GPU push
+// form: PM_PUSH for the node half (tpos, contrib written), PM_STREAM for the
+// edge half (src = contrib). Push and stream need KS <= 16 (the quad kernel).
 int launch_half(hgx_ctx *ctx, int mode, int row0, int R, const int *rp,
                 const int *col, const float *self_in, const float *src,
                 float *out, const int *mm_prev, int src_affine, int *mm_cur,
                 double avg, const int *blk, int nblk, LongRows *lr,
-                bool sample_flush = false) {
+                bool sample_flush = false, int pm = PM_GATHER,
+                const int *tpos = nullptr, float *contrib = nullptr) {
   const int k = ctx->k | (sample_flush ? kSampleFlush : 0), KS = ctx->ks;
   if (R <= 0) return HGX_OK;
+  if (pm != PM_GATHER) {
+    HGX_CHECK(ctx, mode == MODE_FULL && KS <= 16, HGX_EUNSUP,
+              "alg-dist push form needs full rows and k <= 15");
+    HGX_CHECK(ctx, pm == PM_STREAM || !lr || lr->nlong == 0, HGX_EUNSUP,
+              "alg-dist push form: node rows longer than the long-row "
+              "threshold are not pushed");
+    int thresh = INT_MAX;
+    if (lr && lr->nlong > 0) {  // stream: long edge rows from contrib
+      SegFn seg = nullptr;
+      FinFn fin = nullptr;
+      long_fns<MODE_FULL, true>(KS, seg, fin);
+      thresh = lr->thresh;
+      HGX_TRY(hgx_ensure(ctx, lr->part, sizeof(float) * (size_t)lr->nseg * KS));
+      hipLaunchKernelGGL(seg, dim3(grid_for(lr->nseg, kBlock / 64, resident_grid(seg))),
+                         dim3(kBlock), 0, ctx->stream, lr->nseg,
+                         lr->seg.as<int2>(), lr->thresh, rp, col, src,
+                         lr->part.as<float>());
+      hipLaunchKernelGGL(fin, dim3(grid_for(lr->nlong, kBlock / 64, resident_grid(fin))),
+                         dim3(kBlock), 0, ctx->stream, lr->nlong,
+                         lr->rows.as<int>(), lr->off.as<int>(),
+                         lr->part.as<float>(), rp, self_in, out, mm_prev,
+                         src_affine, mm_cur, k);
+    }
+    int g = 0;
+    QuadFn fn = pm == PM_PUSH ? quad_fn<MODE_FULL, PM_PUSH>(KS, avg, g)
+                              : quad_fn<MODE_FULL, PM_STREAM>(KS, avg, g);
+    hipLaunchKernelGGL(fn, dim3(grid_for(R, kBlock / g, resident_grid(fn))),
+                       dim3(kBlock), 0, ctx->stream, row0, R, rp, col, self_in,
+                       src, out, mm_prev, src_affine, mm_cur, k, thresh, tpos,
+                       contrib);
+    HGX_LAUNCH_CHECK(ctx);
+    return HGX_OK;
+  }
   static const bool flat_env = [] {
     return hgx_debug_env("HGX_ALG_FLAT", 0) == 1;
   }();
@@ -1157,17 +1242,22 @@ int launch_half(hgx_ctx *ctx, int mode, int row0, int R, const int *rp,
       }
     }
     int g = 0;
-    HalfFn fn = mode == MODE_FULL ? quad_fn<MODE_FULL>(KS, avg, g)
+    QuadFn qf = mode == MODE_FULL ? quad_fn<MODE_FULL>(KS, avg, g)
                                   : quad_fn<MODE_PARTIAL>(KS, avg, g);
-    if (!fn) {
+    if (qf) {
+      hipLaunchKernelGGL(qf, dim3(grid_for(R, kBlock / g, resident_grid(qf))),
+                         dim3(kBlock), 0, ctx->stream, row0, R, rp, col,
+                         self_in, src, out, mm_prev, src_affine, mm_cur, k,
+                         thresh, nullptr, nullptr);
+    } else {
       g = pick_g(avg);
-      fn = mode == MODE_FULL ? narrow_fn<MODE_FULL>(KS, g)
-                             : narrow_fn<MODE_PARTIAL>(KS, g);
+      HalfFn fn = mode == MODE_FULL ? narrow_fn<MODE_FULL>(KS, g)
+                                    : narrow_fn<MODE_PARTIAL>(KS, g);
+      hipLaunchKernelGGL(fn, dim3(grid_for(R, kBlock / g, resident_grid(fn))),
+                         dim3(kBlock), 0,
+                         ctx->stream, row0, R, rp, col, self_in, src, out,
+                         mm_prev, src_affine, mm_cur, k, thresh);
     }
-    hipLaunchKernelGGL(fn, dim3(grid_for(R, kBlock / g, resident_grid(fn))),
-                       dim3(kBlock), 0,
-                       ctx->stream, row0, R, rp, col, self_in, src, out,
-                       mm_prev, src_affine, mm_cur, k, thresh);
   } else {
     auto fn = mode == MODE_FULL ? algdist_half_wide<MODE_FULL>
                                 : algdist_half_wide<MODE_PARTIAL>;
@@ -1204,6 +1294,66 @@ int init_mm(hgx_ctx *ctx, int *mm, int64_t words) {
                      ctx->stream, mm, words, INT_MIN);
   HGX_LAUNCH_CHECK(ctx);
   return HGX_OK;
+}
+
+__global__ void iota_i32(int *p, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = (int)i;
+}
+__global__ void invert_perm(const int *perm, int *inv, int64_t n) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x)
+    inv[perm[j]] = (int)j;
+}
+
+// tpos[t] = position of node-major incidence t in the edge-major CSR: a
+// stable radix sort of the incidences by edge id keeps node order inside an
+// edge, which is col_e's order (rows sorted by node id).
+int build_tpos(hgx_ctx *ctx) {
+  if (ctx->tpos_ok) return HGX_OK;
+  const int64_t n = ctx->nnz;
+  HGX_TRY(hgx_ensure(ctx, ctx->tpos, sizeof(int) * (size_t)(n + 1)));
+  DevBuf k2, v1, v2, tmp;
+  int rc = HGX_OK;
+  do {
+    if ((rc = hgx_ensure(ctx, k2, sizeof(int) * (size_t)(n + 1))) != HGX_OK) break;
+    if ((rc = hgx_ensure(ctx, v1, sizeof(int) * (size_t)(n + 1))) != HGX_OK) break;
+    if ((rc = hgx_ensure(ctx, v2, sizeof(int) * (size_t)(n + 1))) != HGX_OK) break;
+    hipLaunchKernelGGL(iota_i32, dim3(grid_for(n, 256)), dim3(256), 0,
+                       ctx->stream, v1.as<int>(), n);
+    // keys: a copy of col_n (the sort ping-pongs its buffers)
+    if (hipMemcpyAsync(ctx->tpos.p, ctx->col_n.p, sizeof(int) * (size_t)n,
+                       hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess) {
+      rc = hgx_fail(ctx, HGX_EHIP, "tpos key copy failed");
+      break;
+    }
+    int bits = 1;
+    while (bits < 31 && (1ll << bits) < ctx->E) bits++;
+    hipcub::DoubleBuffer<int> keys(ctx->tpos.as<int>(), k2.as<int>());
+    hipcub::DoubleBuffer<int> vals(v1.as<int>(), v2.as<int>());
+    size_t tb = 0;
+    hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, vals, (int)n, 0, bits,
+                                       ctx->stream);
+    if ((rc = hgx_ensure(ctx, tmp, tb + 256)) != HGX_OK) break;
+    if (hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, keys, vals, (int)n, 0, bits,
+                                           ctx->stream) != hipSuccess) {
+      rc = hgx_fail(ctx, HGX_EHIP, "tpos radix sort failed");
+      break;
+    }
+    // vals.Current()[j] = node-major index of edge-major incidence j
+    hipLaunchKernelGGL(invert_perm, dim3(grid_for(n, 256)), dim3(256), 0,
+                       ctx->stream, vals.Current(), ctx->tpos.as<int>(), n);
+    if (hipGetLastError() != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+      rc = hgx_fail(ctx, HGX_EHIP, "tpos build failed");
+  } while (0);
+  hgx_release(k2);
+  hgx_release(v1);
+  hgx_release(v2);
+  hgx_release(tmp);
+  if (rc == HGX_OK) ctx->tpos_ok = true;
+  return rc;
 }
 
 int final_affine(hgx_ctx *ctx, int node_row0, int node_rows, const int *last) {
@@ -1281,6 +1431,12 @@ extern "C" int hgx_alg_run(hgx_ctx *ctx, int iters) {
   const size_t slot = 2 * (size_t)KS * kRep;
   HGX_TRY(hgx_ensure(ctx, ctx->mm, sizeof(int) * slot * iters));
   int *mm = ctx->mm.as<int>();
+  // push form where it applies (KS <= 16, no long node rows)
+  const bool push = ctx->tune.alg_push && KS <= 16 && ctx->long_n.nlong == 0;
+  if (push) {
+    HGX_TRY(build_tpos(ctx));
+    HGX_TRY(hgx_ensure(ctx, ctx->contrib, sizeof(float) * (size_t)ctx->nnz * KS));
+  }
   HGX_TRY(init_mm(ctx, mm, (int64_t)slot * iters));
   HGX_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
   static const bool sample_env = [] {
@@ -1303,7 +1459,8 @@ extern "C" int hgx_alg_run(hgx_ctx *ctx, int iters) {
     HGX_TRY(launch_half(ctx, MODE_FULL, 0, ctx->N, ctx->rp_n.as<int>(),
                         ctx->col_n.as<int>(), xc, yc, xn, prev, prev != nullptr,
                         cur, ctx->avg_deg_n, ctx->blk_n.as<int>(), ctx->nblk_n,
-                        &ctx->long_n, sample));
+                        &ctx->long_n, sample, push ? PM_PUSH : PM_GATHER,
+                        ctx->tpos.as<int>(), ctx->contrib.as<float>()));
 #ifdef HGX_DEBUG_KNOBS
     {
       const int he = hgx_debug_env("HGX_ALG_HOT_E", 0x7fffffff);
@@ -1313,9 +1470,10 @@ extern "C" int hgx_alg_run(hgx_ctx *ctx, int iters) {
 #endif
     // edge half: self y (scaled), gathered NEW x (raw)
     HGX_TRY(launch_half(ctx, MODE_FULL, 0, ctx->E, ctx->rp_e.as<int>(),
-                        ctx->col_e.as<int>(), yc, xn, yn, prev, 0, cur,
+                        ctx->col_e.as<int>(), yc,
+                        push ? ctx->contrib.as<float>() : xn, yn, prev, 0, cur,
                         ctx->avg_deg_e, ctx->blk_e.as<int>(), ctx->nblk_e,
-                        &ctx->long_e, sample));
+                        &ctx->long_e, sample, push ? PM_STREAM : PM_GATHER));
     ctx->xcur ^= 1;
     ctx->ycur ^= 1;
   }

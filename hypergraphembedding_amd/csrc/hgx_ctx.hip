@@ -130,6 +130,9 @@ extern "C" int hgx_set_tuning(hgx_ctx *ctx, const char *key, int64_t value) {
     HGX_CHECK(ctx, value == 0 || (value >= 64 && value <= (1 << 20)), HGX_EINVAL,
               "alg_long must be 0 or in [64, 2^20]");
     t.alg_long = (int)value;
+  } else if (k == "alg_push") {
+    HGX_CHECK(ctx, value == 0 || value == 1, HGX_EINVAL, "alg_push must be 0 or 1");
+    t.alg_push = (int)value;
   } else if (k == "alg_ks") {
     HGX_CHECK(ctx, value == 0 || (value % 4 == 0 && value <= 20), HGX_EINVAL,
               "alg_ks must be 0 or a multiple of 4 <= 20");
@@ -208,6 +211,7 @@ extern "C" int hgx_upload_incidence(hgx_ctx *ctx, int32_t N, int32_t E,
   ctx->avg_deg_n = (double)nnz / N;
   ctx->avg_deg_e = (double)nnz / E;
   ctx->k = 0;  // alg coords belong to the previous incidence
+  ctx->tpos_ok = false;
   ctx->n_rec = 0;
   ctx->features_ok = ctx->centroids_ok = false;
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -53,6 +53,10 @@ struct Tuning {
   // (0: round_up(k + 1, 4))
   int alg_long = 0;
   int alg_ks = 0;
+  // alg-dist edge half: 0 gather the new node rows through col_e, 1 push
+  // form (the node half writes per-incidence contributions in edge-major
+  // order, the edge half streams them; single GPU, k <= 15)
+  int alg_push = 0;
 };
 
 struct hgx_ctx {
@@ -78,6 +82,10 @@ struct hgx_ctx {
   DevBuf X[2], Y[2];
   int xcur = 0, ycur = 0;
   DevBuf mm;            // per iteration [2][ks] int32 (max, ~min) encodings
+  // push form (tuning alg_push): tpos[t] = edge-major position of node-major
+  // incidence t (built once per incidence), contrib = nnz x ks rows
+  DevBuf tpos, contrib;
+  bool tpos_ok = false;
   // sharded (node-row) mode: own node rows [row0,row1), local edge sub-CSR
   // of those rows, caller-owned exchange buffers (reduced by the caller).
   int32_t row0 = 0, row1 = 0;

@@ -9,3 +9,6 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout
 echo tests-ok
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKEFAIL; tail -20 $O/smoke.log; exit 13; }
 echo smoke-ok
+timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo BENCHFAIL; tail -20 $O/bench.err; exit 14; }
+echo bench-ok
+tail -c 3000 $O/bench.json
