@@ -11,8 +11,10 @@ from hypergraphembedding_amd.synthetic import powerlaw_hypergraph, random_hyperg
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c4"
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+ks = int(sys.argv[4]) if len(sys.argv) > 4 else 0  # alg_ks tuning (0: 12)
 inc = random_hypergraph() if cfg == "c3" else powerlaw_hypergraph()
 ctx = _hgx.Context(0)
+ctx.set_tuning("alg_ks", ks)
 ctx.upload(inc)
 rs = np.random.RandomState(0)
 x0 = rs.random_sample((inc.N, 10)).astype(np.float32)
@@ -29,7 +31,7 @@ for r in range(rounds):
     wall = time.perf_counter() - t
     ms, _ = ctx.alg_stats()
     res[mode].append(ms / iters)
-    print(json.dumps({"cfg": cfg, "push": mode, "round": r,
+    print(json.dumps({"cfg": cfg, "push": mode, "round": r, "ks": ks,
                       "ms_per_iter": round(ms / iters, 4),
                       "gbps": round(b_iter / (ms / iters) / 1e6, 1),
                       "wall_s": round(wall, 3)}), flush=True)
@@ -37,6 +39,6 @@ for r in range(rounds):
       out[mode] = ctx.alg_get()
 d = max(float(np.abs(out[0][0] - out[1][0]).max()),
         float(np.abs(out[0][1] - out[1][1]).max()))
-print(json.dumps({"cfg": cfg, "median_ms_per_iter": {m: round(float(np.median(v)), 4)
+print(json.dumps({"cfg": cfg, "ks": ks, "median_ms_per_iter": {m: round(float(np.median(v)), 4)
                                                       for m, v in res.items()},
                   "max_abs_diff_push_vs_gather": d}), flush=True)
