@@ -1382,9 +1382,17 @@ extern "C" int hgx_alg_set(hgx_ctx *ctx, int k, const float *node_xy,
   HGX_TRY(check_nonempty(ctx));
   int KS = ((k + 1) + 3) / 4 * 4;
   {
-    // rows of 12 floats straddle 64-byte sectors; the alg_ks tuning forces
-    // a wider row stride
+    // Rows of 12 floats (k = 8..11, HOBE's k = 10) straddle the 64-B memory
+    // sectors: half of the random row gathers touch two. Where the tables
+    // spill the 256 MiB Infinity Cache the gathers are served by HBM at the
+    // random-sector rate, and 64-B rows read one sector each: C4 8.17 ->
+    // 7.16 ms per iteration (tools/perf_alg_ks.py, profiles/r03/); C3's
+    // cache-resident 48-B rows stay (0.0447 vs 0.0453 ms). The alg_ks
+    // tuning overrides (12 keeps 48-B rows).
     const int want = ctx->tune.alg_ks;
+    if (want == 0 && KS == 12 &&
+        (int64_t)(ctx->N + (int64_t)ctx->E) * 64 > (int64_t)256 << 20)
+      KS = 16;
     if (want > KS && want % 4 == 0 && want <= 20) KS = want;
   }
   ctx->k = k;

@@ -204,7 +204,13 @@ def sample_sharded(inc, num_neighbors, num_samples, ctx=None, seed=0,
   del gi, gt, li, lt
   if gpu:
     torch.cuda.synchronize(dev)
+    # the gather buffers go back to the device before the context grows its
+    # record buffer (hipMalloc) for the chunk: per rank the peak is the
+    # import copy plus fi (SURVEY §8e budget)
+    torch.cuda.empty_cache()
     ctx.records_import(total, K, fi.data_ptr(), ft.data_ptr(), gbounds)
+    del fi, ft
+    torch.cuda.empty_cache()
   else:
     ctx.records_set(fi[:total].numpy(), ft[:total].numpy())
   return total, allsz

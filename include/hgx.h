@@ -70,7 +70,13 @@ int hgx_synchronize(hgx_ctx *ctx);
  *   "train_tb"         fused step workgroup size (0 auto, 128, 256, 512;
  *                      a size the geometry has no form for -> its default)
  *   "alg_long"         alg-dist long-row threshold (0 = 512, else >= 64)
- *   "alg_ks"           alg-dist coordinate row width in floats (0 = auto)
+ *   "alg_ks"           alg-dist coordinate row width in floats (0 = auto:
+ *                      round_up(k + 1, 4), widened from 12 to 16 floats
+ *                      when the node + edge rows exceed 256 MiB)
+ *   "alg_push"         alg-dist edge half: 0 gather (default), 1 push form
+ *                      (the node half writes per-incidence contributions in
+ *                      edge-major order, the edge half streams them; single
+ *                      GPU, k <= 15; measured slower, kept for the record)
  * Unknown keys and out-of-range values -> HGX_EINVAL. */
 int hgx_set_tuning(hgx_ctx *ctx, const char *key, int64_t value);
 

@@ -11,3 +11,5 @@ timeout -k 10 200 python -u tools/perf_alg_ks.py c3 20 3 > $O/ks_c3.json 2>&1 ||
 cat $O/ks_c3.json
 timeout -k 10 300 python -u tools/perf_alg_ks.py c4 20 3 > $O/ks_c4.json 2>&1 || { echo KS4FAIL; tail $O/ks_c4.json; exit 13; }
 cat $O/ks_c4.json
+timeout -k 10 300 python -u tools/ab_train.py 128 hobe tools/_ab/base.so tools/_ab/gfirst.so > $O/ab_gfirst.log 2>&1 || { echo ABFAIL; tail $O/ab_gfirst.log; exit 14; }
+cat $O/ab_gfirst.log
