@@ -49,7 +49,9 @@ constexpr int kGraphBatches = 64;  // batches per chunk buffer and per graph
 // results are wrong when set): 1 empty K1, 2 empty K2, 4 K1 gathers hit
 // row 0, 8 K1 skips gradient stores, 16 K2 skips slot sums, 32 K2 skips
 // the table read-modify-write; train_step: 1024 shared-row gradients by
-// plain stores.
+// plain stores, 2048 no row-0 partial loads, 4096 no forward reductions,
+// 8192 no Adagrad arithmetic, 16384 no end-of-batch barrier / partial
+// stores, 32768 no neighbour-list gathers (timing ablations: wrong sums).
 #ifdef HGX_DEBUG_KNOBS
 __constant__ int g_tab = 0;  // ablation bits (diagnostic builds only)
 #else
@@ -724,7 +726,8 @@ __device__ __forceinline__ void row0_issue(const TrainArgs &a, int q, int np,
   const int last = max(np - 1, 0);
 #pragma unroll
   for (int u = 0; u < RL::MAXPER; u++)
-    ld.gv[u] = gp[(size_t)min(sub + u * RL::TPC, last) * RL::NC + col];
+    ld.gv[u] = (g_tab & 2048) ? SV<VW>::zero()  // (debug ablation)
+                              : gp[(size_t)min(sub + u * RL::TPC, last) * RL::NC + col];
 }
 // this thread's fixed-order partial sum of partials [0, np) -> s_red
 template <int L, int VW, int TB, int NBFM>
@@ -880,9 +883,12 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
       }
       gather(s);
     }
-    if (wave_lists) {
+    if (wave_lists && !(g_tab & 32768)) {  // (debug ablation: no list gathers)
 #pragma unroll
       for (int s = 4; s < R; s++) gather(s);
+    } else if (wave_lists) {
+#pragma unroll
+      for (int s = 4; s < R; s++) Pv[s] = Av[s] = S::zero();
     }
     // flush slot 0 (one deferred row per group in the common case) rides on
     // the same round trip
@@ -980,12 +986,23 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
         if (row[s] == 0) Pv[s] = s_r0[slot_is_edge(s, K) ? 1 : 0][lane];
       const float inv_b = 1.0f / (float)nb;
       const V &Nl = Pv[0], &El = Pv[1], &Nr = Pv[2], &Er = Pv[3];
-      float z1 = group_sum<L>(S::dot(Nl, Nr)), z2 = group_sum<L>(S::dot(El, Er));
-      float za[K], zb[K];
+      float z1, z2, za[K], zb[K];
+      if (g_tab & 4096) {  // (debug ablation: no reductions)
+        z1 = S::dot(Nl, Nr);
+        z2 = S::dot(El, Er);
 #pragma unroll
-      for (int k = 0; k < K; k++) {
-        za[k] = group_sum<L>(S::dot(Pv[4 + k], Nl));
-        zb[k] = group_sum<L>(S::dot(Pv[4 + K + k], Er));
+        for (int k = 0; k < K; k++) {
+          za[k] = S::dot(Pv[4 + k], Nl);
+          zb[k] = S::dot(Pv[4 + K + k], Er);
+        }
+      } else {
+        z1 = group_sum<L>(S::dot(Nl, Nr));
+        z2 = group_sum<L>(S::dot(El, Er));
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+          za[k] = group_sum<L>(S::dot(Pv[4 + k], Nl));
+          zb[k] = group_sum<L>(S::dot(Pv[4 + K + k], Er));
+        }
       }
       const int act = MODE == 1 ? 0 : 1;
       const int lossk = MODE == 1 ? 0 : 1;
@@ -1043,7 +1060,12 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
           }
         } else {
           V pv = Pv[s], av = Av[s];
-          S::adagrad(pv, av, g, a.lr, a.eps);
+          if (g_tab & 8192) {  // (debug ablation: no Adagrad arithmetic)
+            pv = S::add(pv, g);
+            av = S::add(av, g);
+          } else {
+            S::adagrad(pv, av, g, a.lr, a.eps);
+          }
           tab_row<L, VW>(a, edge, 0, row[s])[lane] = pv;
           tab_row<L, VW>(a, edge, 1, row[s])[lane] = av;
         }
@@ -1067,9 +1089,9 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
     s_z[0][grp][lane] = zN;
     s_z[1][grp][lane] = zE;
     if (lane == 0) s_loss[grp] = lrec;
-    __syncthreads();
+    if (!(g_tab & 16384)) __syncthreads();  // (debug ablation: no barrier)
     // this batch's row-0 partial: the workgroup's fixed-order sum
-    if (threadIdx.x < NC) {
+    if (threadIdx.x < NC && !(g_tab & 16384)) {
       V sz = S::zero();
       for (int g = 0; g < RPB; g++) sz = S::add(sz, s_z[tab0][g][c0]);
       reinterpret_cast<V *>(a.gp)[((size_t)(q & 1) * NBFM + blockIdx.x) * NC + col] = sz;
