@@ -119,10 +119,13 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None,
   ctx.upload(inc)
   ctx.alg_set(x0, y0)
   k = x0.shape[1]
-  ks = ((k + 1) + 3) // 4 * 4
-  M = 2 * ks * 64  # HGX_MM_REPLICAS
-  part = torch.zeros(inc.E * ks, dtype=torch.float32, device=dev)
-  mm = torch.zeros(iterations * M, dtype=torch.int32, device=dev)
+  # the library picks the row width KS (round_up(k + 1, 4), widened to 16
+  # floats on large graphs, or the alg_ks tuning, at most 20 on the narrow
+  # path): size the exchange buffers for the widest, trim after begin
+  ks_max = ((k + 1) + 3) // 4 * 4
+  ks_max = max(ks_max, 20) if ks_max <= 20 else ks_max
+  part = torch.zeros(inc.E * ks_max, dtype=torch.float32, device=dev)
+  mm = torch.zeros(iterations * 2 * ks_max * 64, dtype=torch.int32, device=dev)
   slot = None
   if compact:
     # ranks holding incidences of each edge (one int32 all-reduce, once)
@@ -138,8 +141,6 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None,
     wire = torch.zeros(max(n_shared, 1) * (k + 1), dtype=torch.float32,
                        device=dev)[:n_shared * (k + 1)]
     exch = wire
-  else:
-    exch = part
   stream = None
   if on_gpu:
     # kernels and collectives share one (non-default) torch stream: stream
@@ -148,9 +149,13 @@ def alg_dist_sharded(ctx, inc, x0, y0, iterations, group=None, device=None,
     torch.cuda.synchronize(dev)
     ctx.set_stream(stream.cuda_stream)
   try:
-    ks_lib = ctx.alg_shard_begin(r0, r1, part.data_ptr(), mm.data_ptr(),
-                                 iterations)
-    assert ks_lib == ks
+    ks = ctx.alg_shard_begin(r0, r1, part.data_ptr(), mm.data_ptr(),
+                             iterations)
+    assert ks <= ks_max
+    M = 2 * ks * 64  # HGX_MM_REPLICAS
+    part, mm = part[:inc.E * ks], mm[:iterations * M]
+    if not compact:
+      exch = part
     if compact:
       ctx.alg_shard_wire(wire.data_ptr() if n_shared else None, n_shared, slot)
     segs = [exch]

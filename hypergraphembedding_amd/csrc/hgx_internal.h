@@ -272,6 +272,41 @@ __device__ __forceinline__ float group_allreduce_sum(float x) {
   return x;
 }
 
+// group_allreduce_sum<64> of N values at once, bit for bit the same sums:
+// every DPP step of all N values, then the N v_permlane16_swaps back to
+// back, then the N v_permlane32_swaps (four per asm block: 8 operands),
+// instead of N dependent chains each ordered behind the previous one's
+// volatile swaps.
+#define HGX_SWAP4(op)                                                        \
+  asm volatile("s_nop 1\n\t" op " %0, %1\n\t" op " %2, %3\n\t" op       \
+               " %4, %5\n\t" op " %6, %7"                                  \
+               : "+v"(a[i]), "+v"(b[i]), "+v"(a[i + 1]), "+v"(b[i + 1]),      \
+                 "+v"(a[i + 2]), "+v"(b[i + 2]), "+v"(a[i + 3]), "+v"(b[i + 3]))
+template <int N>
+__device__ __forceinline__ void wave_allreduce_sum_n(float (&x)[N]) {
+  static_assert(N % 4 == 0, "groups of four");
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] += dpp_f<0xB1>(x[i]);
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] += dpp_f<0x4E>(x[i]);
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] += dpp_f<0x141>(x[i]);
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] += dpp_f<0x140>(x[i]);
+  float a[N], b[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) a[i] = b[i] = x[i];
+#pragma unroll
+  for (int i = 0; i < N; i += 4) HGX_SWAP4("v_permlane16_swap_b32");
+#pragma unroll
+  for (int i = 0; i < N; i++) a[i] = b[i] = a[i] + b[i];
+#pragma unroll
+  for (int i = 0; i < N; i += 4) HGX_SWAP4("v_permlane32_swap_b32");
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] = a[i] + b[i];
+}
+#undef HGX_SWAP4
+
 // Whole-wave min / max without LDS traffic: the four in-row DPP steps, then
 // the four row results by v_readlane (wave-uniform result). ds_bpermute
 // shuffles go through the CU's LDS pipe: at a kernel tail where every

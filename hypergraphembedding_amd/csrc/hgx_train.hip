@@ -702,59 +702,78 @@ __device__ __forceinline__ void flush_row(const TrainArgs &a, int par, int key, 
 }
 
 // The padding row's partials of the previous batch (np workgroups, at most
-// NBFM: MAXPER = NBFM / TPC loads per thread, index clamped, masked in
-// row0_stage) and its base (shadow of the previous batch, or the table for
-// the first batch of an epoch), issued on the first round trip.
+// NBFM) and its base (shadow of the previous batch, or the table for the
+// first batch of an epoch), issued on the first round trip. A partial is
+// 2 x dp floats (both tables' row 0), loaded as NC4 = 2 dp / 4 float4
+// columns: TPC = TB / NC4 threads per float4 column, MAXPER = NBFM / TPC
+// 16-byte loads per thread (index clamped, masked in row0_stage). Every
+// workgroup reads all np partials (NBFM KB at dp = 128): from the Infinity
+// Cache at its per-CU rate, so 16-byte loads (r03; 8-byte float2 loads at
+// the float2 geometry before) matter. The step's V columns (VW floats) are
+// views of these float4 columns.
 template <int L, int VW, int TB, int NBFM>
 struct Row0Loads {
-  static constexpr int NC = 2 * L, TPC = TB / NC, MAXPER = (NBFM + TPC - 1) / TPC;
-  typename SV<VW>::T gv[MAXPER];
+  static constexpr int NC = 2 * L;                 // V columns
+  static constexpr int NC4 = 2 * L * VW / 4;       // float4 columns
+  static constexpr int TPC = TB / NC4, MAXPER = (NBFM + TPC - 1) / TPC;
+  float4 gv[MAXPER];
   typename SV<VW>::T rp, ra;
 };
 template <int L, int VW, int TB, int NBFM>
 __device__ __forceinline__ void row0_issue(const TrainArgs &a, int q, int np,
                                            Row0Loads<L, VW, TB, NBFM> &ld) {
   using RL = Row0Loads<L, VW, TB, NBFM>;
-  using V = typename SV<VW>::T;
-  static_assert(TB % RL::NC == 0, "workgroup covers whole columns");
-  const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
+  static_assert(TB % RL::NC == 0 && TB % RL::NC4 == 0, "workgroup covers whole columns");
+  const int col = threadIdx.x % RL::NC;
   const int tab = col / L, c = col % L, ppar = (q + 2) % 3;
   // the address is selected (q is uniform), not the loaded value
   ld.rp = (q ? sh_row<L, VW>(a, ppar, tab, 0) : tab_row<L, VW>(a, tab, 0, 0))[c];
   ld.ra = (q ? sh_row<L, VW>(a, ppar, tab, 1) : tab_row<L, VW>(a, tab, 1, 0))[c];
-  const V *gp = reinterpret_cast<const V *>(a.gp) + (size_t)((q + 1) & 1) * NBFM * RL::NC;
+  const int col4 = threadIdx.x % RL::NC4, sub = threadIdx.x / RL::NC4;
+  const float4 *gp = reinterpret_cast<const float4 *>(a.gp) +
+                     (size_t)((q + 1) & 1) * NBFM * RL::NC4;
   const int last = max(np - 1, 0);
 #pragma unroll
   for (int u = 0; u < RL::MAXPER; u++)
-    ld.gv[u] = (g_tab & 2048) ? SV<VW>::zero()  // (debug ablation)
-                              : gp[(size_t)min(sub + u * RL::TPC, last) * RL::NC + col];
+    ld.gv[u] = (g_tab & 2048) ? f4(0.f)  // (debug ablation)
+                              : gp[(size_t)min(sub + u * RL::TPC, last) * RL::NC4 + col4];
 }
 // this thread's fixed-order partial sum of partials [0, np) -> s_red
 template <int L, int VW, int TB, int NBFM>
 __device__ __forceinline__ void row0_stage(int np, const Row0Loads<L, VW, TB, NBFM> &ld,
-                                           typename SV<VW>::T (*s_red)[2 * L]) {
+                                           float4 (*s_red)[Row0Loads<L, VW, TB, NBFM>::NC4]) {
   using RL = Row0Loads<L, VW, TB, NBFM>;
-  using S = SV<VW>;
-  const int col = threadIdx.x % RL::NC, sub = threadIdx.x / RL::NC;
-  typename S::T g = S::zero();
+  const int col4 = threadIdx.x % RL::NC4, sub = threadIdx.x / RL::NC4;
+  float4 g = f4(0.f);
 #pragma unroll
-  for (int u = 0; u < RL::MAXPER; u++)
-    g = S::add(g, S::mul(ld.gv[u], (float)(sub + u * RL::TPC < np)));
-  s_red[sub][col] = g;
+  for (int u = 0; u < RL::MAXPER; u++) {
+    const float m = (float)(sub + u * RL::TPC < np);
+    const float4 v = ld.gv[u];
+    g = g + make_float4(v.x * m, v.y * m, v.z * m, v.w * m);
+  }
+  s_red[sub][col4] = g;
 }
-// after a workgroup barrier: column owners (sub == 0) add the TPC staged sums
-// in order and apply the previous batch's row-0 step (zero gradient for the
-// first batch of an epoch: an identity)
+// after a workgroup barrier: V-column owners (threads < NC) add the TPC
+// staged sums of their float4 column in order (their half of it at VW = 2)
+// and apply the previous batch's row-0 step (zero gradient for the first
+// batch of an epoch: an identity)
 template <int L, int VW, int TB, int NBFM>
 __device__ __forceinline__ void row0_finish(const TrainArgs &a,
-                                            typename SV<VW>::T (*s_red)[2 * L],
+                                            float4 (*s_red)[Row0Loads<L, VW, TB, NBFM>::NC4],
                                             typename SV<VW>::T &p0, typename SV<VW>::T &a0) {
   using RL = Row0Loads<L, VW, TB, NBFM>;
   using S = SV<VW>;
   const int col = threadIdx.x % RL::NC;
   typename S::T gs = S::zero();
 #pragma unroll
-  for (int j = 0; j < RL::TPC; j++) gs = S::add(gs, s_red[j][col]);
+  for (int j = 0; j < RL::TPC; j++) {
+    const float4 v = s_red[j][col * VW / 4];
+    if constexpr (VW == 4) {
+      gs = S::add(gs, v);
+    } else {
+      gs = S::add(gs, (col & 1) ? make_float2(v.z, v.w) : make_float2(v.x, v.y));
+    }
+  }
   S::adagrad(p0, a0, gs, a.lr, a.eps);
 }
 
@@ -772,7 +791,8 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
   static_assert(R + kWX <= 32, "slot and batch words fit the first 32 lanes");
   __shared__ V s_z[2][RPB][L];
   __shared__ V s_gl[RPB][R][L];  // gradients of local (one-record) rows
-  __shared__ V s_red[TB / NC][NC];
+  using RL0 = Row0Loads<L, VW, TB, NBFM>;
+  __shared__ float4 s_red[RL0::TPC][RL0::NC4];
   __shared__ V s_r0[2][L];
   __shared__ float s_loss[RPB];
   unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -994,6 +1014,24 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
         for (int k = 0; k < K; k++) {
           za[k] = S::dot(Pv[4 + k], Nl);
           zb[k] = S::dot(Pv[4 + K + k], Er);
+        }
+      } else if constexpr (L == 64 && (2 + 2 * K) % 4 == 0) {
+        // the 2 + 2K head dots reduced together (same sums, no serial chain)
+        float zz[2 + 2 * K];
+        zz[0] = S::dot(Nl, Nr);
+        zz[1] = S::dot(El, Er);
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+          zz[2 + k] = S::dot(Pv[4 + k], Nl);
+          zz[2 + K + k] = S::dot(Pv[4 + K + k], Er);
+        }
+        hgx::wave_allreduce_sum_n<2 + 2 * K>(zz);
+        z1 = zz[0];
+        z2 = zz[1];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+          za[k] = zz[2 + k];
+          zb[k] = zz[2 + K + k];
         }
       } else {
         z1 = group_sum<L>(S::dot(Nl, Nr));
@@ -1656,7 +1694,7 @@ void step_fns(int loss, KStepFn *kf, KFlushFn &kfl) {
                     : train_step<SL, VW, 5, 2, TB, NBFM, false>;
   kf[1] = loss == 0 ? train_step<SL, VW, 5, 1, TB, NBFM, true>
                     : train_step<SL, VW, 5, 2, TB, NBFM, true>;
-  kfl = train_flush<SL * VW / 4, NBFM, TB / (2 * SL)>;
+  kfl = train_flush<SL * VW / 4, NBFM, Row0Loads<SL, VW, TB, NBFM>::TPC>;
 }
 // lanes = the tuning (0 auto, 32 or 64 lanes per record where dp = 128);
 // sets sl (the step's lanes per record), tb, nbfm and the kernels

@@ -33,7 +33,8 @@ def _graph(name):
   return powerlaw_hypergraph(N=20_000, E=10_000, seed=5)  # long edge rows
 
 
-def _worker(rank, world, port, out_path, iters, graph="tiny", edge_ranges=1):
+def _worker(rank, world, port, out_path, iters, graph="tiny", edge_ranges=1,
+            ks=0):
   import torch
   import torch.distributed as dist
   import sys
@@ -50,6 +51,7 @@ def _worker(rank, world, port, out_path, iters, graph="tiny", edge_ranges=1):
   r = O.Rng(0)
   x0, y0 = r.random((inc.N, 10)), r.random((inc.E, 10))
   ctx = _hgx.Context(0)
+  ctx.set_tuning("alg_ks", ks)  # 16: the 64-B rows large graphs get
   (r0, r1, xo), y, ms = alg_dist_sharded(ctx, inc, x0, y0, iters,
                                          edge_ranges=edge_ranges)
   np.savez(out_path + f".{rank}.npz", r0=r0, r1=r1, x=xo, y=y)
@@ -78,15 +80,17 @@ def test_sharded_algdist_matches_reference(tmp_path, world):
   assert np.abs(ys[0] - z["y_20"]).max() <= 1e-4
 
 
-@pytest.mark.parametrize("ranges", [1, 4])
-def test_sharded_algdist_powerlaw_long_rows(tmp_path, ranges):
+@pytest.mark.parametrize("ranges,ks", [(1, 0), (4, 0), (4, 16)])
+def test_sharded_algdist_powerlaw_long_rows(tmp_path, ranges, ks):
   """ranges = 4: edge partials per range (each with its own long rows) and
-  the exchange of each range issued asynchronously."""
+  the exchange of each range issued asynchronously; ks = 16: 64-B
+  coordinate rows (the library's choice above 256 MiB of rows), exchange
+  buffers sized by the library's row width."""
   import torch.multiprocessing as mp
   world, iters = 2, 10
   out = str(tmp_path / "shard")
   mp.start_processes(_worker, args=(world, _free_port(), out, iters, "powerlaw",
-                                    ranges),
+                                    ranges, ks),
                      nprocs=world, join=True, start_method="spawn")
   inc = _graph("powerlaw")
   r = O.Rng(0)
