@@ -111,15 +111,17 @@ struct TrainArgs {
   // keys from train_prep; deferred entries per batch (pM), flush overflow
   // list (pfo). gacc [3][MX][dp] fixed-point sums and shadow [3][MX][2][dp]
   // base rows of deferred entries by batch parity (entries 0 / 1: row 0 of
-  // the node / edge table, shadow only); gp [2][NBF][2][dp] the padding
-  // row's per-workgroup gradient partials; ovf the fixed-point range flag.
+  // the node / edge table, shadow only); r0acc the padding row's gradient
+  // sums, kR0Slots fixed-point accumulators per batch parity; ovf the
+  // fixed-point range flag.
   int fused, prpb, RW, MX, Mmax;
   int *pidx, *pbrk;
   unsigned *pcode, *scode;
   float *ptgt;
   int2 *pfo;
   long long *gacc;
-  float *shadow, *gp;
+  float *shadow;
+  long long *r0acc;  // [3][kR0Slots][2][dp] fixed point, see Row0Loads
   int *ovf;
 };
 
@@ -620,6 +622,13 @@ struct SV<4> {
     longlong2 *g = reinterpret_cast<longlong2 *>(e) + 2 * lane;
     g[0] = g[1] = make_longlong2(0, 0);
   }
+  static __device__ __forceinline__ Fx fxadd(const Fx &x, const Fx &y) {
+    return {make_longlong2(x.a.x + y.a.x, x.a.y + y.a.y),
+            make_longlong2(x.b.x + y.b.x, x.b.y + y.b.y)};
+  }
+  static __device__ __forceinline__ Fx fxzero() {
+    return {make_longlong2(0, 0), make_longlong2(0, 0)};
+  }
 };
 template <>
 struct SV<2> {
@@ -661,6 +670,10 @@ struct SV<2> {
   static __device__ __forceinline__ void zerofix(long long *e, int lane) {
     reinterpret_cast<longlong2 *>(e)[lane] = make_longlong2(0, 0);
   }
+  static __device__ __forceinline__ Fx fxadd(const Fx &x, const Fx &y) {
+    return {make_longlong2(x.a.x + y.a.x, x.a.y + y.a.y)};
+  }
+  static __device__ __forceinline__ Fx fxzero() { return {make_longlong2(0, 0)}; }
 };
 // the deferred Adagrad step of the previous batch: (p, a) += sum
 template <int VW>
@@ -701,80 +714,59 @@ __device__ __forceinline__ void flush_row(const TrainArgs &a, int par, int key, 
   tab_row<L, VW>(a, edge, 1, row)[lane] = ac;
 }
 
-// The padding row's partials of the previous batch (np workgroups, at most
-// NBFM) and its base (shadow of the previous batch, or the table for the
-// first batch of an epoch), issued on the first round trip. A partial is
-// 2 x dp floats (both tables' row 0), loaded as NC4 = 2 dp / 4 float4
-// columns: TPC = TB / NC4 threads per float4 column, MAXPER = NBFM / TPC
-// 16-byte loads per thread (index clamped, masked in row0_stage). Every
-// workgroup reads all np partials (NBFM KB at dp = 128): from the Infinity
-// Cache at its per-CU rate, so 16-byte loads (r03; 8-byte float2 loads at
-// the float2 geometry before) matter. The step's V columns (VW floats) are
-// views of these float4 columns.
-template <int L, int VW, int TB, int NBFM>
+// The padding row (row 0 of both tables) of the previous batch. Its
+// gradient sum arrives in kR0Slots fixed-point accumulators r0acc[q % 3]:
+// every workgroup of batch q adds its records' row-0 gradients (a
+// fixed-order float sum over its records, then one 2^44 fixed-point
+// integer atomic per element) to slot blockIdx % kR0Slots, so the sum is
+// exact and independent of arrival order. Batch q + 1 reads the kR0Slots
+// slots (the owner thread of each column: kR0Slots x VW int64), adds them
+// as integers and applies the Adagrad step to the base (the previous
+// batch's shadow, or the table for the first batch of an epoch); batch q
+// zeroes set (q + 1) % 3 for the next batch. r02/r03a instead had every
+// workgroup store a float partial and every workgroup of the next batch
+// read all 64 of them: 64 KB per workgroup from the Infinity Cache, about
+// 0.9 us per batch at its per-CU rate (tools/ablate_train.py); now 16 KB.
+constexpr int kR0Slots = 8;
+template <int L, int VW>
+__device__ __forceinline__ long long *r0_row(const TrainArgs &a, int par, int slot,
+                                             int tab) {
+  return a.r0acc + (((size_t)par * kR0Slots + slot) * 2 + tab) * (VW * L);
+}
+template <int L, int VW>
 struct Row0Loads {
-  static constexpr int NC = 2 * L;                 // V columns
-  static constexpr int NC4 = 2 * L * VW / 4;       // float4 columns
-  static constexpr int TPC = TB / NC4, MAXPER = (NBFM + TPC - 1) / TPC;
-  float4 gv[MAXPER];
+  static constexpr int NC = 2 * L;  // V columns (both tables)
+  typename SV<VW>::Fx g[kR0Slots];
   typename SV<VW>::T rp, ra;
 };
-template <int L, int VW, int TB, int NBFM>
-__device__ __forceinline__ void row0_issue(const TrainArgs &a, int q, int np,
-                                           Row0Loads<L, VW, TB, NBFM> &ld) {
-  using RL = Row0Loads<L, VW, TB, NBFM>;
-  static_assert(TB % RL::NC == 0 && TB % RL::NC4 == 0, "workgroup covers whole columns");
+// every load issued unconditionally, first thing in the kernel (a load
+// under a branch is waited for at the join); threads >= NC load column
+// col - NC's words too (unused), q == 0 loads set 2 (not read)
+template <int L, int VW>
+__device__ __forceinline__ void row0_issue(const TrainArgs &a, int q,
+                                           Row0Loads<L, VW> &ld) {
+  using RL = Row0Loads<L, VW>;
   const int col = threadIdx.x % RL::NC;
   const int tab = col / L, c = col % L, ppar = (q + 2) % 3;
   // the address is selected (q is uniform), not the loaded value
   ld.rp = (q ? sh_row<L, VW>(a, ppar, tab, 0) : tab_row<L, VW>(a, tab, 0, 0))[c];
   ld.ra = (q ? sh_row<L, VW>(a, ppar, tab, 1) : tab_row<L, VW>(a, tab, 1, 0))[c];
-  const int col4 = threadIdx.x % RL::NC4, sub = threadIdx.x / RL::NC4;
-  const float4 *gp = reinterpret_cast<const float4 *>(a.gp) +
-                     (size_t)((q + 1) & 1) * NBFM * RL::NC4;
-  const int last = max(np - 1, 0);
 #pragma unroll
-  for (int u = 0; u < RL::MAXPER; u++)
-    ld.gv[u] = (g_tab & 2048) ? f4(0.f)  // (debug ablation)
-                              : gp[(size_t)min(sub + u * RL::TPC, last) * RL::NC4 + col4];
+  for (int j = 0; j < kR0Slots; j++)
+    ld.g[j] = SV<VW>::ldfix(r0_row<L, VW>(a, ppar, j, tab), c);
 }
-// this thread's fixed-order partial sum of partials [0, np) -> s_red
-template <int L, int VW, int TB, int NBFM>
-__device__ __forceinline__ void row0_stage(int np, const Row0Loads<L, VW, TB, NBFM> &ld,
-                                           float4 (*s_red)[Row0Loads<L, VW, TB, NBFM>::NC4]) {
-  using RL = Row0Loads<L, VW, TB, NBFM>;
-  const int col4 = threadIdx.x % RL::NC4, sub = threadIdx.x / RL::NC4;
-  float4 g = f4(0.f);
-#pragma unroll
-  for (int u = 0; u < RL::MAXPER; u++) {
-    const float m = (float)(sub + u * RL::TPC < np);
-    const float4 v = ld.gv[u];
-    g = g + make_float4(v.x * m, v.y * m, v.z * m, v.w * m);
-  }
-  s_red[sub][col4] = g;
-}
-// after a workgroup barrier: V-column owners (threads < NC) add the TPC
-// staged sums of their float4 column in order (their half of it at VW = 2)
-// and apply the previous batch's row-0 step (zero gradient for the first
-// batch of an epoch: an identity)
-template <int L, int VW, int TB, int NBFM>
-__device__ __forceinline__ void row0_finish(const TrainArgs &a,
-                                            float4 (*s_red)[Row0Loads<L, VW, TB, NBFM>::NC4],
+// column owners (threads < NC): the slots' exact integer sum, the previous
+// batch's row-0 step (zero gradient for the first batch of an epoch)
+template <int L, int VW>
+__device__ __forceinline__ void row0_finish(const TrainArgs &a, int q,
+                                            const Row0Loads<L, VW> &ld,
                                             typename SV<VW>::T &p0, typename SV<VW>::T &a0) {
-  using RL = Row0Loads<L, VW, TB, NBFM>;
   using S = SV<VW>;
-  const int col = threadIdx.x % RL::NC;
-  typename S::T gs = S::zero();
+  typename S::Fx t = ld.g[0];
 #pragma unroll
-  for (int j = 0; j < RL::TPC; j++) {
-    const float4 v = s_red[j][col * VW / 4];
-    if constexpr (VW == 4) {
-      gs = S::add(gs, v);
-    } else {
-      gs = S::add(gs, (col & 1) ? make_float2(v.z, v.w) : make_float2(v.x, v.y));
-    }
-  }
-  S::adagrad(p0, a0, gs, a.lr, a.eps);
+  for (int j = 1; j < kR0Slots; j++) t = S::fxadd(t, ld.g[j]);
+  if (g_tab & 2048) t = S::fxzero();  // (debug ablation)
+  if (q) S::adagrad(p0, a0, S::unfix(t), a.lr, a.eps);
 }
 
 // One launch = one batch. q = the batch's index in the epoch (parities
@@ -791,8 +783,6 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
   static_assert(R + kWX <= 32, "slot and batch words fit the first 32 lanes");
   __shared__ V s_z[2][RPB][L];
   __shared__ V s_gl[RPB][R][L];  // gradients of local (one-record) rows
-  using RL0 = Row0Loads<L, VW, TB, NBFM>;
-  __shared__ float4 s_red[RL0::TPC][RL0::NC4];
   __shared__ V s_r0[2][L];
   __shared__ float s_loss[RPB];
   unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -821,11 +811,10 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
     yt1 = yt[1];
     yt2 = yt[2];
   }
-  // the previous launch was a full batch: its NBF workgroups all stored
-  // (none for the first batch of an epoch: row 0 from the table)
-  const int np = q ? NBF : 0;
-  Row0Loads<L, VW, TB, NBFM> r0l;
-  row0_issue<L, VW, TB, NBFM>(a, q, np, r0l);
+  // the previous batch's row-0 gradient slots (none for the first batch of
+  // an epoch: row 0 from the table)
+  Row0Loads<L, VW> r0l;
+  row0_issue<L, VW>(a, q, r0l);
   {
 #pragma unroll
     for (int s = 0; s < R + kFX; s++) {
@@ -866,9 +855,6 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
   const int col = threadIdx.x % NC, sub = threadIdx.x / NC, tab0 = col / L, c0 = col % L;
   int bad = 0;
   if (nval > 0) {
-    // staged before the gathers: frees the partials' registers (and waits
-    // for round trip 1 before the branchy gather issue)
-    row0_stage<L, VW, TB, NBFM>(np, r0l, s_red);
     V p0 = r0l.rp, a0 = r0l.ra;
     S::pin(p0);
     S::pin(a0);
@@ -923,9 +909,8 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
       fa = sh_row<L, VW>(a, ppar, mf, 1)[lane];
       fg = S::ldfix(gacc_row<L, VW>(a, ppar, mf), lane);
     }
-    __syncthreads();  // s_red
     if (sub == 0) {
-      row0_finish<L, VW, TB, NBFM>(a, s_red, p0, a0);
+      row0_finish<L, VW>(a, q, r0l, p0, a0);
       s_r0[tab0][c0] = p0;
       if (blockIdx.x == 0) {
         sh_row<L, VW>(a, par, tab0, 0)[c0] = p0;
@@ -1128,11 +1113,12 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
     s_z[1][grp][lane] = zE;
     if (lane == 0) s_loss[grp] = lrec;
     if (!(g_tab & 16384)) __syncthreads();  // (debug ablation: no barrier)
-    // this batch's row-0 partial: the workgroup's fixed-order sum
+    // this batch's row-0 gradients: the workgroup's fixed-order sum, added
+    // to its slot of r0acc[q % 3] in fixed point
     if (threadIdx.x < NC && !(g_tab & 16384)) {
       V sz = S::zero();
       for (int g = 0; g < RPB; g++) sz = S::add(sz, s_z[tab0][g][c0]);
-      reinterpret_cast<V *>(a.gp)[((size_t)(q & 1) * NBFM + blockIdx.x) * NC + col] = sz;
+      S::addfix(r0_row<L, VW>(a, par, blockIdx.x % kR0Slots, tab0), c0, sz, bad);
     }
     if (threadIdx.x == 0) {
       float sl = 0.f;
@@ -1158,12 +1144,15 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
     flush_row<L, VW>(a, ppar, en.x, en.y, lane);
   }
   // zero the gacc parity the next batch adds into (its deferred entries
-  // [2, 2 + zc) were used two batches ago)
+  // [2, 2 + zc) were used two batches ago) and the row-0 slots it adds into
   {
     longlong2 *z = reinterpret_cast<longlong2 *>(gacc_row<L, VW>(a, zpar, 2));
     const int tot = zc * (VW / 2) * L;
     for (int i = blockIdx.x * TB + threadIdx.x; i < tot; i += NBF * TB)
       z[i] = make_longlong2(0, 0);
+    longlong2 *zr = reinterpret_cast<longlong2 *>(r0_row<L, VW>(a, zpar, 0, 0));
+    for (int i = blockIdx.x * TB + threadIdx.x; i < kR0Slots * VW * L; i += NBF * TB)
+      zr[i] = make_longlong2(0, 0);
   }
   // (timing ablations compute wrong values: no overflow verdict for them)
   if (__any(bad) && !g_tab && (threadIdx.x & 63) == 0) atomicOr(a.ovf, 1);
@@ -1185,15 +1174,11 @@ __global__ __launch_bounds__(256) void train_flush(TrainArgs a, const int *keys,
   const int par = q % 3, opar = (q + 2) % 3;
   const int M = 2 + *Ml, zc = Mp ? *Mp : 0;
   for (int e = blockIdx.x * GPB + grp; e < M; e += gridDim.x * GPB) {
-    if (e < 2) {  // row 0: the partials summed in train_step's order
-      const float4 *gp = reinterpret_cast<const float4 *>(a.gp) +
-                         (size_t)(q & 1) * NBFM * 2 * L + e * L;
-      float4 g = f4(0.f);
-      for (int sub = 0; sub < TPC; sub++) {
-        float4 gs = f4(0.f);
-        for (int w = sub; w < np; w += TPC) gs = gs + gp[(size_t)w * 2 * L + lane];
-        g = g + gs;
-      }
+    if (e < 2) {  // row 0: the last batch's slots, summed as train_step sums
+      SV<4>::Fx t = SV<4>::ldfix(r0_row<L, 4>(a, par, 0, e), lane);
+      for (int j = 1; j < kR0Slots; j++)
+        t = SV<4>::fxadd(t, SV<4>::ldfix(r0_row<L, 4>(a, par, j, e), lane));
+      const float4 g = SV<4>::unfix(t);
       float4 p = sh_row<L, 4>(a, par, e, 0)[lane], ac = sh_row<L, 4>(a, par, e, 1)[lane];
       adagrad4_hw(p, ac, g, a.lr, a.eps);
       tab_row<L, 4>(a, e, 0, 0)[lane] = p;
@@ -1694,7 +1679,7 @@ void step_fns(int loss, KStepFn *kf, KFlushFn &kfl) {
                     : train_step<SL, VW, 5, 2, TB, NBFM, false>;
   kf[1] = loss == 0 ? train_step<SL, VW, 5, 1, TB, NBFM, true>
                     : train_step<SL, VW, 5, 2, TB, NBFM, true>;
-  kfl = train_flush<SL * VW / 4, NBFM, Row0Loads<SL, VW, TB, NBFM>::TPC>;
+  kfl = train_flush<SL * VW / 4, NBFM, 1>;
 }
 // lanes = the tuning (0 auto, 32 or 64 lanes per record where dp = 128);
 // sets sl (the step's lanes per record), tb, nbfm and the kernels
@@ -2091,7 +2076,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   const size_t gz_f = (size_t)nblk1 * 2 * dp;
   const size_t gacc_f = (size_t)3 * MX * dp * 2;  // in floats
   const size_t sh_f = (size_t)3 * MX * 2 * dp;
-  const size_t gp_f = (size_t)2 * NBFM * 2 * dp;
+  const size_t gp_f = (size_t)3 * kR0Slots * 2 * dp * 2;  // r0acc (int64)
   const size_t s3_f = (gz_f + 3) / 4 * 4 + gacc_f + sh_f + gp_f + 16;
   HGX_TRY(hgx_ensure(ctx, ctx->s3, sizeof(float) * s3_f));
   HGX_TRY(hgx_ensure(ctx, ctx->s4, sizeof(float) * (size_t)nbatches * lstride + 16));
@@ -2132,7 +2117,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     f += gacc_f;
     a.shadow = f;
     f += sh_f;
-    a.gp = f;
+    a.r0acc = reinterpret_cast<long long *>(f);
     f += gp_f;
     a.ovf = reinterpret_cast<int *>(f);
   }
@@ -2296,6 +2281,10 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     (void)hipMemsetAsync(dloss, 0, sizeof(double), ctx->stream);
     (void)hipMemsetAsync(a.lossbuf, 0, sizeof(float) * (size_t)nbatches * lstride,
                          ctx->stream);
+    // row-0 slots start at zero every epoch (then each batch zeroes the set
+    // the next one adds into)
+    if (fused)
+      (void)hipMemsetAsync(a.r0acc, 0, sizeof(float) * gp_f, ctx->stream);
     int last_nbc = 0;
     for (int64_t c = 0; c < nchunks; c++) {
       const int64_t base = c * CB;
