@@ -771,10 +771,10 @@ __device__ __forceinline__ void row0_finish(const TrainArgs &a, int q,
 
 // One launch = one batch. q = the batch's index in the epoch (parities
 // q % 3 and q & 1). One L-lane group per record (dp == 4L), RPB = TB / L
-// records per workgroup, ceil(B / RPB) <= NBFM workgroups; records placed by
+// records per workgroup, ceil(B / RPB) workgroups; records placed by
 // train_place, those without neighbour lists first (whole waves skip the list
 // gathers).
-template <int L, int VW, int KMAX, int MODE, int TB, int NBFM, bool MULTI>
+template <int L, int VW, int KMAX, int MODE, int TB, bool MULTI>
 __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, int nb, int q) {
   constexpr int RPB = TB / L, R = 4 + 2 * KMAX, K = KMAX, NC = 2 * L;
   using S = SV<VW>;
@@ -1165,7 +1165,7 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
 // keys from train_prep), and every gacc entry still in use zeroed (the last
 // batch's and the one before it, Ml and Mp entries). One L-lane group per
 // entry.
-template <int L, int NBFM, int TPC>
+template <int L>
 __global__ __launch_bounds__(256) void train_flush(TrainArgs a, const int *keys,
                                                    const int *Ml, const int *Mp,
                                                    int q, int np) {
@@ -1670,21 +1670,20 @@ using KFlushFn = void (*)(TrainArgs, const int *, const int *, const int *, int,
 // HOBE (relu/MSE) heads. One SL-lane group per record with VW floats per lane
 // (dp = SL VW): float4 x 32 lanes or float2 x 64 lanes for dp = 128, float4 x
 // 64 lanes for dp = 256. tb = the workgroup size (records per workgroup =
-// tb / SL); nbfm = the workgroup cap of the instantiation (every workgroup
-// loads nbfm / (tb / 2 SL) row-0 partials per thread). The flush kernel views
-// rows as float4 and sums the row-0 partials in the step's order (its TPC).
-template <int SL, int VW, int TB, int NBFM>
+// tb / SL, ceil(batch / (tb / SL)) workgroups). The flush kernel views rows
+// as float4.
+template <int SL, int VW, int TB>
 void step_fns(int loss, KStepFn *kf, KFlushFn &kfl) {
-  kf[0] = loss == 0 ? train_step<SL, VW, 5, 1, TB, NBFM, false>
-                    : train_step<SL, VW, 5, 2, TB, NBFM, false>;
-  kf[1] = loss == 0 ? train_step<SL, VW, 5, 1, TB, NBFM, true>
-                    : train_step<SL, VW, 5, 2, TB, NBFM, true>;
-  kfl = train_flush<SL * VW / 4, NBFM, 1>;
+  kf[0] = loss == 0 ? train_step<SL, VW, 5, 1, TB, false>
+                    : train_step<SL, VW, 5, 2, TB, false>;
+  kf[1] = loss == 0 ? train_step<SL, VW, 5, 1, TB, true>
+                    : train_step<SL, VW, 5, 2, TB, true>;
+  kfl = train_flush<SL * VW / 4>;
 }
 // lanes = the tuning (0 auto, 32 or 64 lanes per record where dp = 128);
-// sets sl (the step's lanes per record), tb, nbfm and the kernels
-bool pick_step(int L, int VPL, int K, int loss, int act, int batch, int lanes, int &sl,
-               int &tb, int &nbfm, KStepFn *kf, KFlushFn &kfl) {
+// sets sl (the step's lanes per record), tb and the kernels
+bool pick_step(int L, int VPL, int K, int loss, int act, int lanes, int &sl,
+               int &tb, KStepFn *kf, KFlushFn &kfl) {
   if (VPL != 1 || K != 5 || loss != act) return false;
   if (L != 32 && L != 64) return false;
   // dp = 128, measured r02 (tools/ab_train.py, interleaved, us per batch on
@@ -1692,20 +1691,18 @@ bool pick_step(int L, int VPL, int K, int loss, int act, int batch, int lanes, i
   // float4 x 32 lanes at 128 threads 8.07 / 8.42 (8.33 / 8.75 at 256)
   const int vw = L == 32 && lanes != 32 ? 2 : 4;
   sl = L * 4 / vw;
-  if (sl == 32) tb = tb == 256 ? 256 : 128;
-  else if (vw == 2) tb = tb == 512 ? 512 : 256;
-  else tb = 256;
-  const int nbf = (batch + tb / sl - 1) / (tb / sl);
-  nbfm = nbf <= 32 ? 32 : 64;
-  if (nbf > nbfm) return false;
   if (sl == 32) {
-    if (tb == 128) nbfm == 32 ? step_fns<32, 4, 128, 32>(loss, kf, kfl) : step_fns<32, 4, 128, 64>(loss, kf, kfl);
-    else nbfm == 32 ? step_fns<32, 4, 256, 32>(loss, kf, kfl) : step_fns<32, 4, 256, 64>(loss, kf, kfl);
+    tb = tb == 256 ? 256 : 128;
+    if (tb == 128) step_fns<32, 4, 128>(loss, kf, kfl);
+    else step_fns<32, 4, 256>(loss, kf, kfl);
   } else if (vw == 2) {
-    if (tb == 512) nbfm == 32 ? step_fns<64, 2, 512, 32>(loss, kf, kfl) : step_fns<64, 2, 512, 64>(loss, kf, kfl);
-    else nbfm == 32 ? step_fns<64, 2, 256, 32>(loss, kf, kfl) : step_fns<64, 2, 256, 64>(loss, kf, kfl);
+    tb = tb == 512 || tb == 128 ? tb : 256;
+    if (tb == 512) step_fns<64, 2, 512>(loss, kf, kfl);
+    else if (tb == 128) step_fns<64, 2, 128>(loss, kf, kfl);
+    else step_fns<64, 2, 256>(loss, kf, kfl);
   } else {
-    nbfm == 32 ? step_fns<64, 4, 256, 32>(loss, kf, kfl) : step_fns<64, 4, 256, 64>(loss, kf, kfl);
+    tb = 256;
+    step_fns<64, 4, 256>(loss, kf, kfl);
   }
   return true;
 }
@@ -2034,11 +2031,11 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   KStepFn kf[2] = {nullptr, nullptr};  // light / MULTI pending-slot forms
   KFlushFn kfl = nullptr;
   int tbf = ctx->tune.train_tb;  // workgroup size (0: per geometry)
-  int NBFM = 0, SL = 0;
+  int SL = 0;
   const bool fused = ctx->tune.train_fused && env_int("HGX_TRAIN_GENERIC", 0) != 1 &&
                      batch <= kPackB &&
-                     pick_step(L, VPL, K, loss, act, batch, ctx->tune.train_lanes, SL, tbf,
-                               NBFM, kf, kfl);
+                     pick_step(L, VPL, K, loss, act, ctx->tune.train_lanes, SL, tbf,
+                               kf, kfl);
   const int prpb = fused ? tbf / SL : 0;
   const int NBF = fused ? (batch + prpb - 1) / prpb : 0;
   const int RW = R + kWX;
@@ -2072,7 +2069,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   HGX_TRY(hgx_ensure(ctx, ctx->s1, sizeof(int) * (n + 1)));              // perm
   HGX_TRY(hgx_ensure(ctx, ctx->s2, sizeof(float) * (size_t)SB * dp));    // gslot
   // gzero (K1 partials) | gacc [3][MX][dp] int64 | shadow [3][MX][2][dp] |
-  // gp [2][NBFM][2][dp] | ovf
+  // r0acc [3][kR0Slots][2][dp] int64 | ovf
   const size_t gz_f = (size_t)nblk1 * 2 * dp;
   const size_t gacc_f = (size_t)3 * MX * dp * 2;  // in floats
   const size_t sh_f = (size_t)3 * MX * 2 * dp;
