@@ -568,6 +568,7 @@ __device__ int block_exclusive_scan(int v, int *total, int *s_ws) {
 // below 2^63. A value outside the range (a diverged run, or NaN) raises the
 // step's overflow flag and hgx_train fails with HGX_ENUMERIC.
 constexpr double kFixScale = 17592186044416.0;  // 2^44
+constexpr double kFixScaleL = 18014398509481984.0;  // 2^54: row-0 LDS sums
 constexpr double kFixInv = 1.0 / 17592186044416.0;
 constexpr float kFixLimit = 32.f;
 
@@ -1115,17 +1116,20 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
       HGX_STAMP(ts[4]);
     }
     // this batch's row-0 gradients: every group adds its record's to the
-    // workgroup's LDS sums as 2^44 fixed point (exact, order-free); the
-    // wave that counts in last adds the sums to the workgroup's slot of
-    // r0acc[q % 3] and stores the loss sum -- no workgroup barrier (the
-    // other waves end as soon as their updates are issued)
+    // workgroup's LDS sums as 2^54 fixed point (exact, order-free; |v| < 32
+    // and at most 8 records keep the sum below 2^62); the wave that counts
+    // in last rounds the sums to the 2^44 units of r0acc, adds them to the
+    // workgroup's slot of r0acc[q % 3] and stores the loss sum -- no
+    // workgroup barrier (the other waves end as soon as their updates are
+    // issued). One 2^-44 rounding per workgroup, as with a float partial.
+    static_assert(RPB <= 8, "LDS fixed-point headroom: 8 records x 2^59");
     {
       const float *zn = &zN.x, *ze = &zE.x;
 #pragma unroll
       for (int e = 0; e < VW; e++) {
         bad |= !(fabsf(zn[e]) < kFixLimit) | !(fabsf(ze[e]) < kFixLimit);
-        atomicAdd(&s_zf[0][lane][e], to_fix(zn[e]));
-        atomicAdd(&s_zf[1][lane][e], to_fix(ze[e]));
+        atomicAdd(&s_zf[0][lane][e], (unsigned long long)__double2ll_rn((double)zn[e] * kFixScaleL));
+        atomicAdd(&s_zf[1][lane][e], (unsigned long long)__double2ll_rn((double)ze[e] * kFixScaleL));
       }
     }
     if (lane == 0) s_loss[grp] = lrec;
@@ -1140,7 +1144,12 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
           r0_row<L, VW>(a, par, blockIdx.x % kR0Slots, 0));
       // the two tables' rows are adjacent in the slot: [2][L][VW] words
 #pragma unroll
-      for (int i = w; i < 2 * L * VW; i += 64) atomicAdd(dst + i, (&s_zf[0][0][0])[i]);
+      for (int i = w; i < 2 * L * VW; i += 64) {
+        const long long v = (long long)(&s_zf[0][0][0])[i];
+        // 2^54 -> 2^44 units, rounded to nearest (ties away from zero)
+        const long long r = v >= 0 ? (v + (1ll << 9)) >> 10 : -((-v + (1ll << 9)) >> 10);
+        atomicAdd(dst + i, (unsigned long long)r);
+      }
       if (w == 0) {
         float sl = 0.f;
         for (int g = 0; g < RPB; g++) sl += s_loss[g];
