@@ -24,7 +24,8 @@ from .hg2v_sample import (AlgebraicDistanceSamples, BooleanSamples,
 from .hg2v_weighting import UniformWeight, WeightByNeighborhood
 from .hg2v_model import (BooleanModel, KerasModelToEmbedding,
                          UnweightedFloatModel)
-from .proto_native import read_incidence, write_embedding
+from .proto_native import (ShardedEmbedding, read_embedding, read_incidence,
+                           save_embedding, write_embedding)
 from .combine_embeddings_util import (CombineEmbeddingsViaConcatenation,
                                       CombineEmbeddingsViaNodeEdgeClassifier)
 from .evaluation_util import (EXPERIMENT_OPTIONS, CalculateCommunityPredictionMetrics,
@@ -53,7 +54,8 @@ __all__ = [
     "CreateRandomHyperGraph", "FromSparseMatrix", "IsEmpty", "ToCsrMatrix",
     "ToEdgeCsrMatrix", "ToCscMatrix", "Relabel", "CompressRange", "Incidence",
     # native proto I/O
-    "read_incidence", "write_embedding",
+    "read_incidence", "write_embedding", "read_embedding", "save_embedding",
+    "ShardedEmbedding",
     # combiners and link-prediction evaluation
     "CombineEmbeddingsViaConcatenation",
     "CombineEmbeddingsViaNodeEdgeClassifier", "EXPERIMENT_OPTIONS",

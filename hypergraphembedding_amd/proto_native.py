@@ -243,6 +243,17 @@ def write_embedding(path, inc, node_tab, edge_tab, method_name,
   return emb.write(path)
 
 
+def save_embedding(path, emb):
+  """Write an embedder's result: a HypergraphEmbedding message to `path`
+  (runner.py:363-364), or a ShardedEmbedding as its shards. Returns the
+  file names."""
+  if isinstance(emb, ShardedEmbedding):
+    return emb.write(path)
+  with open(path, "wb") as f:
+    f.write(emb.SerializeToString())
+  return [str(path)]
+
+
 def embedding_files(path):
   """The files of the embedding at `path`: [path] or its shards in order."""
   path = str(path)
@@ -322,5 +333,6 @@ def _merge(parts):
 
 
 __all__ = ["read_incidence", "write_embedding", "embedding_bytes",
-           "read_embedding", "ShardedEmbedding", "embedding_files",
+           "read_embedding", "save_embedding", "ShardedEmbedding",
+           "embedding_files",
            "message_bytes", "PROTO_LIMIT", "SHARD_BYTES"]

@@ -261,3 +261,24 @@ def test_oversize_embedding_returns_shards(monkeypatch):
   for m in msgs:
     merged.MergeFrom(m)
   assert merged == small
+
+
+def test_save_embedding_either_form(tmp_path, monkeypatch):
+  from hypergraphembedding_amd import proto_native as pn
+  from hypergraphembedding_amd.algebraic_distance import coords_to_embedding
+  hg = CreateRandomHyperGraph(40, 20, 0.3)
+  inc = Incidence.from_hypergraph(hg)
+  rs = np.random.RandomState(2)
+  x = rs.standard_normal((inc.N, 6)).astype(np.float32)
+  y = rs.standard_normal((inc.E, 6)).astype(np.float32)
+  small = coords_to_embedding(inc, x, y, 6, "M")
+  assert pn.save_embedding(str(tmp_path / "a.pb"), small) == [str(tmp_path / "a.pb")]
+  monkeypatch.setattr(pn, "PROTO_LIMIT", 300)
+  monkeypatch.setattr(pn, "SHARD_BYTES", 300)
+  big = coords_to_embedding(inc, x, y, 6, "M")
+  files = pn.save_embedding(str(tmp_path / "b.pb"), big)
+  assert len(files) > 1
+  for name in ("a.pb", "b.pb"):
+    back = pn.read_embedding(str(tmp_path / name))
+    assert back.method_name == "M" and back.dim == 6
+    assert np.array_equal(back.node_tab, x) and np.array_equal(back.edge_tab, y)
