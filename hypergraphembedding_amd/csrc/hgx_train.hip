@@ -568,7 +568,6 @@ __device__ int block_exclusive_scan(int v, int *total, int *s_ws) {
 // below 2^63. A value outside the range (a diverged run, or NaN) raises the
 // step's overflow flag and hgx_train fails with HGX_ENUMERIC.
 constexpr double kFixScale = 17592186044416.0;  // 2^44
-constexpr double kFixScaleL = 18014398509481984.0;  // 2^54: row-0 LDS sums
 constexpr double kFixInv = 1.0 / 17592186044416.0;
 constexpr float kFixLimit = 32.f;
 
@@ -782,15 +781,10 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
   using V = typename S::T;
   static_assert(L == 32 || L == 64, "step geometry");
   static_assert(R + kWX <= 32, "slot and batch words fit the first 32 lanes");
-  // the workgroup's row-0 gradients, fixed point (LDS integer adds, any
-  // order), and the count of waves that added theirs
-  __shared__ unsigned long long s_zf[2][L][VW];
-  __shared__ int s_zn;
+  __shared__ V s_z[2][RPB][L];
   __shared__ V s_gl[RPB][R][L];  // gradients of local (one-record) rows
   __shared__ V s_r0[2][L];
   __shared__ float s_loss[RPB];
-  for (int i = threadIdx.x; i < 2 * L * VW; i += TB) (&s_zf[0][0][0])[i] = 0ull;
-  if (threadIdx.x == 0) s_zn = 0;  // ordered before use by the s_r0 barrier
   unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (g_trace) ts[0] = __builtin_amdgcn_s_memrealtime();
   const int grp = threadIdx.x / L, lane = threadIdx.x % L;
@@ -1115,46 +1109,21 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
       emit(1, S::fma(dz2, Er, S::zero()));
       HGX_STAMP(ts[4]);
     }
-    // this batch's row-0 gradients: every group adds its record's to the
-    // workgroup's LDS sums as 2^54 fixed point (exact, order-free; |v| < 32
-    // and at most 8 records keep the sum below 2^62); the wave that counts
-    // in last rounds the sums to the 2^44 units of r0acc, adds them to the
-    // workgroup's slot of r0acc[q % 3] and stores the loss sum -- no
-    // workgroup barrier (the other waves end as soon as their updates are
-    // issued). One 2^-44 rounding per workgroup, as with a float partial.
-    static_assert(RPB <= 8, "LDS fixed-point headroom: 8 records x 2^59");
-    {
-      const float *zn = &zN.x, *ze = &zE.x;
-#pragma unroll
-      for (int e = 0; e < VW; e++) {
-        bad |= !(fabsf(zn[e]) < kFixLimit) | !(fabsf(ze[e]) < kFixLimit);
-        atomicAdd(&s_zf[0][lane][e], (unsigned long long)__double2ll_rn((double)zn[e] * kFixScaleL));
-        atomicAdd(&s_zf[1][lane][e], (unsigned long long)__double2ll_rn((double)ze[e] * kFixScaleL));
-      }
-    }
+    s_z[0][grp][lane] = zN;
+    s_z[1][grp][lane] = zE;
     if (lane == 0) s_loss[grp] = lrec;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS adds done
-    int last = 0;
-    if ((threadIdx.x & 63) == 0) last = atomicAdd(&s_zn, 1) == TB / 64 - 1;
-    last = __builtin_amdgcn_readfirstlane(last);
-    asm volatile("" ::: "memory");
-    if (last && !(g_tab & 16384)) {  // (debug ablation: no slot adds)
-      const int w = threadIdx.x & 63;
-      unsigned long long *dst = reinterpret_cast<unsigned long long *>(
-          r0_row<L, VW>(a, par, blockIdx.x % kR0Slots, 0));
-      // the two tables' rows are adjacent in the slot: [2][L][VW] words
-#pragma unroll
-      for (int i = w; i < 2 * L * VW; i += 64) {
-        const long long v = (long long)(&s_zf[0][0][0])[i];
-        // 2^54 -> 2^44 units, rounded to nearest (ties away from zero)
-        const long long r = v >= 0 ? (v + (1ll << 9)) >> 10 : -((-v + (1ll << 9)) >> 10);
-        atomicAdd(dst + i, (unsigned long long)r);
-      }
-      if (w == 0) {
-        float sl = 0.f;
-        for (int g = 0; g < RPB; g++) sl += s_loss[g];
-        a.lossbuf[(size_t)gb * a.lstride + blockIdx.x] = sl;
-      }
+    if (!(g_tab & 16384)) __syncthreads();  // (debug ablation: no barrier)
+    // this batch's row-0 gradients: the workgroup's fixed-order sum, added
+    // to its slot of r0acc[q % 3] in fixed point
+    if (threadIdx.x < NC && !(g_tab & 16384)) {
+      V sz = S::zero();
+      for (int g = 0; g < RPB; g++) sz = S::add(sz, s_z[tab0][g][c0]);
+      S::addfix(r0_row<L, VW>(a, par, blockIdx.x % kR0Slots, tab0), c0, sz, bad);
+    }
+    if (threadIdx.x == 0) {
+      float sl = 0.f;
+      for (int g = 0; g < RPB; g++) sl += s_loss[g];
+      a.lossbuf[(size_t)gb * a.lstride + blockIdx.x] = sl;
     }
     // flush slots 1.. (more deferred rows than records in the batch)
     bool more = false;
