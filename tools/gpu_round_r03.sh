@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round evidence: GPU test suite, bench line, rocprofv3 kernel stats of the
+# bench, FETCH/WRITE PMC passes of bench.py (separate runs) summarised per
+# batch step. Usage: tools/gpu_round_r03.sh TAG
+set -o pipefail
+cd "$(dirname "$0")/.." || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r03}
+mkdir -p $O
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread --durations=15 > $O/gpu_tests.log 2>&1 || { echo TESTFAIL; exit 11; }
+echo tests-ok
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKEFAIL; exit 12; }
+echo smoke-ok
+timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || exit 14
+echo bench-ok
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_bench -o run --output-format csv -- python3 bench.py --no-cpu > $O/bench_prof.json 2> $O/bench_prof.err || exit 15
+find $O/prof_bench -name '*stats.csv' -exec cp {} $O/ \;
+rm -rf $O/prof_bench
+echo prof-ok
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 240 rocprofv3 --pmc $C -d $O/pmc_$C -o run --output-format csv -- \
+    python3 bench.py --steps 1 --warmup 0 --no-cpu --no-c4 --no-extra \
+    > $O/pmc_$C.log 2>&1 || { echo "pmc $C failed rc=$?"; exit 16; }
+done
+F=$(find $O/pmc_FETCH_SIZE -name '*counter_collection.csv' | head -1)
+W=$(find $O/pmc_WRITE_SIZE -name '*counter_collection.csv' | head -1)
+python tools/pmc_train_summary.py "$F" "$W" $O/pmc_train.json 128 3 > /dev/null || exit 18
+rm -rf $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE
+bash tools/gpu_r03_mgpu.sh ${1:-r03}_mgpu || exit 19
+echo all-ok
