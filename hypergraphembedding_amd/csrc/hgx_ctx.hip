@@ -133,6 +133,9 @@ extern "C" int hgx_set_tuning(hgx_ctx *ctx, const char *key, int64_t value) {
   } else if (k == "alg_push") {
     HGX_CHECK(ctx, value == 0 || value == 1, HGX_EINVAL, "alg_push must be 0 or 1");
     t.alg_push = (int)value;
+  } else if (k == "mlp_fuse_head") {
+    HGX_CHECK(ctx, value == 0 || value == 1, HGX_EINVAL, "mlp_fuse_head must be 0 or 1");
+    t.mlp_fuse_head = (int)value;
   } else if (k == "alg_ks") {
     HGX_CHECK(ctx, value == 0 || (value % 4 == 0 && value <= 20), HGX_EINVAL,
               "alg_ks must be 0 or a multiple of 4 <= 20");

@@ -57,6 +57,10 @@ struct Tuning {
   // form (the node half writes per-incidence contributions in edge-major
   // order, the edge half streams them; single GPU, k <= 15)
   int alg_push = 0;
+  // combiner MLP training: 1 the label head computed inside the launch that
+  // forms the joint layers' deltas (one launch per batch fewer), 0 its own
+  // launch
+  int mlp_fuse_head = 1;
 };
 
 struct hgx_ctx {

@@ -429,10 +429,13 @@ struct HeadJob {
 // HEAD_KH: inputs of up to 64 * HEAD_KH columns are kept in registers
 constexpr int kHeadKH = 8;
 
-__global__ __launch_bounds__(kThreads) void mlp_head(HeadJob h, Ctx c) {
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  const int mb = blockIdx.x * 32 + w * 8;  // this wave's 8 rows
-  float lsum = 0.f;
+// One wave's 8 rows mb .. mb + 7 of the head. gstore: y, dz4 and dZprev to
+// global memory; S (optional): dZprev also into LDS rows mb - m0 of S (row
+// stride sld floats), every column k < K (rows past M zero). lsum: lane 0's
+// sum of the squared errors of the wave's valid rows, in row order.
+__device__ __forceinline__ void head_wave(const HeadJob &h, const Ctx &c, int mb,
+                                          int lane, bool gstore, float *S, int srow,
+                                          int sld, float &lsum) {
   // Every load is issued, and consumed, before the first store: on this
   // architecture the vector-memory counter also counts stores, so a load
   // waited for after a store waits for that store too. The same arithmetic
@@ -490,47 +493,61 @@ __global__ __launch_bounds__(kThreads) void mlp_head(HeadJob h, Ctx c) {
     dzs[s] = dz;
   }
   // stores
+  if (gstore) {
 #pragma unroll
-  for (int s = 0; s < 8; s++) {
-    const int m = mb + s;
-    if (m < c.M && h.y && lane == 0) h.y[m] = ys[s];
-    if (h.loss && lane == 0) h.dz4[(int64_t)m * h.ld4] = dzs[s];
-  }
-  if (h.loss) {
-    if (regs) {
-#pragma unroll
-      for (int kk = 0; kk < kHeadKH; kk++) {
-        const int k = lane + 64 * kk;
-        if (k < h.K) {
-#pragma unroll
-          for (int s = 0; s < 8; s++) {
-            const int m = mb + s;
-            h.dZprev[(int64_t)m * h.ldp + k] =
-                m < c.M ? dzs[s] * wv[kk] * act_d(h.act_prev, hv[kk][s]) : 0.f;
-          }
-        }
-      }
-    } else {
-      for (int k = lane; k < h.K; k += 64) {
-        const float wk = h.W[(int64_t)k * h.ldw];
-#pragma unroll
-        for (int s = 0; s < 8; s++) {
-          const int m = mb + s;
-          const bool valid = m < c.M;
-          const float hvv = h.H[(int64_t)min(m, c.M - 1) * h.ldh + k];
-          h.dZprev[(int64_t)m * h.ldp + k] =
-              valid ? dzs[s] * wk * act_d(h.act_prev, hvv) : 0.f;
-        }
-      }
+    for (int s = 0; s < 8; s++) {
+      const int m = mb + s;
+      if (m < c.M && h.y && lane == 0) h.y[m] = ys[s];
+      if (h.loss && lane == 0) h.dz4[(int64_t)m * h.ld4] = dzs[s];
     }
   }
   if (!h.loss) return;
+  if (regs) {
+#pragma unroll
+    for (int kk = 0; kk < kHeadKH; kk++) {
+      const int k = lane + 64 * kk;
+      if (k < h.K) {
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+          const int m = mb + s;
+          const float v = m < c.M ? dzs[s] * wv[kk] * act_d(h.act_prev, hv[kk][s]) : 0.f;
+          if (gstore) h.dZprev[(int64_t)m * h.ldp + k] = v;
+          if (S) S[(srow + s) * sld + k] = v;
+        }
+      }
+    }
+  } else {
+    for (int k = lane; k < h.K; k += 64) {
+      const float wk = h.W[(int64_t)k * h.ldw];
+#pragma unroll
+      for (int s = 0; s < 8; s++) {
+        const int m = mb + s;
+        const bool valid = m < c.M;
+        const float hvv = h.H[(int64_t)min(m, c.M - 1) * h.ldh + k];
+        const float v = valid ? dzs[s] * wk * act_d(h.act_prev, hvv) : 0.f;
+        if (gstore) h.dZprev[(int64_t)m * h.ldp + k] = v;
+        if (S) S[(srow + s) * sld + k] = v;
+      }
+    }
+  }
+}
+
+// the workgroup's loss partial: the 4 waves' sums in wave order
+__device__ __forceinline__ void head_partial(const HeadJob &h, const Ctx &c, int slot,
+                                             float lsum) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   __shared__ float wsum[4];
   if (lane == 0) wsum[w] = lsum;
   __syncthreads();
   if (t == 0)
-    h.part[blockIdx.x] =
-        h.lw * (((wsum[0] + wsum[1]) + wsum[2]) + wsum[3]) / (float)c.M;
+    h.part[slot] = h.lw * (((wsum[0] + wsum[1]) + wsum[2]) + wsum[3]) / (float)c.M;
+}
+
+__global__ __launch_bounds__(kThreads) void mlp_head(HeadJob h, Ctx c) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  float lsum = 0.f;
+  head_wave(h, c, blockIdx.x * 32 + w * 8, lane, true, nullptr, 0, 0, lsum);
+  if (h.loss) head_partial(h, c, blockIdx.x, lsum);
 }
 
 // ============================ BWD ==========================================
@@ -550,9 +567,20 @@ struct BwdJob {
   int ldo, Kreal, tiles_n;
 };
 
-template <int NCH>
-__global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c) {
+// FH (fused head, combiner training): term 0's delta rows are the label
+// head's dZprev for rows m0 .. m0 + 31, computed here by head_wave exactly
+// as mlp_head computes them (same arithmetic, same order) into LDS instead of
+// being read from global memory; the first job's k0 = 0 tile of each row
+// block also stores the head's outputs (dZprev, dz4, loss partial) for the
+// weight gradients. Every tile of the row block recomputes the head for its
+// 32 rows: it reads 32 hidden rows instead of 32 delta rows, and the head's
+// own launch goes away.
+constexpr int kHdLd = 256 + 4;  // LDS row stride of the fused head's rows
+
+template <int NCH, bool FH = false>
+__global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c, HeadJob hj) {
   __shared__ __attribute__((aligned(16))) float lds[2][2][32 * 64];
+  __shared__ __attribute__((aligned(16))) float s_hd[FH ? 32 * kHdLd : 4];
   const int qj = find_job(js.start, js.n, blockIdx.x);
   const BwdJob &J = js.j[qj];
   const int tile = blockIdx.x - js.start[qj];
@@ -577,10 +605,27 @@ __global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c) {
       const int r4 = (first ? ch : ch - nch0) * kChunk + q4;
       const float *dr = dz + (int64_t)(oka ? ma : 0) * lddz + r4;
       const float *wr = W + (int64_t)(k0 + row) * ldw + r4;
-      ra0[ch] = *reinterpret_cast<const float4 *>(dr);
-      ra1[ch] = *reinterpret_cast<const float4 *>(dr + 32);
+      if (!(FH && first)) {
+        ra0[ch] = *reinterpret_cast<const float4 *>(dr);
+        ra1[ch] = *reinterpret_cast<const float4 *>(dr + 32);
+      }
       rb0[ch] = *reinterpret_cast<const float4 *>(wr);
       rb1[ch] = *reinterpret_cast<const float4 *>(wr + 32);
+    }
+    if constexpr (FH) {
+      float lsum = 0.f;
+      const bool gst = qj == 0 && k0 == 0;
+      head_wave(hj, c, m0 + w * 8, lane, gst, s_hd, w * 8, kHdLd, lsum);
+      if (gst) head_partial(hj, c, m0 / kTile, lsum);
+      __syncthreads();
+#pragma unroll
+      for (int ch = 0; ch < NCH; ch++) {
+        if (ch < nch0) {
+          const float *sr = s_hd + row * kHdLd + ch * kChunk + q4;
+          ra0[ch] = *reinterpret_cast<const float4 *>(sr);
+          ra1[ch] = *reinterpret_cast<const float4 *>(sr + 32);
+        }
+      }
     }
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -938,24 +983,61 @@ int launch_fwd(hgx_ctx *ctx, const FwdJob *jobs, const int *tiles, int n,
   }
 }
 
-// BWD: every job of the launch with the same total chunk count (2..8)
+// BWD: every job of the launch with the same total chunk count (2..8); hj:
+// the label head fused into this launch (fused_head_ok), else null
+bool fused_head_ok(const HeadJob &h, const BwdJob *jobs, int n) {
+  if (h.K > 256 || h.K % kChunk) return false;
+  for (int q = 0; q < n; q++)
+    if (jobs[q].tm[0].R != h.K) return false;
+  return true;
+}
+
 int launch_bwd(hgx_ctx *ctx, const BwdJob *jobs, const int *tiles, int n,
-               const Ctx &c) {
+               const Ctx &c, const HeadJob *hj = nullptr) {
   auto chunks = [](const BwdJob &j) {
     return j.tm[0].R / kChunk + (j.nt > 1 ? j.tm[1].R / kChunk : 0);
   };
   int nch = n > 0 ? chunks(jobs[0]) : 0;
   for (int q = 1; q < n; q++)
     if (chunks(jobs[q]) != nch) nch = 0;
+  const HeadJob h = hj ? *hj : HeadJob{};
+  auto go = [&](auto kern) {
+    Jobs<BwdJob> js{};
+    js.n = n;
+    int tot = 0;
+    for (int q = 0; q < n; q++) {
+      js.start[q] = tot;
+      js.j[q] = jobs[q];
+      tot += tiles[q];
+    }
+    js.start[n] = tot;
+    if (tot == 0) return HGX_OK;
+    hipLaunchKernelGGL(kern, dim3(tot), dim3(kThreads), 0, ctx->stream, js, c, h);
+    return HGX_OK;
+  };
+  if (hj) {
+    HGX_CHECK(ctx, nch >= 1 && nch <= 8 && fused_head_ok(h, jobs, n), HGX_EINVAL,
+              "fused head: unsupported layer shape");
+    switch (nch) {
+      case 1: return go(mlp_bwd<1, true>);
+      case 2: return go(mlp_bwd<2, true>);
+      case 3: return go(mlp_bwd<3, true>);
+      case 4: return go(mlp_bwd<4, true>);
+      case 5: return go(mlp_bwd<5, true>);
+      case 6: return go(mlp_bwd<6, true>);
+      case 7: return go(mlp_bwd<7, true>);
+      default: return go(mlp_bwd<8, true>);
+    }
+  }
   switch (nch) {
-    case 2: return launch_jobs(ctx, mlp_bwd<2>, jobs, tiles, n, c);
-    case 3: return launch_jobs(ctx, mlp_bwd<3>, jobs, tiles, n, c);
-    case 4: return launch_jobs(ctx, mlp_bwd<4>, jobs, tiles, n, c);
-    case 5: return launch_jobs(ctx, mlp_bwd<5>, jobs, tiles, n, c);
-    case 6: return launch_jobs(ctx, mlp_bwd<6>, jobs, tiles, n, c);
-    case 7: return launch_jobs(ctx, mlp_bwd<7>, jobs, tiles, n, c);
-    case 8: return launch_jobs(ctx, mlp_bwd<8>, jobs, tiles, n, c);
-    default: return launch_jobs(ctx, mlp_bwd<0>, jobs, tiles, n, c);
+    case 2: return go(mlp_bwd<2>);
+    case 3: return go(mlp_bwd<3>);
+    case 4: return go(mlp_bwd<4>);
+    case 5: return go(mlp_bwd<5>);
+    case 6: return go(mlp_bwd<6>);
+    case 7: return go(mlp_bwd<7>);
+    case 8: return go(mlp_bwd<8>);
+    default: return go(mlp_bwd<0>);
   }
 }
 
@@ -1124,7 +1206,13 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
   h.ld4 = L[lb].Np;
   h.y = yout;
   h.part = slot;
-  hipLaunchKernelGGL(mlp_head, dim3(tm), dim3(kThreads), 0, ctx->stream, h, c);
+  // training: the head rides in the joint layers' delta launch below when
+  // its shape allows (tuning mlp_fuse_head)
+  const int nchj = L[hd].Np / kChunk + (ae ? L[m->post_n].Np / kChunk : 0);
+  const bool fuse = train && ctx->tune.mlp_fuse_head && L[lb].Kp <= 256 &&
+                    L[hd].Np == L[lb].Kp && nchj <= 8;
+  if (!fuse)
+    hipLaunchKernelGGL(mlp_head, dim3(tm), dim3(kThreads), 0, ctx->stream, h, c);
   if (!train) return HGX_OK;
   if (ae) {  // reconstruction layers with the loss epilogue
     const int rn = m->rec_n, re = m->rec_e;
@@ -1184,7 +1272,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
       bj[q].tiles_n = NpJ / kTile;
       bt[q] = tiles(jl[q]);
     }
-    HGX_TRY(launch_bwd(ctx, bj, bt, 2, c));
+    HGX_TRY(launch_bwd(ctx, bj, bt, 2, c, fuse ? &h : nullptr));
   }
   {  // dZ of the pre layers
     BwdJob bj[2] = {};

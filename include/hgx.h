@@ -77,6 +77,9 @@ int hgx_synchronize(hgx_ctx *ctx);
  *                      (the node half writes per-incidence contributions in
  *                      edge-major order, the edge half streams them; single
  *                      GPU, k <= 15; measured slower, kept for the record)
+ *   "mlp_fuse_head"    combiner MLP training: 1 the label head computed in
+ *                      the launch forming the joint layers' deltas (default,
+ *                      bit-identical), 0 its own launch
  * Unknown keys and out-of-range values -> HGX_EINVAL. */
 int hgx_set_tuning(hgx_ctx *ctx, const char *key, int64_t value);
 

@@ -92,6 +92,33 @@ def test_fit_bit_exact_c5_widths(ctx):
   m.close()
 
 
+@pytest.mark.parametrize("kind,I,D", [(1, 40, 24), (2, 40, 24), (1, 512, 256)])
+def test_fused_head_equals_head_launch(ctx, kind, I, D):
+  """Combiner training computes the label head inside the launch that forms
+  the joint layers' deltas (tuning mlp_fuse_head, default 1) instead of in
+  its own launch: the trained weights and epoch losses are bit for bit those
+  of the separate head launch (and both equal oracle/mlpref.c above)."""
+  rng, nt, et, nr, er, lab = make_case(kind, I, D, 700, 5)
+  w0 = None
+  res = []
+  for fuse in (1, 0):
+    ctx.set_tuning("mlp_fuse_head", fuse)
+    try:
+      m = _hgx.Mlp(ctx, kind, I, D)
+      if w0 is None:
+        w0 = glorot(m.shapes, np.random.default_rng(2), 0.1)
+      m.set_weights(w0)
+      m.set_tables(nt, et)
+      m.set_samples(nr, er, lab)
+      losses = m.fit(max_epochs=2, min_delta=-1e30, seed=4)
+      res.append((m.get_weights(), np.asarray(losses)))
+      m.close()
+    finally:
+      ctx.set_tuning("mlp_fuse_head", 1)
+  np.testing.assert_array_equal(res[0][0], res[1][0])
+  np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
 def test_small_batches_and_single_sample(ctx):
   m, _, wg, wc, gl, cl = run_both(ctx, 2, 20, 12, 301, 1, batch=100)
   assert np.abs(wg - wc).max() == 0.0
