@@ -701,19 +701,36 @@ __device__ __forceinline__ typename SV<VW>::T *tab_row(const TrainArgs &a, bool 
   return reinterpret_cast<typename SV<VW>::T *>(t) + (size_t)row * L;
 }
 
-// The step's row stores. float2 rows (the d = 128 geometry): write-through,
-// as agent-scope relaxed atomic stores (global_store sc1), so they leave no
-// dirty lines in the XCD's L2 for the kernel-end release to write back:
-// 6.88 -> 6.68 us per batch (d = 128, C3 HOBE records, interleaved A/B,
-// profiles/r03/trainer/ab_wt_*.log). float4 rows (d = 256) stay plain: two
-// 8-byte atomic stores per row piece measured +0.07 us there, and a 16-byte
-// sc1 store has no atomic form the compiler tracks.
+// The step's row stores are write-through (`global_store … sc1`), so the
+// ~57 KB a workgroup writes per batch leaves no dirty lines in its XCD's L2
+// for the kernel-end release to write back. Interleaved A/B against plain
+// stores (profiles/r03/trainer/ab_wt_*.log): d = 128 (float2 rows) 6.88 ->
+// 6.68 us per batch, d = 256 (float4 rows) 8.70 -> 8.49.
+// float2: an agent-scope relaxed atomic store, which is exactly that store.
 __device__ __forceinline__ void st_row(float2 *p, float2 v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long *>(p),
                      __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void st_row(float4 *p, float4 v) { *p = v; }
+// float4: there is no 16-byte atomic store, so the instruction is written
+// out. s_nop 1: the wait states a >8-byte store's data registers need
+// before a VALU may overwrite them (the compiler's hazard check does not see
+// into asm; without it d = 256 training diverged). The "memory" clobber keeps
+// the compiler's memory operations in program order around it; its vmcnt
+// waits only get stricter for an extra store in flight (loads still return
+// in order). HGX_TRAIN_WT4=0 (A/B builds): a plain store.
+#ifndef HGX_TRAIN_WT4
+#define HGX_TRAIN_WT4 1
+#endif
+__device__ __forceinline__ void st_row(float4 *p, float4 v) {
+  if (HGX_TRAIN_WT4) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(x) : "memory");
+  } else {
+    *p = v;
+  }
+}
 
 // one flush entry: the deferred row (table bit 30 | row) of entry m of the
 // previous batch folded and written back
