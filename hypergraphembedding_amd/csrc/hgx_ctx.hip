@@ -87,6 +87,8 @@ extern "C" int hgx_destroy(hgx_ctx *ctx) {
     for (DevBuf *b : {&l->seg, &l->off, &l->rows, &l->part}) hgx_release(*b);
   for (LongRows &l : ctx->long_elr)
     for (DevBuf *b : {&l.seg, &l.off, &l.rows, &l.part}) hgx_release(*b);
+  for (hipStream_t &s : ctx->tstream)
+    if (s) hipStreamDestroy(s);
   if (ctx->ev0) hipEventDestroy(ctx->ev0);
   if (ctx->ev1) hipEventDestroy(ctx->ev1);
   if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
@@ -136,6 +138,12 @@ extern "C" int hgx_set_tuning(hgx_ctx *ctx, const char *key, int64_t value) {
   } else if (k == "mlp_fuse_head") {
     HGX_CHECK(ctx, value == 0 || value == 1, HGX_EINVAL, "mlp_fuse_head must be 0 or 1");
     t.mlp_fuse_head = (int)value;
+  } else if (k == "train_prep_overlap") {
+    HGX_CHECK(ctx, value == 0 || value == 1, HGX_EINVAL, "train_prep_overlap must be 0 or 1");
+    t.train_prep_overlap = (int)value;
+  } else if (k == "train_prep_cus") {
+    HGX_CHECK(ctx, value >= 0 && value <= 128, HGX_EINVAL, "train_prep_cus must be in [0, 128]");
+    t.train_prep_cus = (int)value;
   } else if (k == "alg_ks") {
     HGX_CHECK(ctx, value == 0 || (value % 4 == 0 && value <= 20), HGX_EINVAL,
               "alg_ks must be 0 or a multiple of 4 <= 20");

@@ -61,6 +61,12 @@ struct Tuning {
   // forms the joint layers' deltas (one launch per batch fewer), 0 its own
   // launch
   int mlp_fuse_head = 1;
+  // trainer: chunk c + 1 prepared (train_prep / train_place) on a second
+  // stream while chunk c trains (1), or in line before it (0); with
+  // train_prep_cus > 0 the two streams get disjoint CU masks, that many CUs
+  // for the preparation
+  int train_prep_overlap = 0;
+  int train_prep_cus = 0;
 };
 
 struct hgx_ctx {
@@ -151,6 +157,10 @@ struct hgx_ctx {
 
   // ---- scratch ----
   DevBuf s0, s1, s2, s3, s4, s5, s6, s7;
+  // trainer streams of the overlapped chunk preparation (batch steps,
+  // preparation), created for train_prep_cus = tstream_cus
+  hipStream_t tstream[2] = {nullptr, nullptr};
+  int tstream_cus = -1;
 };
 
 // Diagnostic knobs of the A/B experiments under tools/ (ablations, kernel

@@ -26,10 +26,10 @@
 // as direct launches (or hipGraphs of 64 batches, HGX_GRAPH=1), the
 // chunk-local batch index passed as a kernel argument (no device counters,
 // no dependent index load).
-// Preparation runs once per chunk of up to 1024 batches, on the same stream:
-// overlapping it with training on a second stream measured slower (the
-// per-batch kernels are latency-bound and lose more to the interference
-// than the preparation costs).
+// Preparation runs once per chunk of up to 1024 batches, by default on the
+// same stream before the chunk's batches; tuning train_prep_overlap runs
+// chunk c + 1's on a second stream while chunk c trains (train_prep_cus:
+// disjoint CU masks for the two streams).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -1962,6 +1962,45 @@ extern "C" int hgx_model_get(hgx_ctx *ctx, float *node_tab, float *edge_tab) {
 // ---------------------------------------------------------------------------
 // fit
 // ---------------------------------------------------------------------------
+// The two streams of the overlapped chunk preparation (tuning
+// train_prep_overlap): tstream[0] the batch steps, tstream[1] the
+// preparation. With cus > 0 they get disjoint CU masks: the first `cus`
+// CU-mask bits (rounded up to a multiple of 8) for the preparation, the rest
+// for the steps (which use 64 workgroups per batch): a preparation workgroup
+// never shares a CU with a batch step. Mask bit i is CU i / 8 of XCD i % 8
+// (probed on MI355X, tools/cumask_probe.hip); a mask that leaves an XCD
+// without CUs is ignored by the runtime (the whole device), so each side
+// keeps CUs on every XCD.
+static int train_streams(hgx_ctx *ctx, int cus) {
+  if (ctx->tstream_cus == cus && ctx->tstream[0]) return HGX_OK;
+  for (hipStream_t &s : ctx->tstream) {
+    if (s) {
+      HGX_HIP(ctx, hipStreamSynchronize(s));
+      HGX_HIP(ctx, hipStreamDestroy(s));
+      s = nullptr;
+    }
+  }
+  ctx->tstream_cus = -1;
+  if (cus <= 0) {
+    for (hipStream_t &s : ctx->tstream)
+      HGX_HIP(ctx, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  } else {
+    int ncu = 0;
+    HGX_HIP(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount,
+                                       ctx->device));
+    HGX_CHECK(ctx, cus <= ncu / 2, HGX_EINVAL, "train_prep_cus %d above half of %d CUs",
+              cus, ncu);
+    const int W = (ncu + 31) / 32;
+    std::vector<uint32_t> ms(W, 0u), mp(W, 0u);
+    const int np = (cus + 7) / 8 * 8;
+    for (int i = 0; i < ncu; i++) (i < np ? mp : ms)[i / 32] |= 1u << (i % 32);
+    HGX_HIP(ctx, hipExtStreamCreateWithCUMask(&ctx->tstream[0], W, ms.data()));
+    HGX_HIP(ctx, hipExtStreamCreateWithCUMask(&ctx->tstream[1], W, mp.data()));
+  }
+  ctx->tstream_cus = cus;
+  return HGX_OK;
+}
+
 extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
                          float eps, int loss, int act, float min_delta,
                          uint64_t shuffle_seed, const int64_t *perms,
@@ -2091,9 +2130,13 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   const size_t inv_n = (size_t)CB * SB + (size_t)RPB * R * 2 + 64;
   const size_t pg = fused ? (size_t)CB * NBF * prpb : 0;  // placed groups
   // step buffers: pfo, pidx, pcode, ptgt, scode, skey [2], sM [2], pbrk
+  // (with the overlapped preparation the placed buffers pfo, pidx, pcode,
+  // ptgt, pbrk twice: chunk c + 1 is placed while chunk c trains)
+  const bool overlap = fused && ctx->tune.train_prep_overlap == 1;
+  const size_t placed_ints = 2 * (size_t)CB * Mmax + pg * RW * 2 + pg * 3 + (size_t)CB + 2;
   const size_t step_ints = fused ? 2 * (size_t)CB * Mmax + pg * RW * 2 + pg * 3 +
                                        (size_t)CB * SB + 2 * (size_t)CB * Mmax +
-                                       3 * (size_t)CB + 64
+                                       3 * (size_t)CB + 64 + (overlap ? placed_ints : 0)
                                  : 0;
   const size_t prep_ints = bidx_n + btgt_n + inv_n + (size_t)CB * SB +
                            (size_t)CB * (SB + 1) + CB + 2 * CB + 64 + step_ints;
@@ -2189,7 +2232,23 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
         q += CB;
       }
       a.pbrk = q;
+      q += CB;
     }
+  }
+  // placed-buffer sets by chunk parity (one set unless overlapped)
+  TrainArgs ap[2] = {a, a};
+  if (overlap) {
+    int *q = ap[0].pbrk + CB;
+    q += ((uintptr_t)q / sizeof(int)) % 2;  // 8-B align (pfo)
+    ap[1].pfo = reinterpret_cast<int2 *>(q);
+    q += 2 * (size_t)CB * Mmax;
+    ap[1].pidx = q;
+    q += pg * RW;
+    ap[1].pcode = reinterpret_cast<unsigned *>(q);
+    q += pg * RW;
+    ap[1].ptgt = reinterpret_cast<float *>(q);
+    q += pg * 3;
+    ap[1].pbrk = q;
   }
   double *dloss = reinterpret_cast<double *>(ctx->s6.as<char>() + 32);
   double *dpart = reinterpret_cast<double *>(ctx->s6.as<char>() + 64);
@@ -2222,7 +2281,18 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     }
     int *hbrk = nullptr;  // pinned: the chunk's MULTI flags (train_place)
   } res;
-  if (fused) HGX_HIP(ctx, hipHostMalloc(reinterpret_cast<void **>(&res.hbrk), sizeof(int) * CB));
+  if (fused)
+    HGX_HIP(ctx, hipHostMalloc(reinterpret_cast<void **>(&res.hbrk),
+                               sizeof(int) * CB * (overlap ? 2 : 1)));
+  // overlapped preparation: the batch-step stream and the preparation stream
+  // (disjoint CU masks when train_prep_cus > 0), ordered after everything
+  // queued on ctx->stream so far and joined back into it at the end
+  hipStream_t sst = ctx->stream, spr = ctx->stream;
+  if (overlap) {
+    HGX_TRY(train_streams(ctx, ctx->tune.train_prep_cus));
+    sst = ctx->tstream[0];
+    spr = ctx->tstream[1];
+  }
   // Direct launches by default: measured as fast as hipGraph replay of the
   // same kernels (10.6 us per batch both ways at d=128) with less host time,
   // and rocprofv3 kernel tracing crashes on the replays. HGX_GRAPH=1 replays
@@ -2253,6 +2323,13 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   std::vector<hipEvent_t> bev(2 * nchunks);
   for (auto &e : bev) {
     HGX_HIP(ctx, hipEventCreate(&e));
+    res.ev.push_back(e);
+  }
+  // overlapped preparation: chunk c prepared (pev[c]), the epoch's join
+  // with ctx->stream (pev[nchunks]); timing off
+  std::vector<hipEvent_t> pev(overlap ? nchunks + 1 : 0);
+  for (auto &e : pev) {
+    HGX_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     res.ev.push_back(e);
   }
   const size_t prep_smem = (size_t)P * (sizeof(unsigned long long) + sizeof(int));
@@ -2314,7 +2391,53 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     if (fused)
       (void)hipMemsetAsync(a.r0acc, 0, sizeof(float) * gp_f, ctx->stream);
     int last_nbc = 0;
-    for (int64_t c = 0; c < nchunks; c++) {
+    if (overlap) {
+      // chunk c + 1 prepared on spr while chunk c trains on sst; placed set
+      // c & 1 is rewritten (chunk c + 2) only after chunk c's steps are done
+      hipEvent_t ej = pev[nchunks];
+      (void)hipEventRecord(ej, ctx->stream);
+      (void)hipStreamWaitEvent(sst, ej, 0);
+      (void)hipStreamWaitEvent(spr, ej, 0);
+      auto prep_ov = [&](int64_t c) {
+        const int nbc = (int)std::min<int64_t>(CB, nbatches - c * CB);
+        const int cp = (int)(c & 1);
+        if (c >= 2) (void)hipStreamWaitEvent(spr, bev[2 * (c - 2) + 1], 0);
+        hipLaunchKernelGGL(train_prep, dim3(CB), dim3(kTB), prep_smem, spr, a, c * CB, nbc, P,
+                           skey[cp], sM[cp]);
+        hipLaunchKernelGGL(train_place, dim3(CB), dim3(kTB), place_smem, spr, ap[cp], nbc, CB,
+                           skey[cp], sM[cp], skey[cp ^ 1], sM[cp ^ 1], c > 0 ? 1 : 0);
+        (void)hipMemcpyAsync(res.hbrk + (size_t)cp * CB, ap[cp].pbrk, sizeof(int) * nbc,
+                             hipMemcpyDeviceToHost, spr);
+        (void)hipEventRecord(pev[c], spr);
+      };
+      prep_ov(0);
+      for (int64_t c = 0; c < nchunks; c++) {
+        const int64_t base = c * CB;
+        const int nbc = (int)std::min<int64_t>(CB, nbatches - base);
+        const int cp = (int)(c & 1);
+        if (c + 1 < nchunks) prep_ov(c + 1);
+        if (hipEventSynchronize(pev[c]) != hipSuccess) {
+          rc = hgx_fail(ctx, HGX_EHIP, "batch preparation failed: %s",
+                        hipGetErrorString(hipGetLastError()));
+          break;
+        }
+        (void)hipStreamWaitEvent(sst, pev[c], 0);
+        (void)hipEventRecord(bev[2 * c], sst);
+        const int *hb = res.hbrk + (size_t)cp * CB;
+        for (int b = 0; b < nbc; b++) {
+          const int64_t gbat = base + b;
+          const int nrec = (int)std::min<int64_t>(batch, n - gbat * batch);
+          const int multi = hb[b] && gbat > 0;
+          nmulti += multi;
+          hipLaunchKernelGGL(kf[multi], dim3(NBF), dim3(tbf), 0, sst, ap[cp], b, (int)gbat,
+                             nrec, (int)gbat);
+        }
+        nfused += nbc;
+        (void)hipEventRecord(bev[2 * c + 1], sst);
+        last_nbc = nbc;
+      }
+    }
+    for (int64_t c = 0; c < nchunks && !overlap; c++) {
       const int64_t base = c * CB;
       const int nbc = (int)std::min<int64_t>(CB, nbatches - base);
       prep_chunk(c, nbc);
@@ -2365,21 +2488,21 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
       const int *mp = last_nbc >= 2 ? sM[cp] + (last_nbc - 2)
                                     : (nchunks >= 2 ? sM[cp ^ 1] + (CB - 1) : nullptr);
       const int nlast = (int)(n - (nbatches - 1) * batch);
-      hipLaunchKernelGGL(kfl, dim3(64), dim3(256), 0, ctx->stream, a,
+      hipLaunchKernelGGL(kfl, dim3(64), dim3(256), 0, sst, a,
                          skey[cp] + (size_t)(last_nbc - 1) * Mmax, ml, mp,
                          (int)(nbatches - 1), std::min(NBF, nlast));
     }
     hipLaunchKernelGGL(loss_partial, dim3(kLossBlocks), dim3(kTB), 0,
-                       ctx->stream, a.lossbuf, nbatches * lstride, dpart);
-    hipLaunchKernelGGL(loss_final, dim3(1), dim3(kLossBlocks), 0, ctx->stream,
+                       sst, a.lossbuf, nbatches * lstride, dpart);
+    hipLaunchKernelGGL(loss_final, dim3(1), dim3(kLossBlocks), 0, sst,
                        dpart, dloss);
     double lsum = 0.0;
     int ovf = 0;
     if (hipMemcpyAsync(&lsum, dloss, sizeof(double), hipMemcpyDeviceToHost,
-                       ctx->stream) != hipSuccess ||
+                       sst) != hipSuccess ||
         (fused && hipMemcpyAsync(&ovf, a.ovf, sizeof(int), hipMemcpyDeviceToHost,
-                                 ctx->stream) != hipSuccess) ||
-        hipStreamSynchronize(ctx->stream) != hipSuccess) {
+                                 sst) != hipSuccess) ||
+        hipStreamSynchronize(sst) != hipSuccess) {
       rc = hgx_fail(ctx, HGX_EHIP, "epoch failed: %s",
                     hipGetErrorString(hipGetLastError()));
       break;
@@ -2405,6 +2528,11 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
       ep++;
       break;
     }
+  }
+  if (overlap) {
+    // join: nothing of this call is left running on the side streams
+    (void)hipStreamSynchronize(spr);
+    (void)hipStreamSynchronize(sst);
   }
   hipEventRecord(ctx->ev1, ctx->stream);
   hipEventSynchronize(ctx->ev1);

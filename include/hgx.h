@@ -80,6 +80,12 @@ int hgx_synchronize(hgx_ctx *ctx);
  *   "mlp_fuse_head"    combiner MLP training: 1 the label head computed in
  *                      the launch forming the joint layers' deltas (default,
  *                      bit-identical), 0 its own launch
+ *   "train_prep_overlap" trainer: 1 prepare chunk c + 1 (train_prep /
+ *                      train_place) on a second stream while chunk c trains,
+ *                      0 in line before each chunk (default); the same
+ *                      batches, bit for bit
+ *   "train_prep_cus"   with train_prep_overlap: CUs reserved for the
+ *                      preparation stream by disjoint CU masks (0 = no masks)
  * Unknown keys and out-of-range values -> HGX_EINVAL. */
 int hgx_set_tuning(hgx_ctx *ctx, const char *key, int64_t value);
 

@@ -312,3 +312,39 @@ def test_step_diverged_gradients_raise(ctx):
   with pytest.raises(FloatingPointError):
     ctx.train(batch=256, max_epochs=1, loss=O.LOSS_MSE, act=O.ACT_RELU,
               perms=np.arange(idx.shape[0])[None, :])
+
+
+@pytest.mark.parametrize("cus", [0, 32])
+def test_overlapped_preparation_bitwise_equal(ctx, cus):
+  """Chunk c + 1 prepared on a second stream while chunk c trains (tuning
+  train_prep_overlap; train_prep_cus: disjoint CU masks) gives the in-line
+  preparation's tables and losses bit for bit. 2,100 batches = three chunks
+  of up to 1,024 (both placed-buffer sets used, one reused), hub batches on
+  both chunk boundaries (deferred rows and MULTI batches across chunks),
+  device shuffle in-order first epoch, then shuffled."""
+  rs = np.random.RandomState(5)
+  K, B, nb = 5, 256, 2100
+  idx, tgt = _mixed_reuse_records(rs, nb, B, K,
+                                  hub_batches={1022, 1023, 1024, 2047, 2048})
+  idx, tgt = idx[:-100], tgt[:-100]
+  perms = np.stack([np.arange(idx.shape[0]), rs.permutation(idx.shape[0])])
+  ctx.records_set(idx, tgt)
+  out = []
+  try:
+    for ov in (0, 1):
+      ctx.set_tuning("train_prep_overlap", ov)
+      ctx.set_tuning("train_prep_cus", cus)
+      ctx.model_init(128, 20002, 20002, seed=9)
+      gl = ctx.train(batch=B, max_epochs=2, loss=O.LOSS_MSE, act=O.ACT_RELU,
+                     perms=perms, min_delta=-1.0)
+      out.append(ctx.model_get() + (gl, ctx.train_path_stats(),
+                                    ctx.train_multi_pending()))
+  finally:
+    ctx.set_tuning("train_prep_overlap", 0)
+    ctx.set_tuning("train_prep_cus", 0)
+  assert out[0][3] == (2 * nb, 0), out[0][3]
+  assert out[0][4] > 0
+  assert out[0][3:] == out[1][3:]
+  assert np.array_equal(out[0][2], out[1][2]), (out[0][2], out[1][2])
+  assert np.array_equal(out[0][0], out[1][0])
+  assert np.array_equal(out[0][1], out[1][1])

@@ -4,11 +4,15 @@ its own context with the same records and model; epochs alternate A, B, ...
 and the per-batch device time (hgx_train_last_stats) is reported per build as
 min / median over rounds. Diagnostic only.
 
-  python tools/ab_train.py D {rand|hobe} lib1.so lib2.so ...
+  python tools/ab_train.py D {rand|hobe} lib1.so[:key=v,key=v] lib2.so ...
+
+Also the whole hgx_train call's wall rate (records / s, preparation and host
+waits included) per build.
 """
 import ctypes
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -19,7 +23,7 @@ kind = sys.argv[2]
 libs = sys.argv[3:]
 N, E, K = 100000, 50000, 5
 R = 4 + 2 * K
-n = 2_000_000
+n = int(os.environ.get("AB_N", 2_000_000))
 rs = np.random.RandomState(0)
 if kind == "hobe":
   from hypergraphembedding_amd import _hgx
@@ -64,8 +68,8 @@ for spec in libs:
                                      ctypes.POINTER(ctypes.c_int64)]
   h = vp()
   assert L.hgx_create(0, ctypes.byref(h)) == 0
-  if tune:
-    key, val = tune.split("=")
+  for kv in filter(None, tune.split(",")):  # lib.so:k=v,k=v
+    key, val = kv.split("=")
     L.hgx_set_tuning.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
     assert L.hgx_set_tuning(h, key.encode(), int(val)) == 0
   assert L.hgx_records_set(h, n, K, idx.ctypes.data, tgt.ctypes.data) == 0
@@ -75,14 +79,19 @@ for spec in libs:
 loss = np.zeros(1, np.float32)
 ran = ctypes.c_int()
 res = [[] for _ in libs]
+wall = [[] for _ in libs]
 for rnd in range(6):
   for i, (L, h) in enumerate(hs):
+    t0 = time.perf_counter()
     assert L.hgx_train(h, 256, 1, 0.01, 1e-7, 1, 1, -1e30, rnd, None,
                        loss.ctypes.data, ctypes.byref(ran)) == 0
+    if rnd > 0:
+      wall[i].append(n / (time.perf_counter() - t0))
     ms, rec, bat = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
     L.hgx_train_last_stats(h, ctypes.byref(ms), ctypes.byref(rec), ctypes.byref(bat))
     if rnd > 0:
       res[i].append(ms.value * 1e3 / bat.value)
-for path, r in zip(libs, res):
-  print(f"{kind} d={d} {os.path.basename(path):>28s}: us/batch min {min(r):.3f} "
-        f"median {np.median(r):.3f}")
+for path, r, w in zip(libs, res, wall):
+  print(f"{kind} d={d} {os.path.basename(path):>40s}: us/batch min {min(r):.3f} "
+        f"median {np.median(r):.3f}; epoch wall {np.median(w) / 1e6:.2f}M records/s "
+        f"(max {max(w) / 1e6:.2f}M)")
