@@ -1472,6 +1472,11 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
     if (threadIdx.x == 0) a.bmeta[cb] = make_int2(0, 0);
     return;
   }
+  // (diagnostic phase trace: the first chunk's workgroups in trace slot
+  // [batch 0][kernel 1][cb], stamps: start, ids, slot gathers, sort, unique
+  // runs, codes)
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (g_trace) ts[0] = __builtin_amdgcn_s_memrealtime();
   const int64_t r0 = (base + cb) * a.B;
   const int nb = (int)min((int64_t)a.B, a.n - r0);
   if (threadIdx.x == 0) a.bmeta[cb] = make_int2(nb, (int)(base + cb));
@@ -1484,6 +1489,7 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
   __shared__ int s_perm[kPrepB];
   for (int i = threadIdx.x; i < nb; i += kTB) s_perm[i] = a.perm[r0 + i];
   __syncthreads();
+  HGX_STAMP(ts[1]);
   for (int t = threadIdx.x; t < nb * 3; t += kTB) {
     const int i = t / 3;
     btgt[t] = a.tgt[(int64_t)s_perm[i] * 3 + (t - 3 * i)];
@@ -1512,6 +1518,7 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
     }
   }
   __syncthreads();
+  HGX_STAMP(ts[2]);
   for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int t = threadIdx.x; t < P / 2; t += kTB) {
@@ -1527,6 +1534,7 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
       __syncthreads();
     }
   }
+  HGX_STAMP(ts[3]);
   // unique starts over a contiguous chunk per thread, then one block scan
   const int per = P / kTB;
   const int t0 = threadIdx.x * per;
@@ -1544,22 +1552,27 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
   int *ukey = a.ukey + (size_t)cb * a.SB;
   int *uoff = a.uoff + (size_t)cb * (a.SB + 1);
   int *inv = a.inv + (size_t)cb * a.SB;
+  // (slot positions and run offsets feed the two-kernel step only)
+  const bool split = !a.fused;
   for (int t = t0; t < t0 + per; t++) {
     const unsigned long long x = s_key[t];
     if (x == ~0ull) break;
-    inv[x & 0xffffffffu] = t;
+    if (split) inv[x & 0xffffffffu] = t;
     if (t == 0 || (unsigned)(s_key[t - 1] >> 32) != (unsigned)(x >> 32)) {
       ukey[u] = (int)(x >> 32);
-      uoff[u] = t;
+      if (split) uoff[u] = t;
       u++;
     }
   }
   if (threadIdx.x == 0) {
-    uoff[U] = V;
+    if (split) uoff[U] = V;
     a.ucount[cb] = U;
   }
+  HGX_STAMP(ts[4]);
   if (a.fused)
     defer_codes(a, cb, V, P, u0, s_key, s_ws, reinterpret_cast<int *>(s_key + P), skey, sM);
+  HGX_STAMP(ts[5]);
+  if (g_trace && base == 0) trace_put(0, 1, 6, ts);
 }
 
 // deterministic two-level sum of the chunk's per-block losses:
@@ -2398,10 +2411,13 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
       (void)hipEventRecord(ej, ctx->stream);
       (void)hipStreamWaitEvent(sst, ej, 0);
       (void)hipStreamWaitEvent(spr, ej, 0);
+      // The host enqueues chunk c + 1's preparation only once chunk c - 1's
+      // steps are done (it waits for them after queueing chunk c's), so the
+      // preparation stream never holds a barrier packet blocked on the step
+      // stream.
       auto prep_ov = [&](int64_t c) {
         const int nbc = (int)std::min<int64_t>(CB, nbatches - c * CB);
         const int cp = (int)(c & 1);
-        if (c >= 2) (void)hipStreamWaitEvent(spr, bev[2 * (c - 2) + 1], 0);
         hipLaunchKernelGGL(train_prep, dim3(CB), dim3(kTB), prep_smem, spr, a, c * CB, nbc, P,
                            skey[cp], sM[cp]);
         hipLaunchKernelGGL(train_place, dim3(CB), dim3(kTB), place_smem, spr, ap[cp], nbc, CB,
@@ -2415,7 +2431,6 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
         const int64_t base = c * CB;
         const int nbc = (int)std::min<int64_t>(CB, nbatches - base);
         const int cp = (int)(c & 1);
-        if (c + 1 < nchunks) prep_ov(c + 1);
         if (hipEventSynchronize(pev[c]) != hipSuccess) {
           rc = hgx_fail(ctx, HGX_EHIP, "batch preparation failed: %s",
                         hipGetErrorString(hipGetLastError()));
@@ -2435,6 +2450,15 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
         nfused += nbc;
         (void)hipEventRecord(bev[2 * c + 1], sst);
         last_nbc = nbc;
+        if (c + 1 < nchunks) {
+          // placed set (c + 1) & 1 is free once chunk c - 1's steps are done
+          if (c >= 1 && hipEventSynchronize(bev[2 * (c - 1) + 1]) != hipSuccess) {
+            rc = hgx_fail(ctx, HGX_EHIP, "batch step failed: %s",
+                          hipGetErrorString(hipGetLastError()));
+            break;
+          }
+          prep_ov(c + 1);
+        }
       }
     }
     for (int64_t c = 0; c < nchunks && !overlap; c++) {

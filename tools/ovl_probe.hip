@@ -102,7 +102,8 @@ int main(int argc, char **argv) {
   for (auto &e : bev) CK(hipEventCreate(&e));
   for (auto &e : pev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 
-  auto run = [&](const char *name, int mode, bool copy, bool prep, bool wait) {
+  auto run = [&](const char *name, int mode, bool copy, bool prep, bool wait,
+                 bool pwait = true) {
     CK(hipDeviceSynchronize());
     const auto t0 = std::chrono::steady_clock::now();
     double steps_ms = 0;
@@ -120,7 +121,8 @@ int main(int argc, char **argv) {
     } else {
       auto prep_ov = [&](int c) {
         const int cp = c & 1;
-        if (c >= 2) CK(hipStreamWaitEvent(P, bev[2 * (c - 2) + 1], 0));
+        if (c >= 2 && pwait) CK(hipStreamWaitEvent(P, bev[2 * (c - 2) + 1], 0));
+        if (c >= 2 && !pwait) CK(hipEventSynchronize(bev[2 * (c - 2) + 1]));
         if (prep) hipLaunchKernelGGL(prepk, dim3(1024), dim3(256), 0, P, po, dflags + cp * CB);
         if (copy)
           CK(hipMemcpyAsync(hflags + cp * CB, dflags + cp * CB, 4 * CB, hipMemcpyDeviceToHost, P));
@@ -164,6 +166,7 @@ int main(int argc, char **argv) {
     run("ovl-nocopy", 1, false, true, true);
     run("ovl-noprep", 1, true, false, true);
     run("ovl-nowait", 1, true, true, false);
+    run("ovl-no-prep-stream-wait", 1, true, true, true, false);
     run("inline", 0, true, true, true);
   }
   return 0;

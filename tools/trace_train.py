@@ -47,6 +47,16 @@ print(f"{extra} {ms * 1e3 / bat:.2f} us/batch (traced run)")
 t = np.fromfile(path, np.uint64).reshape(256, 2, 1024, 8).astype(np.int64)
 print("path (fused, split):", ctx.train_path_stats())
 if ctx.train_path_stats()[0] > 0:
+  # chunk preparation (train_prep of the first chunk: kern slot 1 of batch 0)
+  pp = t[0, 1][t[0, 1, :, 0] > 0][:, :6]
+  if len(pp):
+    dd = np.diff(pp, axis=1) * 0.01
+    print(f"train_prep chunk 0: {len(pp)} workgroups, span {(pp[:, 5].max() - pp[:, 0].min()) * 0.01:.1f} us, "
+          f"per-WG median total {np.median(pp[:, 5] - pp[:, 0]) * 0.01:.2f} us")
+    print("  per-WG median: ids %.2f slot gathers %.2f sort %.2f unique %.2f codes %.2f" %
+          tuple(np.median(dd, axis=0)))
+    print("  per-WG max:    ids %.2f slot gathers %.2f sort %.2f unique %.2f codes %.2f" %
+          tuple(np.max(dd, axis=0)))
   # fused step: kern slot 0 only, stamps start, ids, gathers+row0, compute,
   # emits, multi rows, end
   rows = []
