@@ -31,6 +31,7 @@
 // chunk c + 1's on a second stream while chunk c trains (train_prep_cus:
 // disjoint CU masks for the two streams).
 #include <hipcub/hipcub.hpp>
+#include <rocprim/block/block_radix_sort.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -141,6 +142,7 @@ constexpr int kWX = kFX + 2;                // + batch words: overflow flushes,
                                             //   gacc entries to zero
 constexpr int kPackB = 512;                 // max records per step batch
 constexpr int kPrepB = 1366;  // max records per prepared batch: 8192 slots / R >= 6
+constexpr int kSortP = 4096;  // prepared-batch slot count sorted by block radix sort
 
 __device__ __forceinline__ bool slot_is_edge(int s, int K) {
   return s == 1 || s == 3 || s >= 4 + K;
@@ -805,6 +807,12 @@ __device__ __forceinline__ void row0_finish(const TrainArgs &a, int q,
 // records per workgroup, ceil(B / RPB) workgroups; records placed by
 // train_place, those without neighbour lists first (whole waves skip the list
 // gathers).
+// HGX_TRAIN_R0EARLY (A/B builds): every record group adds its own row-0
+// gradients to the fixed-point slot right after its forward pass, before its
+// row stores, and stores its own loss: no end-of-batch workgroup barrier.
+#ifndef HGX_TRAIN_R0EARLY
+#define HGX_TRAIN_R0EARLY 0
+#endif
 template <int L, int VW, int KMAX, int MODE, int TB, bool MULTI>
 __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, int nb, int q) {
   constexpr int RPB = TB / L, R = 4 + 2 * KMAX, K = KMAX, NC = 2 * L;
@@ -812,6 +820,9 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
   using V = typename S::T;
   static_assert(L == 32 || L == 64, "step geometry");
   static_assert(R + kWX <= 32, "slot and batch words fit the first 32 lanes");
+  // early row-0 sums at float2 rows only (at float4 rows, d = 256, the 4x
+  // integer atomics cost more than the barrier: 8.49 -> 10.42 us per batch)
+  constexpr bool kR0E = HGX_TRAIN_R0EARLY && VW == 2;
   __shared__ V s_z[2][RPB][L];
   __shared__ V s_gl[RPB][R][L];  // gradients of local (one-record) rows
   __shared__ V s_r0[2][L];
@@ -1088,8 +1099,10 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
         const unsigned cd = code[s];
         const bool edge = slot_is_edge(s, K);
         if (row[s] == 0) {
-          if (edge) zE = S::add(zE, g);
-          else zN = S::add(zN, g);
+          if (!kR0E) {
+            if (edge) zE = S::add(zE, g);
+            else zN = S::add(zN, g);
+          }
         } else if (cd & kSLocal) {
           // one record's slots of a row, summed in emit order in LDS (the
           // wave's own accesses, in order); the last one (owner) updates
@@ -1125,14 +1138,42 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
         }
       };
       V gln = S::fma(dz1, Nr, S::zero()), gre = S::fma(dz2, El, S::zero());
+      if (kR0E) {
+        // the row-0 sums in emit order first (the same adds as below), added
+        // to this record's slot before any row store
+        float da[K], db[K];
 #pragma unroll
-      for (int k = 0; k < K; k++) {
-        const float da = dP * act_d(act, za[k], sa[k]);
-        const float db = dQ * act_d(act, zb[k], sb[k]);
-        gln = S::fma(da, Pv[4 + k], gln);
-        gre = S::fma(db, Pv[4 + K + k], gre);
-        emit(4 + k, S::fma(da, Nl, S::zero()));
-        emit(4 + K + k, S::fma(db, Er, S::zero()));
+        for (int k = 0; k < K; k++) {
+          da[k] = dP * act_d(act, za[k], sa[k]);
+          db[k] = dQ * act_d(act, zb[k], sb[k]);
+          gln = S::fma(da[k], Pv[4 + k], gln);
+          gre = S::fma(db[k], Pv[4 + K + k], gre);
+          if (row[4 + k] == 0) zN = S::add(zN, S::fma(da[k], Nl, S::zero()));
+          if (row[4 + K + k] == 0) zE = S::add(zE, S::fma(db[k], Er, S::zero()));
+        }
+        if (row[0] == 0) zN = S::add(zN, gln);
+        if (row[3] == 0) zE = S::add(zE, gre);
+        if (row[2] == 0) zN = S::add(zN, S::fma(dz1, Nl, S::zero()));
+        if (row[1] == 0) zE = S::add(zE, S::fma(dz2, Er, S::zero()));
+        const int slot = (blockIdx.x * RPB + grp) % kR0Slots;
+        S::addfix(r0_row<L, VW>(a, par, slot, 0), lane, zN, bad);
+        S::addfix(r0_row<L, VW>(a, par, slot, 1), lane, zE, bad);
+        if (lane == 0) a.lossbuf[(size_t)gb * a.lstride + blockIdx.x * RPB + grp] = lrec;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+          emit(4 + k, S::fma(da[k], Nl, S::zero()));
+          emit(4 + K + k, S::fma(db[k], Er, S::zero()));
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+          const float da = dP * act_d(act, za[k], sa[k]);
+          const float db = dQ * act_d(act, zb[k], sb[k]);
+          gln = S::fma(da, Pv[4 + k], gln);
+          gre = S::fma(db, Pv[4 + K + k], gre);
+          emit(4 + k, S::fma(da, Nl, S::zero()));
+          emit(4 + K + k, S::fma(db, Er, S::zero()));
+        }
       }
       emit(0, gln);
       emit(3, gre);
@@ -1140,21 +1181,23 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
       emit(1, S::fma(dz2, Er, S::zero()));
       HGX_STAMP(ts[4]);
     }
-    s_z[0][grp][lane] = zN;
-    s_z[1][grp][lane] = zE;
-    if (lane == 0) s_loss[grp] = lrec;
-    if (!(g_tab & 16384)) __syncthreads();  // (debug ablation: no barrier)
-    // this batch's row-0 gradients: the workgroup's fixed-order sum, added
-    // to its slot of r0acc[q % 3] in fixed point
-    if (threadIdx.x < NC && !(g_tab & 16384)) {
-      V sz = S::zero();
-      for (int g = 0; g < RPB; g++) sz = S::add(sz, s_z[tab0][g][c0]);
-      S::addfix(r0_row<L, VW>(a, par, blockIdx.x % kR0Slots, tab0), c0, sz, bad);
-    }
-    if (threadIdx.x == 0) {
-      float sl = 0.f;
-      for (int g = 0; g < RPB; g++) sl += s_loss[g];
-      a.lossbuf[(size_t)gb * a.lstride + blockIdx.x] = sl;
+    if (!kR0E) {
+      s_z[0][grp][lane] = zN;
+      s_z[1][grp][lane] = zE;
+      if (lane == 0) s_loss[grp] = lrec;
+      if (!(g_tab & 16384)) __syncthreads();  // (debug ablation: no barrier)
+      // this batch's row-0 gradients: the workgroup's fixed-order sum, added
+      // to its slot of r0acc[q % 3] in fixed point
+      if (threadIdx.x < NC && !(g_tab & 16384)) {
+        V sz = S::zero();
+        for (int g = 0; g < RPB; g++) sz = S::add(sz, s_z[tab0][g][c0]);
+        S::addfix(r0_row<L, VW>(a, par, blockIdx.x % kR0Slots, tab0), c0, sz, bad);
+      }
+      if (threadIdx.x == 0) {
+        float sl = 0.f;
+        for (int g = 0; g < RPB; g++) sl += s_loss[g];
+        a.lossbuf[(size_t)gb * a.lstride + blockIdx.x] = sl;
+      }
     }
     // flush slots 1.. (more deferred rows than records in the batch)
     bool more = false;
@@ -1313,6 +1356,137 @@ __device__ void defer_codes(const TrainArgs &a, int cb, int V, int P, int u0,
       code = kSLocal | (last ? kSOwn : 0u) | (first ? kSFirst : 0u) | (unsigned)own;
     }
     sc[slot(t)] = code;
+  }
+  if (threadIdx.x == 0) sM[cb] = S;
+}
+
+// The unique-key and slot-code phases of train_prep for the radix-sorted
+// batch (P == kSortP), from the sort's registers: thread t holds sorted
+// positions [t * PER, t * PER + PER) (keys kk, slots vv), the same chunk the
+// generic path scans in LDS. Run starts, run ends (the last slot of the run
+// by a backward pass over the chunk; a run leaving the chunk is followed in
+// LDS) and the run classes stay in registers, every array indexed at compile
+// time; local runs (rare) use the generic LDS scan. Same outputs as the
+// generic unique phase + defer_codes, bit for bit.
+template <int PER>
+__device__ void prep_runs_regs(const TrainArgs &a, int cb, int P, const unsigned (&kk)[PER],
+                               const int (&vv)[PER], const unsigned long long *s_key, int *s_ws,
+                               unsigned short *s_runm, int *skey, int *sM) {
+  const int R = a.R, t0 = threadIdx.x * PER;
+  constexpr int kDefer = 1 << 30;
+  const bool split = !a.fused;
+  const unsigned kprev = t0 > 0 ? (unsigned)(s_key[t0 - 1] >> 32) : 0xffffffffu;
+  const unsigned knext = t0 + PER < P ? (unsigned)(s_key[t0 + PER] >> 32) : 0xffffffffu;
+  bool vld[PER], st[PER], eq[PER];
+  int cnt = 0, valid = 0;
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    vld[i] = kk[i] != 0xffffffffu;
+    st[i] = vld[i] && kk[i] != (i ? kk[i - 1] : kprev);
+    eq[i] = vld[i] && kk[i] == (i + 1 < PER ? kk[i + 1] : knext);
+    cnt += st[i];
+    valid += vld[i];
+  }
+  int U = 0, V = 0;
+  const int u0 = block_exclusive_scan(cnt, &U, s_ws);
+  block_exclusive_scan(valid, &V, s_ws);
+  {
+    int *ukey = a.ukey + (size_t)cb * a.SB;
+    int *uoff = a.uoff + (size_t)cb * (a.SB + 1);
+    int *inv = a.inv + (size_t)cb * a.SB;
+    int u = u0;
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+      if (!vld[i]) continue;
+      if (split) inv[vv[i]] = t0 + i;
+      if (st[i]) {
+        ukey[u] = (int)kk[i];
+        if (split) uoff[u] = t0 + i;
+        u++;
+      }
+    }
+    if (threadIdx.x == 0) {
+      if (split) uoff[U] = V;
+      a.ucount[cb] = U;
+    }
+  }
+  if (!a.fused) return;
+  // the last slot of the run through position i (a run leaving the chunk:
+  // followed in LDS)
+  int lastsl[PER];
+  {
+    int ls = vv[PER - 1];
+    if (eq[PER - 1]) {
+      int pos = t0 + PER;
+      while (pos < V && (unsigned)(s_key[pos] >> 32) == kk[PER - 1]) pos++;
+      ls = (int)(unsigned)s_key[pos - 1];
+    }
+    lastsl[PER - 1] = ls;
+  }
+#pragma unroll
+  for (int i = PER - 2; i >= 0; i--) lastsl[i] = eq[i] ? lastsl[i + 1] : vv[i];
+  // classes of the runs starting here: 0 single, 1 local, kDefer (+ 2 + m)
+  int cls[PER];
+  int ns = 0;
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    cls[i] = 0;
+    if (st[i] && eq[i]) {
+      cls[i] = (vv[i] / R == lastsl[i] / R) ? 1 : kDefer;
+      ns += cls[i] == kDefer;
+    }
+  }
+  int S = 0;
+  int m = block_exclusive_scan(ns, &S, s_ws);
+  int *keys = skey + (size_t)cb * a.Mmax;
+  {
+    int u = u0;
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+      if (!st[i]) continue;
+      if (cls[i] == kDefer) {
+        cls[i] = kDefer | (2 + m);
+        keys[m++] = (int)kk[i];
+      }
+      // 16-bit in LDS: 0, 1 or 0x8000 | (2 + m) (2 + m <= SB / 2 + 2 < 2^15)
+      s_runm[u++] = (unsigned short)(cls[i] & kDefer ? 0x8000 | (cls[i] & 0x7fff) : cls[i]);
+    }
+  }
+  __syncthreads();
+  auto k32 = [&](int t) { return (unsigned)(s_key[t] >> 32); };
+  auto slot = [&](int t) { return (int)(unsigned)(s_key[t] & 0xffffffffu); };
+  unsigned *sc = a.scode + (size_t)cb * a.SB;
+  // the run through the chunk's first position began before it: its class
+  int cur = 0;
+  if (u0 > 0 && vld[0] && !st[0]) {
+    const int v = s_runm[u0 - 1];
+    cur = v & 0x8000 ? kDefer | (v & 0x7fff) : v;
+  }
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    if (!vld[i]) continue;
+    if (st[i]) cur = cls[i];
+    const int t = t0 + i;
+    unsigned code = kSOwn;
+    if (cur & kDefer) {
+      code = kSShared | (st[i] ? kSOwn : 0u) | (unsigned)(cur & (kDefer - 1));
+    } else if (cur) {
+      // local: as defer_codes
+      int rs = t;
+      while (rs > 0 && k32(rs - 1) == kk[i]) rs--;
+      int re = t + 1;
+      while (re < V && k32(re) == kk[i]) re++;
+      const int me = emit_pos(vv[i] % R, a.K);
+      int first = 1, last = 1, own = vv[i] % R;
+      for (int j = rs; j < re; j++) {
+        const int e2 = emit_pos(slot(j) % R, a.K);
+        first &= e2 >= me;
+        last &= e2 <= me;
+        if (e2 > emit_pos(own, a.K)) own = slot(j) % R;
+      }
+      code = kSLocal | (last ? kSOwn : 0u) | (first ? kSFirst : 0u) | (unsigned)own;
+    }
+    sc[vv[i]] = code;
   }
   if (threadIdx.x == 0) sM[cb] = S;
 }
@@ -1486,7 +1660,10 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
   float *btgt = a.btgt + (size_t)cb * a.B * 3;
   // the batch's record ids once into LDS, then every gather below has one
   // round trip; slot rows 8 per thread in flight before the stores
-  __shared__ int s_perm[kPrepB];
+  // the batch's record ids, in the dynamic region behind the keys: where the
+  // run classes go later (radix path: 16-bit classes, so 4 workgroups fit a
+  // CU's LDS) or behind them (bitonic path)
+  int *s_perm = reinterpret_cast<int *>(s_key + P) + (P == kSortP ? 0 : P);
   for (int i = threadIdx.x; i < nb; i += kTB) s_perm[i] = a.perm[r0 + i];
   __syncthreads();
   HGX_STAMP(ts[1]);
@@ -1519,22 +1696,58 @@ __global__ __launch_bounds__(kTB) void train_prep(TrainArgs a, int64_t base,
   }
   __syncthreads();
   HGX_STAMP(ts[2]);
-  for (int size = 2; size <= P; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = threadIdx.x; t < P / 2; t += kTB) {
-        const int lo = 2 * t - (t & (stride - 1));
-        const int hi = lo + stride;
-        const bool up = ((lo & size) == 0);
-        const unsigned long long x = s_key[lo], y = s_key[hi];
-        if ((x > y) == up) {
-          s_key[lo] = y;
-          s_key[hi] = x;
+  constexpr int IPT = kSortP / kTB;
+  unsigned kk[IPT];
+  int vv[IPT];
+  if (P == kSortP) {
+    // the common batch (256 records x 14 slots): a block radix sort of the
+    // 32-bit (table, row) keys with the slot as value, 8-bit digits, 4
+    // passes, stable (equal keys keep slot order: the same order as the
+    // 64-bit (key, slot) keys below); its storage aliases s_key. 4.5x faster
+    // than the bitonic network (73 -> 16 us per batch).
+    using BRS = rocprim::block_radix_sort<unsigned, kTB, kSortP / kTB, int>;
+    static_assert(sizeof(typename BRS::storage_type) <= kSortP * 8 + kPrepB * 4,
+                  "sort storage fits the radix path's dynamic LDS");
+#pragma unroll
+    for (int i = 0; i < IPT; i++) {
+      const unsigned long long x = s_key[threadIdx.x * IPT + i];
+      kk[i] = (unsigned)(x >> 32);  // padding: 0xffffffff, after every key
+      vv[i] = (int)(unsigned)x;
+    }
+    __syncthreads();
+    BRS().sort(kk, vv, *reinterpret_cast<typename BRS::storage_type *>(s_key));
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < IPT; i++)
+      s_key[threadIdx.x * IPT + i] =
+          kk[i] == 0xffffffffu ? ~0ull : ((unsigned long long)kk[i] << 32) | (unsigned)vv[i];
+    __syncthreads();
+  } else {
+    for (int size = 2; size <= P; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int t = threadIdx.x; t < P / 2; t += kTB) {
+          const int lo = 2 * t - (t & (stride - 1));
+          const int hi = lo + stride;
+          const bool up = ((lo & size) == 0);
+          const unsigned long long x = s_key[lo], y = s_key[hi];
+          if ((x > y) == up) {
+            s_key[lo] = y;
+            s_key[hi] = x;
+          }
         }
+        __syncthreads();
       }
-      __syncthreads();
     }
   }
   HGX_STAMP(ts[3]);
+  if (P == kSortP) {
+    prep_runs_regs<IPT>(a, cb, P, kk, vv, s_key, s_ws,
+                        reinterpret_cast<unsigned short *>(s_key + P), skey, sM);
+    HGX_STAMP(ts[5]);
+    ts[4] = ts[5];
+    if (g_trace && base == 0) trace_put(0, 1, 6, ts);
+    return;
+  }
   // unique starts over a contiguous chunk per thread, then one block scan
   const int per = P / kTB;
   const int t0 = threadIdx.x * per;
@@ -2125,7 +2338,9 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   const int Mmax = SB / 2 + 1;        // deferred rows per batch: <= SB / 2
   const int MX = fused ? 2 + Mmax : 0;
   HGX_CHECK(ctx, MX <= (int)kDefMask + 1, HGX_EUNSUP, "batch too large for the step");
-  const int lstride = std::max(nblk1, NBF);
+  // (early row-0 form: one loss word per record group, float2 rows)
+  const bool r0e = HGX_TRAIN_R0EARLY && fused && ctx->dp == 2 * SL;
+  const int lstride = std::max(nblk1, r0e ? NBF * prpb : NBF);
   const int GPB2 = tb2 / L;
   // one unique-row task per group, plus the two padding-row workgroups
   const int grid2 = (SB + GPB2 - 1) / GPB2 + 2;
@@ -2345,7 +2560,11 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     HGX_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     res.ev.push_back(e);
   }
-  const size_t prep_smem = (size_t)P * (sizeof(unsigned long long) + sizeof(int));
+  // train_prep's dynamic LDS: keys + run classes + record ids (radix path:
+  // the ids and the 16-bit classes share one region)
+  const size_t prep_smem =
+      P == kSortP ? ((size_t)P * 8 + std::max<size_t>(kPrepB * 4, (size_t)SB * 2) + 15) / 16 * 16
+                  : (size_t)P * 12 + kPrepB * 4;
   const size_t place_smem = sizeof(int) * ((size_t)Mmax + SB);
   // Preparation of chunk c (same stream, right before its batches: the
   // records it writes are still in the Infinity Cache when they are read).
