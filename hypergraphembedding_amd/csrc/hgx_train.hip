@@ -21,8 +21,8 @@
 //      sum its slot rows in sorted slot order (deterministic) and apply
 //      Adagrad in place.
 // The unique-row lists come from train_prep, run for a whole chunk of
-// batches in parallel (one workgroup per batch: LDS bitonic sort of the
-// batch's (row, slot) keys). K1/K2 for a run of batches are captured once
+// batches in parallel (one workgroup per batch: block radix sort of the
+// batch's (row, slot) keys; an LDS bitonic network for other batch shapes). K1/K2 for a run of batches are captured once
 // as direct launches (or hipGraphs of 64 batches, HGX_GRAPH=1), the
 // chunk-local batch index passed as a kernel argument (no device counters,
 // no dependent index load).
@@ -807,11 +807,15 @@ __device__ __forceinline__ void row0_finish(const TrainArgs &a, int q,
 // records per workgroup, ceil(B / RPB) workgroups; records placed by
 // train_place, those without neighbour lists first (whole waves skip the list
 // gathers).
-// HGX_TRAIN_R0EARLY (A/B builds): every record group adds its own row-0
-// gradients to the fixed-point slot right after its forward pass, before its
-// row stores, and stores its own loss: no end-of-batch workgroup barrier.
+// Early row-0 sums (float2 rows, d = 128): every record group adds its own
+// row-0 gradients (the same float adds in emit order) to the fixed-point
+// slot right after its forward pass, before its row stores, and stores its
+// own loss word: no end-of-batch workgroup barrier. Interleaved A/B on C3
+// HOBE records: 6.69 -> 6.65 us per batch, epoch 36.85M -> 37.09M records/s
+// (profiles/r03/trainer/prep2/ab_diet_128.txt). HGX_TRAIN_R0EARLY=0 (A/B
+// builds): the workgroup's fixed-order float sum, one atomic per column.
 #ifndef HGX_TRAIN_R0EARLY
-#define HGX_TRAIN_R0EARLY 0
+#define HGX_TRAIN_R0EARLY 1
 #endif
 template <int L, int VW, int KMAX, int MODE, int TB, bool MULTI>
 __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, int nb, int q) {

@@ -270,8 +270,11 @@ int hgx_train_last_stats(hgx_ctx *ctx, double *ms, int64_t *records,
  * deferred-row step rounds each slot gradient (after the 1/batch factor) to
  * the nearest multiple of 2^-44 and adds them exactly as 64-bit integers
  * (order-free, bitwise reproducible): a quantisation of 2^-45 absolute per
- * slot, so values below 2^-45 (~2.8e-14) vanish. A slot gradient of
- * magnitude >= 32 fails the call with HGX_ENUMERIC. */
+ * slot, so values below 2^-45 (~2.8e-14) vanish. The padding row's
+ * gradients are summed in fp32 per record (steps holding a float2 of the row
+ * per lane, d = 128 by default) or per workgroup of records (float4 per
+ * lane, d = 256) before that rounding. A slot gradient
+ * of magnitude >= 32 fails the call with HGX_ENUMERIC. */
 int hgx_train_path_stats(hgx_ctx *ctx, int64_t *fused_batches,
                          int64_t *split_batches);
 /* Of the last hgx_train: step batches launched in the MULTI pending-slot form
