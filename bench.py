@@ -51,7 +51,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = ("training samples/sec + alg-dist SpMV GB/s, HOBE dim=128 at "
           "1/2/4/8 MI355X")
-PMC_TRAIN = os.path.join(ROOT, "profiles", "r03_end", "pmc_train.json")
+PMC_TRAIN = os.path.join(ROOT, "profiles", "r03_final", "pmc_train.json")
 
 
 def parse():

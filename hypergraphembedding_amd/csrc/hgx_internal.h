@@ -62,9 +62,11 @@ struct Tuning {
   // launch
   int mlp_fuse_head = 1;
   // trainer: chunk c + 1 prepared (train_prep / train_place) on a second
-  // stream while chunk c trains (1), or in line before it (0); with
-  // train_prep_cus > 0 the two streams get disjoint CU masks, that many CUs
-  // for the preparation
+  // stream while chunk c trains (1), on the same stream one chunk ahead
+  // (2: queued before chunk c's batches, so the host never waits on the
+  // batches for the next chunk's MULTI flags), or in line before it (0);
+  // with train_prep_cus > 0 the two streams of form 1 get disjoint CU masks,
+  // that many CUs for the preparation
   int train_prep_overlap = 0;
   int train_prep_cus = 0;
 };

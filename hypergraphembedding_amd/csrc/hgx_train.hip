@@ -2364,7 +2364,8 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   // step buffers: pfo, pidx, pcode, ptgt, scode, skey [2], sM [2], pbrk
   // (with the overlapped preparation the placed buffers pfo, pidx, pcode,
   // ptgt, pbrk twice: chunk c + 1 is placed while chunk c trains)
-  const bool overlap = fused && ctx->tune.train_prep_overlap == 1;
+  const bool overlap = fused && ctx->tune.train_prep_overlap >= 1;
+  const bool ahead = overlap && ctx->tune.train_prep_overlap == 2;  // one stream
   const size_t placed_ints = 2 * (size_t)CB * Mmax + pg * RW * 2 + pg * 3 + (size_t)CB + 2;
   const size_t step_ints = fused ? 2 * (size_t)CB * Mmax + pg * RW * 2 + pg * 3 +
                                        (size_t)CB * SB + 2 * (size_t)CB * Mmax +
@@ -2520,7 +2521,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   // (disjoint CU masks when train_prep_cus > 0), ordered after everything
   // queued on ctx->stream so far and joined back into it at the end
   hipStream_t sst = ctx->stream, spr = ctx->stream;
-  if (overlap) {
+  if (overlap && !ahead) {
     HGX_TRY(train_streams(ctx, ctx->tune.train_prep_cus));
     sst = ctx->tstream[0];
     spr = ctx->tstream[1];
@@ -2630,10 +2631,12 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
     if (overlap) {
       // chunk c + 1 prepared on spr while chunk c trains on sst; placed set
       // c & 1 is rewritten (chunk c + 2) only after chunk c's steps are done
-      hipEvent_t ej = pev[nchunks];
-      (void)hipEventRecord(ej, ctx->stream);
-      (void)hipStreamWaitEvent(sst, ej, 0);
-      (void)hipStreamWaitEvent(spr, ej, 0);
+      if (!ahead) {
+        hipEvent_t ej = pev[nchunks];
+        (void)hipEventRecord(ej, ctx->stream);
+        (void)hipStreamWaitEvent(sst, ej, 0);
+        (void)hipStreamWaitEvent(spr, ej, 0);
+      }
       // The host enqueues chunk c + 1's preparation only once chunk c - 1's
       // steps are done (it waits for them after queueing chunk c's), so the
       // preparation stream never holds a barrier packet blocked on the step
@@ -2654,12 +2657,16 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
         const int64_t base = c * CB;
         const int nbc = (int)std::min<int64_t>(CB, nbatches - base);
         const int cp = (int)(c & 1);
+        // one stream: chunk c + 1's preparation queued ahead of chunk c's
+        // batches (stream order protects placed set (c + 1) & 1, last read
+        // by chunk c - 1's batches, queued before it)
+        if (ahead && c + 1 < nchunks) prep_ov(c + 1);
         if (hipEventSynchronize(pev[c]) != hipSuccess) {
           rc = hgx_fail(ctx, HGX_EHIP, "batch preparation failed: %s",
                         hipGetErrorString(hipGetLastError()));
           break;
         }
-        (void)hipStreamWaitEvent(sst, pev[c], 0);
+        if (!ahead) (void)hipStreamWaitEvent(sst, pev[c], 0);
         (void)hipEventRecord(bev[2 * c], sst);
         const int *hb = res.hbrk + (size_t)cp * CB;
         for (int b = 0; b < nbc; b++) {
@@ -2673,7 +2680,7 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
         nfused += nbc;
         (void)hipEventRecord(bev[2 * c + 1], sst);
         last_nbc = nbc;
-        if (c + 1 < nchunks) {
+        if (!ahead && c + 1 < nchunks) {
           // placed set (c + 1) & 1 is free once chunk c - 1's steps are done
           if (c >= 1 && hipEventSynchronize(bev[2 * (c - 1) + 1]) != hipSuccess) {
             rc = hgx_fail(ctx, HGX_EHIP, "batch step failed: %s",

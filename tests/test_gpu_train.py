@@ -314,10 +314,11 @@ def test_step_diverged_gradients_raise(ctx):
               perms=np.arange(idx.shape[0])[None, :])
 
 
-@pytest.mark.parametrize("cus", [0, 32])
-def test_overlapped_preparation_bitwise_equal(ctx, cus):
+@pytest.mark.parametrize("mode,cus", [(1, 0), (1, 32), (2, 0)])
+def test_overlapped_preparation_bitwise_equal(ctx, mode, cus):
   """Chunk c + 1 prepared on a second stream while chunk c trains (tuning
-  train_prep_overlap; train_prep_cus: disjoint CU masks) gives the in-line
+  train_prep_overlap 1; train_prep_cus: disjoint CU masks) or on the same
+  stream one chunk ahead (train_prep_overlap 2) gives the in-line
   preparation's tables and losses bit for bit. 2,100 batches = three chunks
   of up to 1,024 (both placed-buffer sets used, one reused), hub batches on
   both chunk boundaries (deferred rows and MULTI batches across chunks),
@@ -331,7 +332,7 @@ def test_overlapped_preparation_bitwise_equal(ctx, cus):
   ctx.records_set(idx, tgt)
   out = []
   try:
-    for ov in (0, 1):
+    for ov in (0, mode):
       ctx.set_tuning("train_prep_overlap", ov)
       ctx.set_tuning("train_prep_cus", cus)
       ctx.model_init(128, 20002, 20002, seed=9)
