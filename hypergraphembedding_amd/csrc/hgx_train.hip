@@ -1588,21 +1588,11 @@ __global__ __launch_bounds__(kTB) void train_place(TrainArgs a, int nbc, int CB,
   int *pidx = a.pidx + (size_t)cb * G * RW;
   unsigned *pcode = a.pcode + (size_t)cb * G * RW;
   float *ptgt = a.ptgt + (size_t)cb * G * 3;
-  // zero what the scattered writes below may leave unset: the flush-slot
-  // words of every group, and whole groups no record lands in (a ragged
-  // batch); record slots and batch words are always written
-  for (int t = threadIdx.x; t < G * kFX; t += kTB) {
-    const int g = t / kFX, w = g * RW + R + (t - g * kFX);
-    pidx[w] = 0;
-    pcode[w] = 0u;
+  for (int t = threadIdx.x; t < G * RW; t += kTB) {
+    pidx[t] = 0;
+    pcode[t] = 0u;
   }
-  if (nb < G) {
-    for (int t = threadIdx.x; t < G * RW; t += kTB) {
-      pidx[t] = 0;
-      pcode[t] = 0u;
-    }
-    for (int t = threadIdx.x; t < G * 3; t += kTB) ptgt[t] = 0.f;
-  }
+  for (int t = threadIdx.x; t < G * 3; t += kTB) ptgt[t] = 0.f;
   __syncthreads();  // s_pos, s_prev, s_u; zero fill before the scattered writes
   const unsigned *sc = a.scode + (size_t)cb * SB;
   for (int t = threadIdx.x; t < nb * R; t += kTB) {
