@@ -760,7 +760,10 @@ __device__ __forceinline__ void flush_row(const TrainArgs &a, int par, int key, 
 // workgroup store a float partial and every workgroup of the next batch
 // read all 64 of them: 64 KB per workgroup from the Infinity Cache, about
 // 0.9 us per batch at its per-CU rate (tools/ablate_train.py); now 16 KB.
-constexpr int kR0Slots = 8;
+#ifndef HGX_R0_SLOTS
+#define HGX_R0_SLOTS 8
+#endif
+constexpr int kR0Slots = HGX_R0_SLOTS;  // (A/B builds: HGX_R0_SLOTS)
 template <int L, int VW>
 __device__ __forceinline__ long long *r0_row(const TrainArgs &a, int par, int slot,
                                              int tab) {
