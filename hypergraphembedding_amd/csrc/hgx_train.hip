@@ -760,19 +760,24 @@ __device__ __forceinline__ void flush_row(const TrainArgs &a, int par, int key, 
 // workgroup store a float partial and every workgroup of the next batch
 // read all 64 of them: 64 KB per workgroup from the Infinity Cache, about
 // 0.9 us per batch at its per-CU rate (tools/ablate_train.py); now 16 KB.
-#ifndef HGX_R0_SLOTS
-#define HGX_R0_SLOTS 8
-#endif
-constexpr int kR0Slots = HGX_R0_SLOTS;  // (A/B builds: HGX_R0_SLOTS)
+// Slots per row width (interleaved A/B, profiles/r03/trainer/ab_slots_*.txt):
+// 128-float rows (each record adds its own sums, 256 adders per batch) 8
+// slots: 6.68 us per batch vs 7.77 at 4 and 6.81 at 16; 256-float rows (one
+// add per workgroup, 64 adders) 4 slots: 8.36 vs 8.50 at 8 and 9.12 at 16.
+constexpr int kR0Slots = 8;  // the most any width uses (buffer sizing)
+template <int DP>
+struct R0S {
+  static constexpr int n = DP >= 256 ? 4 : kR0Slots;
+};
 template <int L, int VW>
 __device__ __forceinline__ long long *r0_row(const TrainArgs &a, int par, int slot,
                                              int tab) {
-  return a.r0acc + (((size_t)par * kR0Slots + slot) * 2 + tab) * (VW * L);
+  return a.r0acc + (((size_t)par * R0S<VW * L>::n + slot) * 2 + tab) * (VW * L);
 }
 template <int L, int VW>
 struct Row0Loads {
   static constexpr int NC = 2 * L;  // V columns (both tables)
-  typename SV<VW>::Fx g[kR0Slots];
+  typename SV<VW>::Fx g[R0S<VW * L>::n];
   typename SV<VW>::T rp, ra;
 };
 // every load issued unconditionally, first thing in the kernel (a load
@@ -788,7 +793,7 @@ __device__ __forceinline__ void row0_issue(const TrainArgs &a, int q,
   ld.rp = (q ? sh_row<L, VW>(a, ppar, tab, 0) : tab_row<L, VW>(a, tab, 0, 0))[c];
   ld.ra = (q ? sh_row<L, VW>(a, ppar, tab, 1) : tab_row<L, VW>(a, tab, 1, 0))[c];
 #pragma unroll
-  for (int j = 0; j < kR0Slots; j++)
+  for (int j = 0; j < R0S<VW * L>::n; j++)
     ld.g[j] = SV<VW>::ldfix(r0_row<L, VW>(a, ppar, j, tab), c);
 }
 // column owners (threads < NC): the slots' exact integer sum, the previous
@@ -800,7 +805,7 @@ __device__ __forceinline__ void row0_finish(const TrainArgs &a, int q,
   using S = SV<VW>;
   typename S::Fx t = ld.g[0];
 #pragma unroll
-  for (int j = 1; j < kR0Slots; j++) t = S::fxadd(t, ld.g[j]);
+  for (int j = 1; j < R0S<VW * L>::n; j++) t = S::fxadd(t, ld.g[j]);
   if (g_tab & 2048) t = S::fxzero();  // (debug ablation)
   if (q) S::adagrad(p0, a0, S::unfix(t), a.lr, a.eps);
 }
@@ -1162,7 +1167,7 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
         if (row[3] == 0) zE = S::add(zE, gre);
         if (row[2] == 0) zN = S::add(zN, S::fma(dz1, Nl, S::zero()));
         if (row[1] == 0) zE = S::add(zE, S::fma(dz2, Er, S::zero()));
-        const int slot = (blockIdx.x * RPB + grp) % kR0Slots;
+        const int slot = (blockIdx.x * RPB + grp) % R0S<VW * L>::n;
         S::addfix(r0_row<L, VW>(a, par, slot, 0), lane, zN, bad);
         S::addfix(r0_row<L, VW>(a, par, slot, 1), lane, zE, bad);
         if (lane == 0) a.lossbuf[(size_t)gb * a.lstride + blockIdx.x * RPB + grp] = lrec;
@@ -1198,7 +1203,7 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
       if (threadIdx.x < NC && !(g_tab & 16384)) {
         V sz = S::zero();
         for (int g = 0; g < RPB; g++) sz = S::add(sz, s_z[tab0][g][c0]);
-        S::addfix(r0_row<L, VW>(a, par, blockIdx.x % kR0Slots, tab0), c0, sz, bad);
+        S::addfix(r0_row<L, VW>(a, par, blockIdx.x % R0S<VW * L>::n, tab0), c0, sz, bad);
       }
       if (threadIdx.x == 0) {
         float sl = 0.f;
@@ -1232,7 +1237,7 @@ __global__ __launch_bounds__(TB) void train_step(TrainArgs a, int cb, int gb, in
     for (int i = blockIdx.x * TB + threadIdx.x; i < tot; i += NBF * TB)
       z[i] = make_longlong2(0, 0);
     longlong2 *zr = reinterpret_cast<longlong2 *>(r0_row<L, VW>(a, zpar, 0, 0));
-    for (int i = blockIdx.x * TB + threadIdx.x; i < kR0Slots * VW * L; i += NBF * TB)
+    for (int i = blockIdx.x * TB + threadIdx.x; i < R0S<VW * L>::n * VW * L; i += NBF * TB)
       zr[i] = make_longlong2(0, 0);
   }
   // (timing ablations compute wrong values: no overflow verdict for them)
@@ -1257,7 +1262,7 @@ __global__ __launch_bounds__(256) void train_flush(TrainArgs a, const int *keys,
   for (int e = blockIdx.x * GPB + grp; e < M; e += gridDim.x * GPB) {
     if (e < 2) {  // row 0: the last batch's slots, summed as train_step sums
       SV<4>::Fx t = SV<4>::ldfix(r0_row<L, 4>(a, par, 0, e), lane);
-      for (int j = 1; j < kR0Slots; j++)
+      for (int j = 1; j < R0S<4 * L>::n; j++)
         t = SV<4>::fxadd(t, SV<4>::ldfix(r0_row<L, 4>(a, par, j, e), lane));
       const float4 g = SV<4>::unfix(t);
       float4 p = sh_row<L, 4>(a, par, e, 0)[lane], ac = sh_row<L, 4>(a, par, e, 1)[lane];
