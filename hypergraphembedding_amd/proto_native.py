@@ -219,7 +219,20 @@ def shard_name(path, i, n):
   return f"{path}-{i:05d}-of-{n:05d}"
 
 
+def _shard_files(path):
+  return glob.glob(glob.escape(str(path)) + "-[0-9]*-of-[0-9]*")
+
+
+def _clear_outputs(path):
+  """Remove an earlier embedding at `path` (the single file and any shards
+  of any count), so that a later read never mixes layouts or shard counts."""
+  for name in [str(path)] + _shard_files(path):
+    if os.path.isfile(name):
+      os.remove(name)
+
+
 def _write_shards(path, bufs, n):
+  _clear_outputs(path)
   if n == 1:
     names = [str(path)]
   else:
@@ -249,20 +262,29 @@ def save_embedding(path, emb):
   file names."""
   if isinstance(emb, ShardedEmbedding):
     return emb.write(path)
+  _clear_outputs(path)
   with open(path, "wb") as f:
     f.write(emb.SerializeToString())
   return [str(path)]
 
 
 def embedding_files(path):
-  """The files of the embedding at `path`: [path] or its shards in order."""
+  """The files of the embedding at `path`: [path] or its shards in order.
+  Raises if both layouts, or shards of more than one count, are present (a
+  stale earlier write: the caller cannot tell which one is current)."""
   path = str(path)
+  names = sorted(_shard_files(path))
   if os.path.exists(path):
+    if names:
+      raise FileExistsError(f"{path} exists both as one file and as "
+                            f"{len(names)} shard files")
     return [path]
-  names = sorted(glob.glob(glob.escape(path) + "-[0-9]*-of-[0-9]*"))
   if not names:
     raise FileNotFoundError(path)
-  n = int(names[0].rsplit("-of-", 1)[1])
+  counts = sorted({int(x.rsplit("-of-", 1)[1]) for x in names})
+  if len(counts) > 1:
+    raise FileExistsError(f"{path}: shards of {counts} different counts")
+  n = counts[0]
   want = [shard_name(path, i, n) for i in range(n)]
   missing = sorted(set(want) - set(names))
   if missing:
@@ -311,14 +333,26 @@ def _message_tables(m):
 
 
 def _merge(parts):
-  """Later parts win on a repeated key, as protobuf's merge does."""
+  """Later parts win on a repeated key, as protobuf's merge does. Shards
+  written here hold ascending, disjoint id ranges: then the parts are only
+  concatenated (one part: returned as parsed), with no dedup copy."""
   out = {}
   for side in ("node", "edge"):
-    ids = np.concatenate([p[f"{side}_ids"] for p in parts])
     tabs = [p[f"{side}_tab"] for p in parts]
     w = max((t.shape[1] for t in tabs if t.size), default=0)
-    tab = np.concatenate([t.reshape(-1, w) if t.size else
-                          np.zeros((0, w), np.float32) for t in tabs])
+    tabs = [t.reshape(-1, w) if t.size else np.zeros((0, w), np.float32)
+            for t in tabs]
+    if len(parts) == 1:
+      ids, tab = parts[0][f"{side}_ids"], tabs[0]
+    else:
+      ids = np.concatenate([p[f"{side}_ids"] for p in parts])
+      tab = None
+    if ids.size < 2 or bool(np.all(ids[1:] > ids[:-1])):
+      out[f"{side}_ids"] = ids
+      out[f"{side}_tab"] = tab if tab is not None else np.concatenate(tabs)
+      continue
+    if tab is None:
+      tab = np.concatenate(tabs)
     rev = np.argsort(ids[::-1], kind="stable")  # last occurrence first
     first = np.ones(ids.size, bool)
     first[1:] = ids[::-1][rev][1:] != ids[::-1][rev][:-1]

@@ -282,3 +282,38 @@ def test_save_embedding_either_form(tmp_path, monkeypatch):
     back = pn.read_embedding(str(tmp_path / name))
     assert back.method_name == "M" and back.dim == 6
     assert np.array_equal(back.node_tab, x) and np.array_equal(back.edge_tab, y)
+
+
+def test_overwrite_never_reads_a_stale_embedding(tmp_path):
+  """A write replaces whatever embedding was at the path before: one file by
+  shards, 2 shards by 3, shards by one file. A directory holding both
+  layouts, or shards of two counts, is an error, never a silent pick."""
+  from hypergraphembedding_amd import proto_native as pn
+  path = str(tmp_path / "e.pb")
+  cases = [_emb_case(n, n // 2, 16, s) for n, s in ((40, 1), (700, 2),
+                                                     (1100, 3), (30, 4))]
+  caps = [1 << 30, 28 * 1024, 28 * 1024, 1 << 30]
+  counts = []
+  for (nid, nt, eid, et), cap in zip(cases, caps):
+    emb = pn.ShardedEmbedding(nid, nt, eid, et, 16, "M", shard_bytes=cap)
+    files = emb.write(path)
+    counts.append(len(files))
+    back = pn.read_embedding(path)
+    o = np.argsort(nid)
+    assert np.array_equal(back.node_ids, nid[o])
+    assert np.array_equal(back.node_tab, nt[o])
+    left = sorted(os.listdir(str(tmp_path)))
+    assert left == sorted(os.path.basename(f) for f in files)
+  assert counts[0] == 1 and 1 < counts[1] < counts[2] and counts[3] == 1
+  # stale layouts written by someone else are refused
+  nid, nt, eid, et = cases[1]
+  pn.ShardedEmbedding(nid, nt, eid, et, 16, "M", shard_bytes=28 * 1024).write(path)
+  with open(path, "wb") as f:
+    f.write(b"")
+  with pytest.raises(FileExistsError):
+    pn.read_embedding(path)
+  os.remove(path)
+  with open(pn.shard_name(path, 0, 7), "wb") as f:
+    f.write(b"")
+  with pytest.raises(FileExistsError):
+    pn.read_embedding(path)

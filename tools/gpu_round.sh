@@ -1,14 +1,16 @@
 #!/bin/bash
 # Round evidence: GPU test suite, bench line, rocprofv3 kernel stats of the
 # bench, FETCH/WRITE PMC passes of bench.py (separate runs) summarised per
-# batch step. Usage: tools/gpu_round_r02.sh TAG
+# batch step. Usage: tools/gpu_round.sh TAG
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/${1:-r02}
+O=gpurun_out/${1:-round}
 mkdir -p $O
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread --durations=15 > $O/gpu_tests.log 2>&1 || { echo TESTFAIL; exit 11; }
 echo tests-ok
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKEFAIL; exit 12; }
+echo smoke-ok
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || exit 14
 echo bench-ok
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_bench -o run --output-format csv -- python3 bench.py --no-cpu > $O/bench_prof.json 2> $O/bench_prof.err || exit 15
@@ -22,6 +24,9 @@ for C in FETCH_SIZE WRITE_SIZE; do
 done
 F=$(find $O/pmc_FETCH_SIZE -name '*counter_collection.csv' | head -1)
 W=$(find $O/pmc_WRITE_SIZE -name '*counter_collection.csv' | head -1)
-python tools/pmc_train_summary.py "$F" "$W" $O/pmc_train.json 128 2 > /dev/null || exit 18
+python tools/pmc_train_summary.py "$F" "$W" $O/pmc_train.json 128 3 > /dev/null || exit 18
 rm -rf $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE
+# the --gpus N path rehearsed on one GPU: 2 ranks over gloo on cuda:0 (not
+# a scaling measurement: both ranks share one GPU)
+timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 1 --warmup 0 --one-device --dist-backend gloo --no-cpu --no-extra > $O/bench_2rank_gloo.json 2> $O/bench_2rank_gloo.err || { echo G2FAIL; exit 19; }
 echo all-ok
