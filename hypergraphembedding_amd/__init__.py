@@ -21,7 +21,9 @@ from .algebraic_distance import EmbedAlgebraicDistance
 from .hg2v_sample import (AlgebraicDistanceSamples, BooleanSamples,
                           SamplesToModelInput, SimilarityRecord,
                           WeightedJaccardSamples)
-from .hg2v_weighting import UniformWeight, WeightByNeighborhood
+from .hg2v_weighting import (ComputeSpans, UniformWeight, WeightByAlgebraicSpan,
+                             WeightByDistance, WeightByDistanceCluster,
+                             WeightByNeighborhood, WeightBySameTypeDistance)
 from .hg2v_model import (BooleanModel, KerasModelToEmbedding,
                          UnweightedFloatModel)
 from .proto_native import (ShardedEmbedding, read_embedding, read_incidence,
@@ -48,6 +50,8 @@ __all__ = [
     # hot-path pieces
     "BooleanSamples", "AlgebraicDistanceSamples", "SamplesToModelInput",
     "SimilarityRecord", "UniformWeight", "WeightByNeighborhood",
+    "WeightByDistance", "WeightBySameTypeDistance", "WeightByDistanceCluster",
+    "WeightByAlgebraicSpan", "ComputeSpans",
     "BooleanModel", "UnweightedFloatModel", "KerasModelToEmbedding",
     # hypergraph util
     "AddNodeToEdge", "RemoveNodeFromEdge", "RemoveNode", "RemoveEdge",

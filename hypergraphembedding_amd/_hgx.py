@@ -21,6 +21,7 @@ LOSS_KLD, LOSS_MSE = 0, 1
 ACT_SIGMOID, ACT_RELU = 0, 1
 HOBE_NN, HOBE_EE, HOBE_NE = 0, 1, 2
 WEIGHT_UNIFORM, WEIGHT_NEIGHBORHOOD, WEIGHT_DISTANCE = 0, 1, 2
+NORM_L2, NORM_INF = 0, 1
 MLP_LP_CLASSIFIER, MLP_NE_SUPERVISED, MLP_NE_SEMI_SUPERVISED = 0, 1, 2
 
 _lib = None
@@ -60,6 +61,10 @@ SIGNATURES = {
     "hgx_alg_shard_edge_partial_range": (_int, [_vp, _int, _int]),
     "hgx_hobe_probs": (_int, [_vp, _int, _i64, _vp, _vp, _vp]),
     "hgx_incidence_weights": (_int, [_vp, _int, ctypes.c_double, _vp, _vp]),
+    "hgx_weight_distance": (_int, [_vp, _int, ctypes.c_double, _vp, _vp]),
+    "hgx_weight_same_type": (_int, [_vp, _int, _int, ctypes.c_double, _pi64,
+                                    _vp, _vp, _vp]),
+    "hgx_weight_span": (_int, [_vp, ctypes.c_double, _vp, _vp, _vp, _vp]),
     "hgx_sample_fobe": (_int, [_vp, _u64, _int, _vp, _vp, _vp, _vp, _pi64]),
     "hgx_sample_hobe": (_int, [_vp, _u64, _int, _int, _pi64]),
     "hgx_sample_hobe_rows": (_int, [_vp, _u64, _int, _vp, _vp, _int, _pi64]),
@@ -77,6 +82,7 @@ SIGNATURES = {
     "hgx_records_import": (_int, [_vp, _i64, _int, _vp, _vp, _int, _vp]),
     "hgx_model_init": (_int, [_vp, _int, _i64, _i64, _u64, _vp, _vp]),
     "hgx_model_get": (_int, [_vp, _vp, _vp]),
+    "hgx_model_get_rows": (_int, [_vp, _int, _i64, _vp, _vp]),
     "hgx_train": (_int, [_vp, _int, _int, _f32, _f32, _int, _int, _f32, _u64,
                          _vp, _vp, _pint]),
     "hgx_train_last_stats": (_int, [_vp, _pdbl, _pi64, _pi64]),
@@ -302,6 +308,41 @@ class Context:
                                           _ptr(e)))
     return n, e
 
+  # hg2v_weighting distance / span weights (vectors = the alg coordinates)
+  def weight_distance(self, norm=NORM_L2, alpha=0.0):
+    """WeightByDistance values per incidence, A and A^T CSR order."""
+    n = np.empty(self.inc.nnz, np.float32)
+    e = np.empty(self.inc.nnz, np.float32)
+    self._chk(lib().hgx_weight_distance(self.h, norm, float(alpha), _ptr(n),
+                                        _ptr(e)))
+    return n, e
+
+  def weight_same_type(self, side, norm=NORM_L2, alpha=0.0):
+    """WeightBySameTypeDistance CSR (rowptr int64, col int32, val float32)
+    of the node (side 0) or edge (side 1) pattern, compressed ids."""
+    R = self.inc.N if side == 0 else self.inc.E
+    nnz = ctypes.c_int64()
+    rp = np.empty(R + 1, np.int64)
+    self._chk(lib().hgx_weight_same_type(self.h, side, norm, float(alpha),
+                                         ctypes.byref(nnz), _ptr(rp), None, None))
+    col = np.empty(nnz.value, np.int32)
+    val = np.empty(nnz.value, np.float32)
+    self._chk(lib().hgx_weight_same_type(self.h, side, norm, float(alpha),
+                                         ctypes.byref(nnz), _ptr(rp), _ptr(col),
+                                         _ptr(val)))
+    return rp, col, val
+
+  def weight_span(self, alpha=0.0):
+    """(node spans, edge spans) float32 and the span weights per incidence
+    (A and A^T CSR order)."""
+    sn = np.empty(self.inc.N, np.float32)
+    se = np.empty(self.inc.E, np.float32)
+    n = np.empty(self.inc.nnz, np.float32)
+    e = np.empty(self.inc.nnz, np.float32)
+    self._chk(lib().hgx_weight_span(self.h, float(alpha), _ptr(sn), _ptr(se),
+                                    _ptr(n), _ptr(e)))
+    return sn, se, n, e
+
   # ---- samplers / records ----
   def sample_fobe(self, seed, K, node_q, edge_q, neg_node_q=None,
                   neg_edge_q=None):
@@ -426,6 +467,13 @@ class Context:
     et = np.empty((self.edge_rows, self.d), np.float32)
     self._chk(lib().hgx_model_get(self.h, _ptr(nt), _ptr(et)))
     return nt, et
+
+  def model_get_rows(self, table, rows):
+    """Rows of the node (0) or edge (1) table, (len(rows), d) float32."""
+    r = _c(rows, np.int64).ravel()
+    out = np.empty((r.size, self.d), np.float32)
+    self._chk(lib().hgx_model_get_rows(self.h, table, r.size, _ptr(r), _ptr(out)))
+    return out
 
   def train(self, batch=256, max_epochs=10, lr=0.01, eps=1e-7, loss=LOSS_MSE,
             act=ACT_RELU, min_delta=1e-3, shuffle_seed=0, perms=None):

@@ -714,21 +714,31 @@ __device__ __forceinline__ void st_row(float2 *p, float2 v) {
                      __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
-// float4: there is no 16-byte atomic store, so the instruction is written
-// out. s_nop 1: the wait states a >8-byte store's data registers need
-// before a VALU may overwrite them (the compiler's hazard check does not see
-// into asm; without it d = 256 training diverged). The "memory" clobber keeps
-// the compiler's memory operations in program order around it; its vmcnt
-// waits only get stricter for an extra store in flight (loads still return
-// in order). HGX_TRAIN_WT4=0 (A/B builds): a plain store.
+// float4: there is no 16-byte atomic store. The store is a raw buffer store
+// with the sc1 cache-policy bit (`buffer_store_dwordx4 … sc1`, the compiler's
+// own instruction, so its hazard checks cover the data registers). Every
+// call stores within one row (a wave holds one record at 256-float rows),
+// so the descriptor's base is the first lane's address minus 2^31 (wave
+// uniform, two readfirstlanes) and each lane's 32-bit offset is 2^31 plus
+// its distance from that lane. dword 3 = 0x00020000: the raw-buffer format
+// word of gfx9 (CDNA). HGX_TRAIN_WT4=0 (A/B builds): a plain store.
 #ifndef HGX_TRAIN_WT4
 #define HGX_TRAIN_WT4 1
 #endif
 __device__ __forceinline__ void st_row(float4 *p, float4 v) {
   if (HGX_TRAIN_WT4) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v x = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(x) : "memory");
+    typedef int i4v __attribute__((ext_vector_type(4)));
+    const unsigned long long u = reinterpret_cast<unsigned long long>(p);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+    const unsigned long long base =
+        ((unsigned long long)hi << 32 | lo) - (1ull << 31);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void *>(base), (short)0, (int)0xffffffffu, 0x00020000);
+    const i4v x = {__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z),
+                   __float_as_int(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)(unsigned)(u - base), 0,
+                                           16 /* sc1 */);
   } else {
     *p = v;
   }
@@ -2194,6 +2204,45 @@ extern "C" int hgx_model_get(hgx_ctx *ctx, float *node_tab, float *edge_tab) {
     HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   }
   HGX_LAUNCH_CHECK(ctx);
+  return HGX_OK;
+}
+
+__global__ void gather_rows(const float *__restrict__ src,
+                            const int64_t *__restrict__ rows, float *dst,
+                            int64_t n, int d, int dp) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * d;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = i / d;
+    dst[i] = src[rows[q] * dp + (int)(i % d)];
+  }
+}
+
+extern "C" int hgx_model_get_rows(hgx_ctx *ctx, int table, int64_t n,
+                                  const int64_t *rows, float *out) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->d > 0, HGX_ESTATE, "no model on device");
+  HGX_CHECK(ctx, table == 0 || table == 1, HGX_EINVAL, "table must be 0 or 1");
+  HGX_CHECK(ctx, n >= 0, HGX_EINVAL, "negative row count");
+  if (n == 0) return HGX_OK;
+  HGX_CHECK(ctx, rows && out, HGX_EINVAL, "null rows / out");
+  const int64_t nr = table == 0 ? ctx->node_rows : ctx->edge_rows;
+  for (int64_t q = 0; q < n; q++)
+    HGX_CHECK(ctx, rows[q] >= 0 && rows[q] < nr, HGX_EINVAL,
+              "row %lld outside the table (%lld rows)", (long long)rows[q],
+              (long long)nr);
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  const int d = ctx->d;
+  HGX_TRY(hgx_ensure(ctx, ctx->s2, sizeof(int64_t) * n));
+  HGX_TRY(hgx_ensure(ctx, ctx->s1, sizeof(float) * n * d));
+  HGX_HIP(ctx, hipMemcpyAsync(ctx->s2.p, rows, sizeof(int64_t) * n,
+                              hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(gather_rows, dim3(grid_for(n * d, 256)), dim3(256), 0,
+                     ctx->stream, (table == 0 ? ctx->ntab : ctx->etab).as<float>(),
+                     ctx->s2.as<int64_t>(), ctx->s1.as<float>(), n, d, ctx->dp);
+  HGX_LAUNCH_CHECK(ctx);
+  HGX_HIP(ctx, hipMemcpyAsync(out, ctx->s1.p, sizeof(float) * n * d,
+                              hipMemcpyDeviceToHost, ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return HGX_OK;
 }
 

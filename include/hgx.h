@@ -238,6 +238,33 @@ int hgx_records_export(hgx_ctx *ctx, void *d_idx, void *d_tgt);
 int hgx_records_import(hgx_ctx *ctx, int64_t n, int K, const void *d_idx,
                        const void *d_tgt, int nblocks, const int64_t *bounds);
 
+/* ---- hg2v_weighting distance / span weights ------------------------------ *
+ * hg2v_weighting.py:34-64 (WeightBySameTypeDistance), 67-103
+ * (WeightByDistance), 170-192 + 236-293 (WeightByAlgebraicSpan,
+ * ComputeSpans). The vectors are the alg coordinates on the context
+ * (hgx_alg_set of the reference embedding's node / edge rows). `norm`:
+ * np.linalg.norm (HGX_NORM_L2: numpy's float32 sdot arithmetic) or its
+ * ord=inf (HGX_NORM_INF). Values are the reference's after
+ * ZeroOneScaleValues -> OneMinusValues -> AlphaScaleValues, float32 (the
+ * reference's arrays of protobuf float fields are float32); zeros are
+ * returned (the reference's lil_matrix drops them). */
+#define HGX_NORM_L2 0
+#define HGX_NORM_INF 1
+/* first order: per incidence, in A's (node_major) and A^T's (edge_major)
+ * CSR order (either may be NULL) */
+int hgx_weight_distance(hgx_ctx *ctx, int norm, double alpha, float *node_major,
+                        float *edge_major);
+/* second order: the A A^T (side 0, node rows) or A^T A (side 1) pattern,
+ * diagonal included, as CSR over compressed ids (rows sorted, columns
+ * ascending). col == val == NULL: only *nnz (and rowptr[R+1] if given);
+ * HGX_EUNSUP when the pattern's expansion exceeds 2^31 paths. */
+int hgx_weight_same_type(hgx_ctx *ctx, int side, int norm, double alpha,
+                         int64_t *nnz, int64_t *rowptr, int32_t *col, float *val);
+/* spans (ComputeSpans) and the span weights per incidence (node_major[v,e]
+ * = edge e's value, edge_major[e,v] = node v's); any output may be NULL */
+int hgx_weight_span(hgx_ctx *ctx, double alpha, float *node_span,
+                    float *edge_span, float *node_major, float *edge_major);
+
 /* ---- model + trainer ---------------------------------------------------- *
  * Replaces BooleanModel / UnweightedFloatModel (hg2v_model.py:51-203) and
  * the model.fit loop (embedding.py:269-305): two tables of (rows x d) fp32,
@@ -248,6 +275,11 @@ int hgx_records_import(hgx_ctx *ctx, int64_t n, int K, const void *d_idx,
 int hgx_model_init(hgx_ctx *ctx, int d, int64_t node_rows, int64_t edge_rows,
                    uint64_t seed, const float *node_tab, const float *edge_tab);
 int hgx_model_get(hgx_ctx *ctx, float *node_tab, float *edge_tab);
+/* Rows `rows[0..n)` of the node (table 0) or edge (table 1) table into
+ * out[n x d]: the touched rows of a 10M-row table without downloading it
+ * (KerasModelToEmbedding reads rows idx + 1, hg2v_model.py:31-48). */
+int hgx_model_get_rows(hgx_ctx *ctx, int table, int64_t n, const int64_t *rows,
+                       float *out);
 /* perms: NULL -> a fresh device shuffle per epoch keyed by shuffle_seed,
  * else max_epochs x n int64 permutations (Keras' np.random.shuffle order).
  * epoch_loss: max_epochs floats (may be NULL). */

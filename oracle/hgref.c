@@ -972,3 +972,236 @@ int hgref_train(int64_t n, int K, const int32_t *idx, const float *tgt, int d,
   free(a_k); free(b_k); free(sa); free(sb);
   return 0;
 }
+
+/* ------------------------------------------------------------------------- */
+/* hg2v_weighting.py distance and span weights (34-64, 67-103, 170-192,      */
+/* 207-293) with the dict helpers ZeroOneScaleValues / OneMinusValues /       */
+/* AlphaScaleValues (301-333).                                               */
+/* `norm` = np.linalg.norm = sqrt(x.dot(x)): numpy's FLOAT_dot / DOUBLE_dot   */
+/* call OpenBLAS sdot / ddot. The fixtures come from numpy's OpenBLAS 0.3.29  */
+/* SkylakeX kernels, restated here (probed on 3,000 random vectors):          */
+/* sdot: k & ~31 elements in 4 x 8 float FMA accumulators (64-blocks in       */
+/* 4 x 16, folded l + l+8), ((a0+a1)+a2)+a3, lanes l + l+4, (h0+h1)+(h2+h3),  */
+/* the rest added in double as float products; float sqrt of the float.      */
+/* ddot: k & ~15 in 4 x 4 double FMA accumulators (32-blocks 4 x 8, folded    */
+/* l + l+4), same sum, (s0+s2)+(s1+s3), the rest by double FMA; sqrt.          */
+/* norm 1 = ord inf (max |d|).                                                 */
+/* ------------------------------------------------------------------------- */
+float hgref_norm32(const float *a, const float *b, int k, int norm) {
+  if (norm == 1) {
+    float m = 0.0f;
+    for (int i = 0; i < k; i++) {
+      float d = fabsf(a[i] - b[i]);
+      if (d > m) m = d;
+    }
+    return m;
+  }
+  int n1 = k & ~31, n64 = n1 & ~63, i = 0;
+  float tot = 0.0f;
+  if (n1) {
+    float acc[32] = {0}, s[8], h[4];
+    if (n64) {
+      float a5[64] = {0};
+      for (; i < n64; i += 64)
+        for (int t = 0; t < 64; t++) {
+          float d = a[i + t] - b[i + t];
+          a5[t] = fmaf(d, d, a5[t]);
+        }
+      for (int j = 0; j < 4; j++)
+        for (int l = 0; l < 8; l++) acc[j * 8 + l] = a5[j * 16 + l] + a5[j * 16 + l + 8];
+    }
+    for (; i < n1; i += 32)
+      for (int t = 0; t < 32; t++) {
+        float d = a[i + t] - b[i + t];
+        acc[t] = fmaf(d, d, acc[t]);
+      }
+    for (int l = 0; l < 8; l++) s[l] = ((acc[l] + acc[8 + l]) + acc[16 + l]) + acc[24 + l];
+    for (int l = 0; l < 4; l++) h[l] = s[l] + s[l + 4];
+    tot = (h[0] + h[1]) + (h[2] + h[3]);
+  }
+  double dot = tot;
+  for (; i < k; i++) {
+    float d = a[i] - b[i];
+    float p = d * d;
+    dot += (double)p;
+  }
+  return sqrtf((float)dot);
+}
+
+double hgref_norm64(const float *a, const float *b, int k, int norm) {
+  if (norm == 1) {
+    double m = 0.0;
+    for (int i = 0; i < k; i++) {
+      double d = fabs((double)a[i] - (double)b[i]);
+      if (d > m) m = d;
+    }
+    return m;
+  }
+  int n1 = k & ~15, n32 = n1 & ~31, i = 0;
+  double dot = 0.0;
+  if (n1) {
+    double acc[16] = {0}, s[4];
+    if (n32) {
+      double a5[32] = {0};
+      for (; i < n32; i += 32)
+        for (int t = 0; t < 32; t++) {
+          double d = (double)a[i + t] - (double)b[i + t];
+          a5[t] = fma(d, d, a5[t]);
+        }
+      for (int j = 0; j < 4; j++)
+        for (int l = 0; l < 4; l++) acc[j * 4 + l] = a5[j * 8 + l] + a5[j * 8 + l + 4];
+    }
+    for (; i < n1; i += 16)
+      for (int t = 0; t < 16; t++) {
+        double d = (double)a[i + t] - (double)b[i + t];
+        acc[t] = fma(d, d, acc[t]);
+      }
+    for (int l = 0; l < 4; l++) s[l] = ((acc[l] + acc[4 + l]) + acc[8 + l]) + acc[12 + l];
+    dot = (s[0] + s[2]) + (s[1] + s[3]);
+  }
+  for (; i < k; i++) {
+    double d = (double)a[i] - (double)b[i];
+    dot = fma(d, d, dot);
+  }
+  return sqrt(dot);
+}
+
+/* ZeroOneScaleValues -> OneMinusValues -> AlphaScaleValues on np.float32
+ * values (hg2v_weighting.py:94-95): float32 arithmetic, alpha and 1 - alpha
+ * weak Python scalars cast to float32 (numpy 2, NEP 50) */
+static void scale_f32(int64_t n, float *v, float mn, float mx, double alpha) {
+  float delta = mx - mn, a32 = (float)alpha, b32 = (float)(1.0 - alpha);
+  for (int64_t t = 0; t < n; t++) {
+    float o = delta == 0.0f ? 0.0f : 1.0f - (v[t] - mn) / delta;
+    float p = b32 * o;
+    v[t] = a32 + p;
+  }
+}
+
+/* WeightByDistance (hg2v_weighting.py:67-103): per incidence (v, e) of A
+ * (out_n, A's CSR order) and A^T (out_e), norm(node_vec - edge_vec) with
+ * float32 vectors X[N x k], Y[E x k], then the scaling over all incidences.
+ * Zeros are kept here (the reference's lil_matrix drops them). */
+void hgref_weight_distance(int64_t N, int64_t E, const int32_t *rp_n,
+                           const int32_t *col_n, const int32_t *rp_e,
+                           const int32_t *col_e, const float *X, const float *Y,
+                           int k, int norm, double alpha, float *out_n,
+                           float *out_e) {
+  float mn = INFINITY, mx = 0.0f;
+  for (int64_t v = 0; v < N; v++)
+    for (int32_t t = rp_n[v]; t < rp_n[v + 1]; t++) {
+      float w = hgref_norm32(X + v * k, Y + (int64_t)col_n[t] * k, k, norm);
+      out_n[t] = w;
+      if (w < mn) mn = w;
+      if (w > mx) mx = w;
+    }
+  for (int64_t e = 0; e < E; e++)
+    for (int32_t t = rp_e[e]; t < rp_e[e + 1]; t++)
+      out_e[t] = hgref_norm32(X + (int64_t)col_e[t] * k, Y + e * k, k, norm);
+  int64_t nnz = rp_n[N];
+  if (nnz == 0) return;
+  scale_f32(nnz, out_n, mn, mx, alpha);
+  scale_f32(nnz, out_e, mn, mx, alpha);
+}
+
+static int cmp_i32(const void *a, const void *b) {
+  int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
+  return (x > y) - (x < y);
+}
+
+/* WeightBySameTypeDistance, one half (hg2v_weighting.py:37-52 on
+ * node2edge * node2edge.T, :55-62): the pattern of P Q (P = rp/col over R
+ * rows, Q = rq/cq), diagonal included, as CSR with ascending columns;
+ * value = norm of the difference of the rows' vectors tab[R x k], scaled
+ * over all entries. float32 throughout: np.array(emb.values) of protobuf's
+ * upb repeated-float container (protobuf 7) is a float32 array. Returns
+ * nnz; with col_out == NULL only counts (rowptr still filled). */
+int64_t hgref_weight_same_type(int64_t R, const int32_t *rp, const int32_t *col,
+                               const int32_t *rq, const int32_t *cq,
+                               const float *tab, int k, int norm, double alpha,
+                               int64_t *rowptr, int32_t *col_out,
+                               float *val_out) {
+  int64_t nnz = 0, cap = 16;
+  int32_t *buf = (int32_t *)malloc(sizeof(int32_t) * cap);
+  float mn = INFINITY, mx = 0.0f;
+  for (int64_t r = 0; r < R; r++) {
+    int64_t m = 0;
+    for (int32_t t = rp[r]; t < rp[r + 1]; t++) {
+      int32_t e = col[t];
+      for (int32_t j = rq[e]; j < rq[e + 1]; j++) {
+        if (m == cap) {
+          cap *= 2;
+          buf = (int32_t *)realloc(buf, sizeof(int32_t) * cap);
+        }
+        buf[m++] = cq[j];
+      }
+    }
+    qsort(buf, (size_t)m, sizeof(int32_t), cmp_i32);
+    if (rowptr) rowptr[r] = nnz;
+    for (int64_t i = 0; i < m; i++) {
+      if (i > 0 && buf[i] == buf[i - 1]) continue;
+      if (col_out) {
+        float v = hgref_norm32(tab + r * k, tab + (int64_t)buf[i] * k, k, norm);
+        col_out[nnz] = buf[i];
+        val_out[nnz] = v;
+        if (v < mn) mn = v;
+        if (v > mx) mx = v;
+      }
+      nnz++;
+    }
+  }
+  if (rowptr) rowptr[R] = nnz;
+  free(buf);
+  if (col_out && nnz) scale_f32(nnz, val_out, mn, mx, alpha);
+  return nnz;
+}
+
+/* ComputeSpans (hg2v_weighting.py:214-233, 236-293): per row r of P, over
+ * its neighbours c and dimensions, diff = other[c] - mine[r] (np.subtract
+ * of two float32 containers: float32); span = max(0, max diff) -
+ * min(0, min diff) */
+static void spans_of(int64_t R, const int32_t *rp, const int32_t *col,
+                     const float *mine, const float *other, int k, float *span) {
+  for (int64_t r = 0; r < R; r++) {
+    float lo = 0.0f, hi = 0.0f;
+    for (int32_t t = rp[r]; t < rp[r + 1]; t++)
+      for (int d = 0; d < k; d++) {
+        float df = other[(int64_t)col[t] * k + d] - mine[r * k + d];
+        if (df > hi) hi = df;
+        if (df < lo) lo = df;
+      }
+    span[r] = (hi - lo) + 0.0f;
+  }
+}
+
+/* WeightByAlgebraicSpan (hg2v_weighting.py:170-192) given the spans'
+ * embedding: spans of nodes (over their edges) and edges (over their
+ * nodes), each side zero-one / one-minus / alpha scaled (np.float32
+ * values) and kept float32 (DictToSparseRow); node_major[t] = the value of
+ * incidence t's edge (A multiply), edge_major[t] = its node's (A^T). */
+void hgref_weight_span(int64_t N, int64_t E, const int32_t *rp_n,
+                       const int32_t *col_n, const int32_t *rp_e,
+                       const int32_t *col_e, const float *X, const float *Y,
+                       int k, double alpha, float *sn, float *se,
+                       float *node_major, float *edge_major) {
+  spans_of(N, rp_n, col_n, X, Y, k, sn);
+  spans_of(E, rp_e, col_e, Y, X, k, se);
+  float *wn = (float *)malloc(sizeof(float) * (N + 1));
+  float *we = (float *)malloc(sizeof(float) * (E + 1));
+  for (int side = 0; side < 2; side++) {
+    int64_t R = side ? E : N;
+    const float *s = side ? se : sn;
+    float *w = side ? we : wn;
+    float mn = INFINITY, mx = 0.0f;
+    for (int64_t r = 0; r < R; r++) {
+      if (s[r] < mn) mn = s[r];
+      if (s[r] > mx) mx = s[r];
+      w[r] = s[r];
+    }
+    if (R) scale_f32(R, w, mn, mx, alpha);
+  }
+  for (int32_t t = 0; t < rp_n[N]; t++) node_major[t] = we[col_n[t]];
+  for (int32_t t = 0; t < rp_e[E]; t++) edge_major[t] = wn[col_e[t]];
+  free(wn);
+  free(we);
+}

@@ -82,6 +82,20 @@ def lib():
     L.hgref_centroids.restype = _i64
     L.hgref_centroids.argtypes = [_i64, _i32p, _i32p, _i64, _i32p, _i32p,
                                   _f32p, _i64p, _vp, _vp]
+    L.hgref_norm32.restype = ctypes.c_float
+    L.hgref_norm32.argtypes = [_f32p, _f32p, _int, _int]
+    L.hgref_norm64.restype = ctypes.c_double
+    L.hgref_norm64.argtypes = [_f32p, _f32p, _int, _int]
+    L.hgref_weight_distance.argtypes = [_i64, _i64, _i32p, _i32p, _i32p, _i32p,
+                                        _f32p, _f32p, _int, _int,
+                                        ctypes.c_double, _f32p, _f32p]
+    L.hgref_weight_same_type.restype = _i64
+    L.hgref_weight_same_type.argtypes = [_i64, _i32p, _i32p, _i32p, _i32p,
+                                         _f32p, _int, _int, ctypes.c_double,
+                                         _vp, _vp, _vp]
+    L.hgref_weight_span.argtypes = [_i64, _i64, _i32p, _i32p, _i32p, _i32p,
+                                    _f32p, _f32p, _int, ctypes.c_double, _f32p,
+                                    _f32p, _f32p, _f32p]
     _lib = L
   return _lib
 
@@ -268,26 +282,36 @@ def train(idx, tgt, K, node_tab, edge_tab, loss, act, batch=256, lr=0.01,
   return nt, et, losses[:ran.value].copy(), na, ea
 
 
-_mt = None
+_mt = {}
+
+
+def _mt_lib(exact):
+  name = "libcpumt_chk.so" if exact else "libcpumt.so"
+  if name not in _mt:
+    build()
+    path = os.path.join(_HERE, name)
+    src = os.path.join(_HERE, "cpu_train_mt.c")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+      subprocess.run(["make", "-C", _HERE, "-s", name], check=True)
+    L = ctypes.CDLL(path)
+    L.cpu_train_mt.restype = _int
+    L.cpu_train_mt.argtypes = [_i64, _int, _i32p, _f32p, _int, _i64, _i64,
+                               _f32p, _f32p, _f32p, _f32p, _int, _int, _int,
+                               ctypes.c_float, ctypes.c_float, _int, _int,
+                               ctypes.POINTER(ctypes.c_double)]
+    _mt[name] = L
+  return _mt[name]
 
 
 def train_mt(idx, tgt, K, node_tab, edge_tab, loss, act, batch=256, lr=0.01,
-             eps=1e-7, epochs=1, threads=0, copy=True):
-  """Multi-threaded CPU baseline trainer (cpu_train_mt.c; records in the
-  given order). Updates copies of the tables (copy=False: the given float32
-  tables in place); returns (nt, et, mean loss)."""
-  global _mt
-  if _mt is None:
-    build()
-    path = os.path.join(_HERE, "libcpumt.so")
-    if not os.path.exists(path):
-      subprocess.run(["make", "-C", _HERE, "-s"], check=True)
-    _mt = ctypes.CDLL(path)
-    _mt.cpu_train_mt.restype = _int
-    _mt.cpu_train_mt.argtypes = [_i64, _int, _i32p, _f32p, _int, _i64, _i64,
-                                 _f32p, _f32p, _f32p, _f32p, _int, _int, _int,
-                                 ctypes.c_float, ctypes.c_float, _int, _int,
-                                 ctypes.POINTER(ctypes.c_double)]
+             eps=1e-7, epochs=1, threads=0, copy=True, exact=False):
+  """Multi-threaded CPU trainer (cpu_train_mt.c; records in the given
+  order). exact=False: the bench's CPU baseline build (-O3, AVX2/FMA);
+  exact=True: the checker build, rounding like hgref_train (no contraction)
+  -- used as the oracle where the stream is too long for the scalar one.
+  Updates copies of the tables (copy=False: the given float32 tables in
+  place); returns (nt, et, mean loss)."""
+  lib_ = _mt_lib(exact)
   idx = np.ascontiguousarray(idx, np.int32)
   tgt = np.ascontiguousarray(tgt, np.float32)
   nt = np.ascontiguousarray(node_tab, np.float32)
@@ -296,9 +320,9 @@ def train_mt(idx, tgt, K, node_tab, edge_tab, loss, act, batch=256, lr=0.01,
     nt, et = nt.copy(), et.copy()
   na, ea = np.zeros_like(nt), np.zeros_like(et)
   lo = ctypes.c_double()
-  _mt.cpu_train_mt(idx.shape[0], K, idx, tgt, nt.shape[1], nt.shape[0],
-                   et.shape[0], nt, et, na, ea, loss, act, batch, lr, eps,
-                   epochs, threads, ctypes.byref(lo))
+  lib_.cpu_train_mt(idx.shape[0], K, idx, tgt, nt.shape[1], nt.shape[0],
+                    et.shape[0], nt, et, na, ea, loss, act, batch, lr, eps,
+                    epochs, threads, ctypes.byref(lo))
   return nt, et, lo.value
 
 _mlp = None
@@ -406,3 +430,57 @@ def cpu_hobe_sample_mt(inc, alg_node, alg_edge, node_q, edge_q, K, seed=0,
                               threads, idx, tgt, b)
   assert n >= 0
   return idx[:n], tgt[:n], b
+
+
+# ---- hg2v_weighting distance / span weights (hgref.c) ----------------------
+NORM_L2, NORM_INF = 0, 1
+
+
+def _csr(inc):
+  return (np.ascontiguousarray(inc.rp_n, np.int32),
+          np.ascontiguousarray(inc.col_n, np.int32),
+          np.ascontiguousarray(inc.rp_e, np.int32),
+          np.ascontiguousarray(inc.col_e, np.int32))
+
+
+def weight_distance(inc, X, Y, norm=NORM_L2, alpha=0.0):
+  """WeightByDistance values per incidence (A, A^T order; zeros kept)."""
+  X = np.ascontiguousarray(X, np.float32)
+  Y = np.ascontiguousarray(Y, np.float32)
+  out_n = np.empty(inc.nnz, np.float32)
+  out_e = np.empty(inc.nnz, np.float32)
+  lib().hgref_weight_distance(inc.N, inc.E, *_csr(inc), X, Y, X.shape[1], norm,
+                              float(alpha), out_n, out_e)
+  return out_n, out_e
+
+
+def weight_same_type(inc, side, tab, norm=NORM_L2, alpha=0.0):
+  """WeightBySameTypeDistance half: (rowptr int64, col int32, val float32)
+  over compressed ids (zeros kept)."""
+  rp_n, col_n, rp_e, col_e = _csr(inc)
+  P = (rp_n, col_n, rp_e, col_e) if side == 0 else (rp_e, col_e, rp_n, col_n)
+  R = inc.N if side == 0 else inc.E
+  tab = np.ascontiguousarray(tab, np.float32)
+  rowptr = np.empty(R + 1, np.int64)
+  nnz = lib().hgref_weight_same_type(R, *P, tab, tab.shape[1], norm,
+                                     float(alpha), rowptr.ctypes.data, None,
+                                     None)
+  col = np.empty(max(nnz, 1), np.int32)
+  val = np.empty(max(nnz, 1), np.float32)
+  lib().hgref_weight_same_type(R, *P, tab, tab.shape[1], norm, float(alpha),
+                               rowptr.ctypes.data, col.ctypes.data,
+                               val.ctypes.data)
+  return rowptr, col[:nnz], val[:nnz]
+
+
+def weight_span(inc, X, Y, alpha=0.0):
+  """ComputeSpans (float32) + WeightByAlgebraicSpan values per incidence."""
+  X = np.ascontiguousarray(X, np.float32)
+  Y = np.ascontiguousarray(Y, np.float32)
+  sn = np.empty(inc.N, np.float32)
+  se = np.empty(inc.E, np.float32)
+  wn = np.empty(inc.nnz, np.float32)
+  we = np.empty(inc.nnz, np.float32)
+  lib().hgref_weight_span(inc.N, inc.E, *_csr(inc), X, Y, X.shape[1],
+                          float(alpha), sn, se, wn, we)
+  return sn, se, wn, we

@@ -31,6 +31,12 @@ def test_train_mt_matches_oracle():
                                threads=4)
     assert np.abs(a_nt - b_nt).max() < 1e-5
     assert np.abs(a_et - b_et).max() < 1e-5
+    # the checker build (the oracle of tests/test_gpu_baseline_parity.py)
+    c_nt, c_et, c_loss = O.train_mt(idx, tgt, K, nt, et, loss, act, epochs=1,
+                                    threads=4, exact=True)
+    assert np.abs(a_nt - c_nt).max() < 1e-6
+    assert np.abs(a_et - c_et).max() < 1e-6
+    assert np.isclose(c_loss, ref[2][0], rtol=1e-6)
 
 
 def test_cpu_hobe_sampler_baseline_computes_the_reference_quantities(small_inc):

@@ -1,0 +1,84 @@
+"""Trainer parity at BASELINE size (SURVEY §8c tolerance).
+
+C3 (BASELINE.json configs[2]): one full HOBE epoch on the random 100k/50k
+graph -- every record the device samples (~60M, d = 128, batch 256) --
+trained on the GPU and by the oracle with identical initial tables and the
+same batch order (the device takes the permutation as `perms`). The oracle at
+this size is cpu_train_mt.c's checker build (oracle/libcpumt_chk.so: the
+records of a batch over OpenMP threads, every product and sum rounded like
+hgref_train; tests/test_cpu_baseline.py pins it to hgref_train), since the
+scalar hgref_train would take ~8 minutes. Bar: epoch loss rtol 1e-4, per-row
+cosine p50 >= 0.9999 and p1 >= 0.999 on both tables.
+
+The C4 window (configs[3], 10M/5M power-law, d = 256, full-size tables,
+the MULTI form on >= 40% of the batches) is in tests/test_gpu_c4.py, where
+the graph is already built.
+
+Keras itself is absent from the image: the trainer stays "parity unpinned"
+against the reference; these tests pin the device against the restatement
+at the sizes the bench runs.
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def row_cos(a, b):
+  a = a.astype(np.float64)
+  b = b.astype(np.float64)
+  num = (a * b).sum(1)
+  den = np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1)
+  ok = den > 0
+  return num[ok] / den[ok]
+
+
+def _threads():
+  return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+@pytest.mark.timeout(900)
+def test_c3_full_hobe_epoch_vs_oracle():
+  from hypergraphembedding_amd import _hgx
+  from hypergraphembedding_amd.synthetic import random_hypergraph
+  inc = random_hypergraph(seed=0)
+  K, S, d = 5, 200, 128
+  ctx = _hgx.Context(0)
+  try:
+    ctx.upload(inc)
+    r = np.random.RandomState(4)
+    ctx.alg_set(r.random_sample((inc.N, 10)), r.random_sample((inc.E, 10)))
+    ctx.alg_run(20)
+    n = ctx.sample_hobe(17, K, S)
+    assert n > 55_000_000
+    rs = np.random.RandomState(12)
+    nt = rs.uniform(-0.05, 0.05, (inc.N + 1, d)).astype(np.float32)
+    et = rs.uniform(-0.05, 0.05, (inc.E + 1, d)).astype(np.float32)
+    perm = rs.permutation(n)
+    ctx.model_init(d, inc.N + 1, inc.E + 1, node_tab=nt, edge_tab=et)
+    gl = ctx.train(batch=256, max_epochs=1, loss=_hgx.LOSS_MSE,
+                   act=_hgx.ACT_RELU, perms=perm[None, :], min_delta=-1e30)
+    fused, split = ctx.train_path_stats()
+    assert split == 0 and fused == -(-n // 256)
+    gnt, get_ = ctx.model_get()
+    idx, tgt = ctx.records_get()
+  finally:
+    ctx.close()
+  idx = np.ascontiguousarray(idx[perm])
+  tgt = np.ascontiguousarray(tgt[perm])
+  del perm
+  ont, oet, oloss = O.train_mt(idx, tgt, K, nt, et, O.LOSS_MSE, O.ACT_RELU,
+                               epochs=1, threads=_threads(), copy=False,
+                               exact=True)
+  assert np.isclose(gl[0], oloss, rtol=1e-4), (gl, oloss)
+  for g, o, name in ((gnt, ont, "node"), (get_, oet, "edge")):
+    c = row_cos(g[1:], o[1:])
+    p50, p1 = np.percentile(c, 50), np.percentile(c, 1)
+    print(f"{name}: cosine p50 {p50:.8f} p1 {p1:.8f} min {c.min():.8f} "
+          f"max-abs {np.abs(g - o).max():.3e}")
+    assert p50 >= 0.9999 and p1 >= 0.999, (name, p50, p1)

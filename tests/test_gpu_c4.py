@@ -176,6 +176,53 @@ def test_c4_hobe_d256_epoch_deterministic_and_learning(ctx, g):
   _cache["hobe"] = ctx.model_get()
 
 
+@pytest.mark.timeout(600)
+def test_c4_d256_window_vs_oracle(ctx, g):
+  """Trainer parity on the real C4 stream: a 2M-record
+  window of a shuffled epoch of the 10M/5M power-law HOBE stream, d = 256,
+  on full-size tables (10M + 1 and 5M + 1 rows, device init), against
+  hgref_train with the same initial rows and batch order. The hub edges
+  make most batches take the MULTI pending-slot form (records naming two
+  rows the previous batch deferred); bar: max-abs <= 1e-5 on every touched
+  row, loss rtol 1e-4. The oracle trains compact tables holding only the
+  touched rows (row ids relabelled; the arithmetic is independent of ids)."""
+  from hypergraphembedding_amd import _hgx
+  n, _, _ = _sample(ctx, g)
+  idx, tgt = ctx.records_get()
+  W = 2_000_000
+  sel = np.random.RandomState(13).permutation(n)[:W]
+  idx, tgt = np.ascontiguousarray(idx[sel]), np.ascontiguousarray(tgt[sel])
+  del sel
+  ctx.records_set(idx, tgt)
+  ctx.model_init(D, g.N + 1, g.E + 1, seed=5)
+  ncols = [0, 2] + list(range(4, 4 + K))
+  ecols = [1, 3] + list(range(4 + K, 4 + 2 * K))
+  un = np.unique(np.concatenate([[0], idx[:, ncols].ravel()])).astype(np.int64)
+  ue = np.unique(np.concatenate([[0], idx[:, ecols].ravel()])).astype(np.int64)
+  nt0, et0 = ctx.model_get_rows(0, un), ctx.model_get_rows(1, ue)
+  perms = np.arange(W)[None, :]
+  gl = ctx.train(batch=256, max_epochs=1, loss=_hgx.LOSS_MSE,
+                 act=_hgx.ACT_RELU, perms=perms, min_delta=-1e30)
+  nb = -(-W // 256)
+  multi = ctx.train_multi_pending()
+  assert ctx.train_path_stats() == (nb, 0)
+  print(f"window: {W} records, {nb} batches, MULTI {multi} "
+        f"({multi / nb:.1%}), touched rows {un.size} node / {ue.size} edge")
+  assert multi >= 0.4 * nb
+  gn, ge = ctx.model_get_rows(0, un), ctx.model_get_rows(1, ue)
+  cidx = idx.copy()
+  cidx[:, ncols] = np.searchsorted(un, idx[:, ncols])
+  cidx[:, ecols] = np.searchsorted(ue, idx[:, ecols])
+  ont, oet, ol, _, _ = O.train(cidx, tgt, K, nt0, et0, O.LOSS_MSE, O.ACT_RELU,
+                               batch=256, max_epochs=1, perms=perms,
+                               min_delta=-1e30)
+  assert np.allclose(gl, ol, rtol=1e-4), (gl, ol)
+  dn, de = np.abs(gn - ont).max(), np.abs(ge - oet).max()
+  print(f"max-abs node {dn:.3e} edge {de:.3e}")
+  assert dn <= 1e-5 and de <= 1e-5
+  assert not np.array_equal(gn, nt0) and not np.array_equal(ge, et0)
+
+
 def test_c4_sharded_embedding_output(ctx, g, tmp_path):
   """The C4 HOBE d=256 embedding (15M rows, ~19 GB of wire bytes: far past
   protobuf's 2 GiB message limit) is written as shards of complete

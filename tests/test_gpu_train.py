@@ -349,3 +349,53 @@ def test_overlapped_preparation_bitwise_equal(ctx, mode, cus):
   assert np.array_equal(out[0][2], out[1][2]), (out[0][2], out[1][2])
   assert np.array_equal(out[0][0], out[1][0])
   assert np.array_equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("d", [128, 256])
+def test_padding_row_fixed_point_vs_split_step_and_oracle(ctx, d):
+  """The padding row (row 0 of both tables) collects the gradients of every
+  absent slot as 2^-44 fixed point: per record at 128-float rows (early
+  row-0 sums), per workgroup at 256-float rows. Batches where nearly every
+  slot is row 0 (node-node records: edge slots and both neighbour lists
+  empty, 12 of 14 slots padding) and mixed batches, in order, against the
+  two-kernel step's fp32 sums (train_fused 0) and the oracle."""
+  rs = np.random.RandomState(31)
+  K, B, nb = 5, 256, 10
+  n = nb * B - 77
+  idx = np.zeros((n, 4 + 2 * K), np.int32)
+  kind = np.where(np.arange(n) < 6 * B, 0, rs.randint(0, 3, n))
+  m0, m1, m2 = kind == 0, kind == 1, kind == 2
+  idx[m0, 0] = rs.randint(1, 50000, m0.sum())
+  idx[m0, 2] = rs.randint(1, 50000, m0.sum())
+  idx[m1, 1] = rs.randint(1, 20000, m1.sum())
+  idx[m1, 3] = rs.randint(1, 20000, m1.sum())
+  idx[m2, 0] = rs.randint(1, 50000, m2.sum())
+  idx[m2, 3] = rs.randint(1, 20000, m2.sum())
+  idx[m2, 4:4 + K] = rs.randint(1, 50000, (m2.sum(), K))
+  idx[m2, 4 + K:] = rs.randint(1, 20000, (m2.sum(), K))
+  tgt = np.zeros((n, 3), np.float32)
+  tgt[np.arange(n), kind] = rs.uniform(0, 1, n).astype(np.float32)
+  perms = np.stack([np.arange(n), rs.permutation(n)])
+  nt = rs.uniform(-0.05, 0.05, (50001, d)).astype(np.float32)
+  et = rs.uniform(-0.05, 0.05, (20001, d)).astype(np.float32)
+  ont, oet, ol, _, _ = O.train(idx, tgt, K, nt, et, O.LOSS_MSE, O.ACT_RELU,
+                               batch=B, max_epochs=2, perms=perms,
+                               min_delta=-1.0)
+  ctx.records_set(idx, tgt)
+  res = {}
+  try:
+    for fused in (1, 0):
+      ctx.set_tuning("train_fused", fused)
+      ctx.model_init(d, 50001, 20001, node_tab=nt, edge_tab=et)
+      gl = ctx.train(batch=B, max_epochs=2, loss=O.LOSS_MSE, act=O.ACT_RELU,
+                     perms=perms, min_delta=-1.0)
+      res[fused] = ctx.model_get() + (gl,)
+  finally:
+    ctx.set_tuning("train_fused", 1)
+  for fused in (1, 0):
+    gnt, get_, gl = res[fused]
+    assert np.allclose(gl, ol, rtol=1e-4, atol=1e-7), (fused, gl, ol)
+    assert np.abs(gnt - ont).max() < 1e-5 and np.abs(get_ - oet).max() < 1e-5
+  for t in (0, 1):  # row 0 moved, and both steps agree on it
+    assert not np.array_equal(res[1][t][0], (nt, et)[t][0])
+    assert np.abs(res[1][t][0] - res[0][t][0]).max() < 1e-6
