@@ -451,9 +451,17 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
     # exchange pipelined over edge ranges (all-reduce of range r overlaps
     # the partials of range r + 1)
     alg_dist_sharded(ctx, big, bx0, by0, 2, edge_ranges=args.edge_ranges)
-    ms4 = max_over_ranks(alg_dist_sharded(ctx, big, bx0, by0, args.alg_iters,
-                                          stats=exch4,
-                                          edge_ranges=args.edge_ranges)[2])
+    (r0, r1, xo), y_sh, ms_sh = alg_dist_sharded(
+        ctx, big, bx0, by0, args.alg_iters, stats=exch4,
+        edge_ranges=args.edge_ranges)
+    ms4 = max_over_ranks(ms_sh)
+    # every rank needs every node's coordinates for the HOBE weights: one
+    # all-gather of the node rows (embedding.hobe_sharded's step 1)
+    from hypergraphembedding_amd.embedding import _all_gather_rows
+    t = time.perf_counter()
+    x_sh = _all_gather_rows(xo, r0, r1, big.N, None,
+                            None if args.dist_backend == "nccl" else "cpu")
+    exch4["coord_allgather_s"] = round(max_over_ranks(time.perf_counter() - t), 3)
     ctx.upload(big)  # HOBE below runs on the whole graph of this rank
   else:
     ctx.alg_set(bx0, by0)
@@ -477,17 +485,18 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
   # edge rows (0 elsewhere; the reference samples S per row everywhere, a
   # ~6e9-record epoch), on the alg coords of the run above; one epoch.
   if world > 1:
-    ctx.alg_set(bx0, by0)
-    ctx.alg_run(args.alg_iters)
+    ctx.alg_set(x_sh, y_sh)  # the sharded relaxation's coordinates
+    del x_sh
   S4, K4, d4 = args.num_samples, args.num_neighbors, 256
   rsq = np.random.RandomState(2)
   nq4 = np.where(rsq.random_sample(big.N) < args.c4_frac, S4, 0).astype(np.int32)
   eq4 = np.where(rsq.random_sample(big.E) < args.c4_frac, S4, 0).astype(np.int32)
   ctx.model_init(d4, big.N + 1, big.E + 1, seed=11 + rank)
   if world > 1:
-    # row-range chunks, each sampled row-sharded over the ranks and
-    # all-gathered (hg2v_sample.sharded_chunk_fn): a replica holds one
-    # chunk's stream at a time, the form the full 5.9e9-record epoch takes
+    # strided row chunks, each sampled over the ranks' strided shares and
+    # all-gathered in row order (hg2v_sample.sharded_chunk_fn): a replica
+    # holds one chunk's stream at a time, the form the full 5.9e9-record
+    # epoch takes (embedding.hobe_sharded)
     from hypergraphembedding_amd.embedding import _row_chunks
     from hypergraphembedding_amd.hg2v_sample import sharded_chunk_fn
     bound = 2 * S4

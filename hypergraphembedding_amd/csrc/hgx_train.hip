@@ -714,31 +714,28 @@ __device__ __forceinline__ void st_row(float2 *p, float2 v) {
                      __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
-// float4: there is no 16-byte atomic store. The store is a raw buffer store
-// with the sc1 cache-policy bit (`buffer_store_dwordx4 … sc1`, the compiler's
-// own instruction, so its hazard checks cover the data registers). Every
-// call stores within one row (a wave holds one record at 256-float rows),
-// so the descriptor's base is the first lane's address minus 2^31 (wave
-// uniform, two readfirstlanes) and each lane's 32-bit offset is 2^31 plus
-// its distance from that lane. dword 3 = 0x00020000: the raw-buffer format
-// word of gfx9 (CDNA). HGX_TRAIN_WT4=0 (A/B builds): a plain store.
+// float4: there is no 16-byte atomic store, so the instruction is written
+// out. s_nop 1: the wait states a >8-byte store's data registers need
+// before a VALU may overwrite them (the compiler's hazard check does not see
+// into asm; without it d = 256 training diverged). The "memory" clobber keeps
+// the compiler's memory operations in program order around it; its vmcnt
+// waits only get stricter for an extra store in flight (loads still return
+// in order). HGX_TRAIN_WT4=0 (A/B builds): a plain store.
+// r04: the compiler-visible form -- a raw buffer store with the sc1 policy
+// bit, its base the first lane's row address (two readfirstlanes) -- is
+// correct but measured 8.62 -> 8.93 us per batch at d = 256 (interleaved
+// A/B, C3 HOBE records, profiles/r04/trainer/ab_wt4_builtin.log), so the
+// asm stays. Every d = 256 trainer test checks the stored rows against the
+// oracle (test_gpu_train.py, the C4 window in test_gpu_c4.py): a toolchain
+// that broke the hazard would fail them.
 #ifndef HGX_TRAIN_WT4
 #define HGX_TRAIN_WT4 1
 #endif
 __device__ __forceinline__ void st_row(float4 *p, float4 v) {
   if (HGX_TRAIN_WT4) {
-    typedef int i4v __attribute__((ext_vector_type(4)));
-    const unsigned long long u = reinterpret_cast<unsigned long long>(p);
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
-    const unsigned long long base =
-        ((unsigned long long)hi << 32 | lo) - (1ull << 31);
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void *>(base), (short)0, (int)0xffffffffu, 0x00020000);
-    const i4v x = {__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z),
-                   __float_as_int(v.w)};
-    __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)(unsigned)(u - base), 0,
-                                           16 /* sc1 */);
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(x) : "memory");
   } else {
     *p = v;
   }

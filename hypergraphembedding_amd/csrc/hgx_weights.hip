@@ -101,7 +101,8 @@ __device__ float norm32(const float *__restrict__ a, const float *__restrict__ b
     const float d = __fsub_rn(a[i], b[i]);
     dot = __dadd_rn(dot, (double)__fmul_rn(d, d));
   }
-  return __fsqrt_rn((float)dot);
+  // correctly rounded float sqrt (v_sqrt_f32 is not): through double
+  return (float)sqrt((double)(float)dot);
 }
 
 // ord = inf: max |a_d - b_d| (exact in any order)

@@ -24,7 +24,8 @@ from .algebraic_distance import EmbedAlgebraicDistance, coords_to_embedding
 from .combine_embeddings_util import (CombineEmbeddingsViaConcatenation,
                                       CombineEmbeddingsViaNodeEdgeClassifier)
 from .hg2v_model import Hg2vModel
-from .hg2v_sample import _quotas, sample_fobe, sample_hobe, sample_jaccard
+from .hg2v_sample import (_quotas, row_class_quota, sample_fobe, sample_hobe,
+                          sample_jaccard)
 from .hypergraph_util import Incidence
 from .proto import HypergraphEmbedding
 from .runtime import get_context, numpy_seed
@@ -107,19 +108,21 @@ def _plot_distributions(path, records):
 
 
 # Records resident at once before the skeleton streams the record stream in
-# row-range chunks (68 B per record at K = 5: 2^30 records = 73 GB of HBM).
+# row chunks (68 B per record at K = 5: 2^30 records = 73 GB of HBM).
 RECORDS_BUDGET = 1 << 30
 
 
 def _row_chunks(inc, bound_per_row, budget):
-  """Split node rows and edge rows into n contiguous ranges so that each
-  chunk's record upper bound (bound_per_row per node row and per edge row)
-  stays within `budget`."""
+  """Split the rows into n strided classes (offset c, stride n: node rows
+  and edge rows r = c mod n) so that each chunk's record upper bound
+  (bound_per_row per node row and per edge row) stays within `budget`.
+  Strided, not contiguous: every chunk is a uniform slice of the id space,
+  so hub rows (low ids in the power-law generator; sorted or community
+  ordered ids in real data) spread over all chunks, chunks cost the same to
+  sample, and each chunk's shuffle window mixes the whole graph."""
   total = bound_per_row * (inc.N + inc.E)
   n = max(1, -(-total // budget))
-  nodes = [(inc.N * c // n, inc.N * (c + 1) // n) for c in range(n)]
-  edges = [(inc.E * c // n, inc.E * (c + 1) // n) for c in range(n)]
-  return list(zip(nodes, edges))
+  return [(c, n) for c in range(n)]
 
 
 def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
@@ -140,7 +143,7 @@ def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
   if callable(bound_per_row):  # a bound that depends on the incidence
     bound_per_row = bound_per_row(inc)
   if chunk_sampler_fn is not None and bound_per_row * (inc.N + inc.E) > budget:
-    # the stream does not fit: sample and train row-range chunks in turn
+    # the stream does not fit: sample and train strided row chunks in turn
     chunks = _row_chunks(inc, bound_per_row, budget)
     seed = numpy_seed()
     prep = chunk_sampler_fn(inc, ctx)
@@ -165,7 +168,7 @@ def EmbedHg2vBoolean(hypergraph, dimension, num_neighbors=5, num_samples=200,
                      debug_summary_path=None, disable_pbar=False,
                      records_budget=None):
   """FOBE: BooleanSamples + BooleanModel (embedding.py:308-329). A stream of
-  more than `records_budget` records is sampled and trained in row-range
+  more than `records_budget` records is sampled and trained in strided row
   chunks (Hg2vModel.fit_streaming)."""
   sampler_fn = lambda inc, ctx: sample_fobe(inc, num_neighbors, num_samples,
                                             neg_samples, ctx=ctx)
@@ -175,12 +178,8 @@ def EmbedHg2vBoolean(hypergraph, dimension, num_neighbors=5, num_samples=200,
     q = [_quotas(w, n) for w in (inc.node_weight, inc.edge_weight)
          for n in (num_samples, neg_samples)]
 
-    def chunk(seed, nodes, edges):
-      nq, gnq, eq, geq = (np.zeros_like(x) for x in q)
-      nq[nodes[0]:nodes[1]] = q[0][nodes[0]:nodes[1]]
-      gnq[nodes[0]:nodes[1]] = q[1][nodes[0]:nodes[1]]
-      eq[edges[0]:edges[1]] = q[2][edges[0]:edges[1]]
-      geq[edges[0]:edges[1]] = q[3][edges[0]:edges[1]]
+    def chunk(seed, offset, stride):
+      nq, gnq, eq, geq = (row_class_quota(x, offset, stride) for x in q)
       neg = neg_samples > 0
       return ctx.sample_fobe(seed, num_neighbors, nq, eq, gnq if neg else None,
                              geq if neg else None)
@@ -205,16 +204,143 @@ def EmbedHg2vBoolean(hypergraph, dimension, num_neighbors=5, num_samples=200,
   return emb
 
 
+def _dist_backend_device(group):
+  import torch.distributed as dist
+  return "cpu" if dist.get_backend(group) == "gloo" else None
+
+
+def _all_gather_rows(part, r0, r1, n_rows, group, device):
+  """Every rank's row range [r0, r1) of an (n_rows x k) float32 table,
+  assembled on every rank (one all-gather of padded row blocks)."""
+  import torch
+  import torch.distributed as dist
+  world = dist.get_world_size(group)
+  k = part.shape[1]
+  dev = torch.device("cpu") if device == "cpu" else torch.device(
+      "cuda", torch.cuda.current_device())
+  lim = torch.tensor([r0, r1], dtype=torch.int64, device=dev)
+  lims = [torch.zeros_like(lim) for _ in range(world)]
+  dist.all_gather(lims, lim, group=group)
+  lims = [tuple(int(v) for v in t.cpu()) for t in lims]
+  m = max(b - a for a, b in lims)
+  buf = torch.zeros((max(m, 1), k), dtype=torch.float32, device=dev)
+  buf[:r1 - r0] = torch.from_numpy(np.ascontiguousarray(part, np.float32))
+  outs = [torch.empty_like(buf) for _ in range(world)]
+  dist.all_gather(outs, buf, group=group)
+  full = np.zeros((n_rows, k), np.float32)
+  for (a, b), t in zip(lims, outs):
+    full[a:b] = t[:b - a].cpu().numpy()
+  return full
+
+
+def _broadcast_seeds(n, group, device):
+  """n 62-bit seeds drawn from rank 0's numpy RandomState, on every rank."""
+  import torch
+  import torch.distributed as dist
+  dev = torch.device("cpu") if device == "cpu" else torch.device(
+      "cuda", torch.cuda.current_device())
+  t = torch.tensor([numpy_seed() for _ in range(n)], dtype=torch.int64,
+                   device=dev)
+  dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None
+                 else 0, group=group)
+  return [int(v) for v in t.cpu()]
+
+
+def hobe_sharded(inc, dimension, num_neighbors=5, num_samples=200,
+                 batch_size=256, epochs=10, group=None, records_budget=None,
+                 edge_ranges=1, alg_coords=None, ctx=None, stats=None):
+  """The HOBE pipeline over the ranks of a torch.distributed group, one GPU
+  per rank (EmbedHg2vAlgDist(..., group=) calls it):
+    1. alg-dist node-row sharded (algebraic_distance.alg_dist_sharded: the
+       edge-side partials all-reduced every iteration), from rank 0's
+       np.random draws (algebraic_distance.py:140-141), then one all-gather
+       of the node coordinates (N x 10 floats: 400 MB at C4) so every rank
+       holds the HOBE weights' inputs;
+    2. the stream in strided row chunks (_row_chunks), each sampled by the
+       ranks on strided shares of its rows and all-gathered in row order
+       (hg2v_sample.sharded_chunk_fn);
+    3. training as replicas (batch-256 Adagrad does not
+       partition): every rank trains the same model on the same chunks in
+       the same order (seeds broadcast from rank 0), Hg2vModel.fit_streaming
+       -- or, when the stream is one chunk, it is sampled once and fit() runs
+       the epochs on it, as the single-process path does.
+  `alg_coords` = (x, y) skips step 1 (tests: the sharded relaxation sums
+  partials in another order than one GPU, within 1e-4; steps 2-3 are then
+  bit-identical to the single-process call). Returns (node_tab, edge_tab)
+  without the padding row, identical on every rank."""
+  import torch.distributed as dist
+  from .algebraic_distance import _init_coords, alg_dist_sharded
+  from .hg2v_sample import sharded_chunk_fn
+  ctx = ctx or get_context()
+  dev = _dist_backend_device(group)
+  world = dist.get_world_size(group)
+  ctx.upload(inc)
+  if alg_coords is None:
+    x0 = y0 = None
+    if dist.get_rank(group) == 0:
+      x0, y0 = _init_coords(inc, 10)
+    import torch
+    tdev = torch.device("cpu") if dev == "cpu" else torch.device(
+        "cuda", torch.cuda.current_device())
+    bx = torch.from_numpy(np.ascontiguousarray(x0, np.float32)) \
+        if x0 is not None else torch.empty((inc.N, 10), dtype=torch.float32)
+    by = torch.from_numpy(np.ascontiguousarray(y0, np.float32)) \
+        if y0 is not None else torch.empty((inc.E, 10), dtype=torch.float32)
+    bx, by = bx.to(tdev), by.to(tdev)
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    dist.broadcast(bx, src=src, group=group)
+    dist.broadcast(by, src=src, group=group)
+    x0, y0 = bx.cpu().numpy(), by.cpu().numpy()
+    (r0, r1, xo), y, ms = alg_dist_sharded(ctx, inc, x0, y0, 20, group=group,
+                                           edge_ranges=edge_ranges,
+                                           stats=stats)
+    x = _all_gather_rows(xo, r0, r1, inc.N, group, dev)
+    if stats is not None:
+      stats["alg_ms"] = ms
+  else:
+    x, y = alg_coords
+  ctx.alg_set(x, y)
+  sample_seed, model_seed, fit_seed = _broadcast_seeds(3, group, dev)
+  budget = (RECORDS_BUDGET // 2 if world > 1 else RECORDS_BUDGET) \
+      if records_budget is None else records_budget
+  chunks = _row_chunks(inc, 2 * num_samples, budget)
+  fn = sharded_chunk_fn(inc, num_neighbors, num_samples, chunks, ctx=ctx,
+                        seed=sample_seed, kind="hobe", group=group, device=dev)
+  model = Hg2vModel(inc.N + 1, inc.E + 1, dimension, num_neighbors,
+                    _hgx.LOSS_MSE, _hgx.ACT_RELU, ctx=ctx, seed=model_seed)
+  if len(chunks) == 1:
+    fn(0)
+    model.fit(batch_size=batch_size, epochs=epochs, shuffle_seed=fit_seed)
+  else:
+    model.fit_streaming(fn, len(chunks), batch_size=batch_size, epochs=epochs,
+                        seed=fit_seed % (2**32))
+  node_w, edge_w = model.get_weights()
+  return node_w[1:], edge_w[1:]
+
+
 def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
                      num_samples=200, batch_size=256, epochs=10,
                      debug_summary_path=None, disable_pbar=False,
-                     records_budget=None):
+                     records_budget=None, group=None, edge_ranges=1):
   """HOBE: alg-dist (k=10, 20 iterations) + AlgebraicDistanceSamples +
   UnweightedFloatModel (embedding.py:389-416). `alpha` is accepted and, as
   in the reference, not used (_alpha_scale is called with alpha=0).
   A stream of more than `records_budget` records (RECORDS_BUDGET) is
-  sampled and trained in row-range chunks (Hg2vModel.fit_streaming)."""
+  sampled and trained in strided row chunks (Hg2vModel.fit_streaming).
+  `group` (a torch.distributed process group, e.g. group.WORLD under
+  torch.distributed.run, one GPU per rank): the multi-GPU pipeline
+  (hobe_sharded); every rank returns the same embedding."""
   del alpha
+  if group is not None:
+    inc = (hypergraph if isinstance(hypergraph, Incidence)
+           else Incidence.from_hypergraph(hypergraph))
+    nt, et = hobe_sharded(inc, dimension, num_neighbors, num_samples,
+                          batch_size, epochs, group=group,
+                          records_budget=records_budget,
+                          edge_ranges=edge_ranges)
+    emb = coords_to_embedding(inc, nt, et, dimension, "")
+    emb.method_name = "HG2V_ALG_DIST"
+    return emb
 
   def alg_dist(inc, ctx):
     x0 = np.random.random((inc.N, 10))  # algebraic_distance.py:140-141
@@ -230,11 +356,9 @@ def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
   def chunk_sampler_fn(inc, ctx):
     alg_dist(inc, ctx)
 
-    def chunk(seed, nodes, edges):
-      nq = np.zeros(inc.N, np.int32)
-      eq = np.zeros(inc.E, np.int32)
-      nq[nodes[0]:nodes[1]] = num_samples
-      eq[edges[0]:edges[1]] = num_samples
+    def chunk(seed, offset, stride):
+      nq = row_class_quota(np.full(inc.N, num_samples, np.int32), offset, stride)
+      eq = row_class_quota(np.full(inc.E, num_samples, np.int32), offset, stride)
       return ctx.sample_hobe(seed, num_neighbors, num_samples, node_q=nq,
                              edge_q=eq)
     return chunk

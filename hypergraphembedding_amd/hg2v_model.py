@@ -45,9 +45,12 @@ class Hg2vModel:
     embedding.py:277-284). chunk_fn(c) makes chunk c resident on the context
     and returns its record count; chunks must be the same records every
     epoch (the device samplers are keyed by seed and row, so re-sampling a
-    row range reproduces it). Per epoch the chunk order is shuffled and each
-    chunk's records are shuffled on the device (a windowed shuffle in place
-    of Keras' global one over records that never coexist); model state
+    row class reproduces it). Per epoch the chunk order is shuffled and each
+    chunk's records are shuffled on the device: a windowed shuffle in place
+    of Keras' global one over records that never coexist. The
+    chunks are strided row classes (embedding._row_chunks), each a uniform
+    slice of the graph, so a window mixes records of the whole id range;
+    model state
     carries across chunks (one-epoch hgx_train calls), the epoch loss is the
     record-weighted mean and EarlyStopping(min_delta, patience=0) applies to
     it. chunk_perms[ep][c] (optional) fixes a chunk's record order.

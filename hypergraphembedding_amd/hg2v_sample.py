@@ -105,27 +105,47 @@ def shard_range(n, world, rank):
   return n * rank // world, n * (rank + 1) // world
 
 
+def row_class_quota(quota, offset, stride):
+  """`quota` on the rows r = offset (mod stride), 0 elsewhere: one row class
+  of a strided split (fit_streaming chunks, sample_sharded ranks). A class
+  is a uniform slice of the id space, so hub rows (the power-law generator
+  numbers edges by popularity; real ids are often sorted or community
+  ordered) spread over every chunk and rank instead of filling the first."""
+  quota = np.asarray(quota, np.int32)
+  out = np.zeros_like(quota)
+  out[offset::stride] = quota[offset::stride]
+  return out
+
+
+# record column holding the row a record was sampled from, per kind block:
+# nn (ln), ee (le), ne of node rows (ln), ne of edge rows (re, swapped);
+# FOBE's negatives nn, ee, ee (the reference's repeated block), ne, ne
+_ROW_COL = {"hobe": (0, 1, 0, 3), "fobe": (0, 1, 0, 3, 0, 1, 1, 0, 3)}
+
+
 def sample_sharded(inc, num_neighbors, num_samples, ctx=None, seed=0,
                    kind="hobe", node_quota=None, edge_quota=None, group=None,
                    gather=True, device=None, rows=None):
   """Row-sharded sampling over the ranks of a torch.distributed group
   (sampling shards by row with no data-path collective).
 
-  `rows` = ((n_lo, n_hi), (e_lo, e_hi)) restricts the call to one row-range
-  chunk of the graph (fit_streaming, default: every row). Rank g samples
-  only its share of those rows (node rows [n0, n1), edge rows [e0, e1),
-  contiguous splits of the chunk; kind "hobe": AlgebraicDistanceSamples,
-  quota S per row unless quotas are given; kind "fobe": BooleanSamples with
-  the given per-row quotas): the other rows' quotas are 0. Every draw,
-  including the K neighbour draws of node-edge records, is keyed by (seed,
-  pattern or block, row, rank in the row), so with the same seed on every
-  rank the ranks' rows are exactly the rows a single process would draw. A
-  count all-gather gives every rank the kind-block sizes of every rank.
-  With `gather`, the per-rank streams are then all-gathered and laid out
-  kind block by kind block, ranks in row order inside each block: the
-  reference's record order (nn, ee, ne node rows, ne edge rows, ...) of the
-  chunk, the stream every training replica needs, identical to a
-  single-process call on the same rows.
+  `rows` = (offset, stride) restricts the call to one row class of a
+  strided split (fit_streaming chunk `offset` of `stride`; default: every
+  row): node rows and edge rows r = offset (mod stride). Rank g samples the
+  rows r = offset + g * stride (mod stride * world) of that class -- a
+  strided share, so the hub rows spread over the ranks -- (kind "hobe":
+  AlgebraicDistanceSamples, quota S per row unless quotas are given; kind
+  "fobe": BooleanSamples with the given per-row quotas); the other rows'
+  quotas are 0. Every draw, including the K neighbour draws of node-edge
+  records, is keyed by (seed, pattern or block, row, rank in the row), so
+  with the same seed on every rank the ranks' rows are exactly the rows a
+  single process would draw. A count all-gather gives every rank the
+  kind-block sizes of every rank. With `gather`, the per-rank streams are
+  then all-gathered and, kind block by kind block, merged back into row
+  order (a stable sort by each record's source row: within a row the
+  owning rank's order stays): the reference's record order (nn, ee, ne node
+  rows, ne edge rows, ...) of the class, the stream every training replica
+  needs, identical to a single-process call on the same rows.
 
   Collectives: RCCL on device buffers for a GPU device (the records never
   leave HBM), gloo through host arrays otherwise. Returns
@@ -136,18 +156,15 @@ def sample_sharded(inc, num_neighbors, num_samples, ctx=None, seed=0,
   ctx = ctx or get_context()
   world, rank = dist.get_world_size(group), dist.get_rank(group)
   K = num_neighbors
-  (nl, nh), (el, eh) = rows if rows is not None else ((0, inc.N), (0, inc.E))
-  assert 0 <= nl <= nh <= inc.N and 0 <= el <= eh <= inc.E
-  n0, n1 = (nl + x for x in shard_range(nh - nl, world, rank))
-  e0, e1 = (el + x for x in shard_range(eh - el, world, rank))
+  offset, stride = rows if rows is not None else (0, 1)
+  assert 0 <= offset < stride
   if node_quota is None:  # HOBE: S per row (hg2v_sample.py:659-703)
     assert kind == "hobe"
     node_quota = np.full(inc.N, num_samples, np.int32)
     edge_quota = np.full(inc.E, num_samples, np.int32)
-  nq = np.zeros(inc.N, np.int32)
-  eq = np.zeros(inc.E, np.int32)
-  nq[n0:n1] = np.asarray(node_quota, np.int32)[n0:n1]
-  eq[e0:e1] = np.asarray(edge_quota, np.int32)[e0:e1]
+  mine = (offset + rank * stride, stride * world)
+  nq = row_class_quota(node_quota, *mine)
+  eq = row_class_quota(edge_quota, *mine)
   if kind == "hobe":
     ctx.sample_hobe(seed, K, num_samples, node_q=nq, edge_q=eq)
   else:
@@ -202,6 +219,17 @@ def sample_sharded(inc, num_neighbors, num_samples, ctx=None, seed=0,
         fi[d:d + c] = gi[r][s0:s0 + c]
         ft[d:d + c] = gt[r][s0:s0 + c]
   del gi, gt, li, lt
+  if world > 1:
+    # the ranks' rows interleave: restore row order inside every block
+    cols = _ROW_COL[kind]
+    assert len(cols) == allsz.shape[1], (kind, allsz.shape)
+    for j, col in enumerate(cols):
+      b0, b1 = int(gbounds[j]), int(gbounds[j + 1])
+      if b1 - b0 > 1:
+        perm = torch.sort(fi[b0:b1, col], stable=True).indices
+        fi[b0:b1] = fi[b0:b1][perm]
+        ft[b0:b1] = ft[b0:b1][perm]
+        del perm
   if gpu:
     torch.cuda.synchronize(dev)
     # the gather buffers go back to the device before the context grows its
@@ -220,12 +248,13 @@ def sharded_chunk_fn(inc, num_neighbors, num_samples, chunks, ctx=None,
                      seed=0, kind="hobe", node_quota=None, edge_quota=None,
                      group=None, device=None):
   """chunk_fn for Hg2vModel.fit_streaming over row-sharded sampling: chunk c
-  (((n_lo, n_hi), (e_lo, e_hi)) = chunks[c]) is sampled by every rank on its
-  share of the chunk's rows and all-gathered, so each training replica holds
-  only one chunk's stream at a time (the reference materialises
-  the whole stream in host RAM, embedding.py:277-284). Returns the records
-  of the chunk now resident on ctx, identical to a single-process
-  sample of the same rows (sample_sharded)."""
+  (the row class (offset, stride) = chunks[c], embedding._row_chunks) is
+  sampled by every rank on its strided share of the class's rows and
+  all-gathered, so each training replica holds only one chunk's stream at a
+  time (the reference materialises the whole stream in host RAM,
+  embedding.py:277-284). Returns the records of the chunk now resident on
+  ctx, identical to a single-process sample of the same rows
+  (sample_sharded)."""
   ctx = ctx or get_context()
 
   def chunk(c):
@@ -398,4 +427,5 @@ __all__ = ["SimilarityRecord", "BooleanSamples", "AlgebraicDistanceSamples",
            "WeightedJaccardSamples", "sample_jaccard",
            "SamplesToModelInput", "ModelInputToArrays", "DeviceRecords",
            "sample_sharded", "sharded_chunk_fn", "shard_range",
+           "row_class_quota",
            "sample_fobe", "sample_hobe", "records_from_arrays"]

@@ -854,6 +854,16 @@ static void head_loss(int loss, float y, float yt, float *lv, float *g) {
   }
 }
 
+/* Duplicate-row gradient sums: 0 (default) in float32 in emit order, as a
+ * sequential TF CPU kernel would; 1 in float64, rounded to float32 once
+ * before the Adagrad step (TF leaves the order of its fp32 segment sums
+ * unspecified; the exact sum is the order-free member of that family, the
+ * one the device's fixed-point sums approach). Test infrastructure: the
+ * trainer parity tests report the distance between the two as the
+ * ambiguity the reference semantics leave. */
+static int g_dup_f64 = 0;
+void hgref_train_set_dup_f64(int on) { g_dup_f64 = on; }
+
 int hgref_train(int64_t n, int K, const int32_t *idx, const float *tgt, int d,
                 int64_t n_node_rows, int64_t n_edge_rows, float *ntab,
                 float *etab, float *nacc, float *eacc, int loss, int act,
@@ -863,6 +873,8 @@ int hgref_train(int64_t n, int K, const int32_t *idx, const float *tgt, int d,
   int R = 4 + 2 * K;
   float *gn = (float *)calloc((size_t)n_node_rows * d, sizeof(float));
   float *ge = (float *)calloc((size_t)n_edge_rows * d, sizeof(float));
+  double *gnd = g_dup_f64 ? (double *)calloc((size_t)n_node_rows * d, sizeof(double)) : NULL;
+  double *ged = g_dup_f64 ? (double *)calloc((size_t)n_edge_rows * d, sizeof(double)) : NULL;
   char *tn = (char *)calloc((size_t)n_node_rows, 1);
   char *te = (char *)calloc((size_t)n_edge_rows, 1);
   int64_t *touched_n = (int64_t *)malloc(sizeof(int64_t) * (size_t)batch * R + 8);
@@ -914,45 +926,66 @@ int hgref_train(int64_t n, int K, const int32_t *idx, const float *tgt, int d,
         float dP = g3 * Q / (float)K, dQ = g3 * P / (float)K;
 #define TOUCH_N(row) do { if (!tn[row]) { tn[row] = 1; touched_n[ntn++] = row; } } while (0)
 #define TOUCH_E(row) do { if (!te[row]) { te[row] = 1; touched_e[nte++] = row; } } while (0)
-        float *gl = gn + (int64_t)ln * d, *gr = gn + (int64_t)rn * d;
+#define ACC(g, gd, row, i, v)                                             \
+  do {                                                                    \
+    float v_ = (v);                                                       \
+    if (gd) gd[(int64_t)(row) * d + (i)] += (double)v_;                   \
+    else g[(int64_t)(row) * d + (i)] += v_;                               \
+  } while (0)
         TOUCH_N(ln); TOUCH_N(rn);
-        for (int i = 0; i < d; i++) { gl[i] += dz1 * Nr[i]; gr[i] += dz1 * Nl[i]; }
-        float *hl = ge + (int64_t)le * d, *hr = ge + (int64_t)re * d;
+        for (int i = 0; i < d; i++) {
+          ACC(gn, gnd, ln, i, dz1 * Nr[i]);
+          ACC(gn, gnd, rn, i, dz1 * Nl[i]);
+        }
         TOUCH_E(le); TOUCH_E(re);
-        for (int i = 0; i < d; i++) { hl[i] += dz2 * Er[i]; hr[i] += dz2 * El[i]; }
+        for (int i = 0; i < d; i++) {
+          ACC(ge, ged, le, i, dz2 * Er[i]);
+          ACC(ge, ged, re, i, dz2 * El[i]);
+        }
         for (int t = 0; t < K; t++) {
           float da = dP * act_d(act, a_k[t], sa[t]);
-          float *gk = gn + (int64_t)nnk[t] * d;
           const float *Nk = ntab + (int64_t)nnk[t] * d;
           TOUCH_N(nnk[t]);
-          for (int i = 0; i < d; i++) { gk[i] += da * Nl[i]; gl[i] += da * Nk[i]; }
+          for (int i = 0; i < d; i++) {
+            ACC(gn, gnd, nnk[t], i, da * Nl[i]);
+            ACC(gn, gnd, ln, i, da * Nk[i]);
+          }
           float db = dQ * act_d(act, b_k[t], sb[t]);
-          float *hk = ge + (int64_t)nek[t] * d;
           const float *Ek = etab + (int64_t)nek[t] * d;
           TOUCH_E(nek[t]);
-          for (int i = 0; i < d; i++) { hk[i] += db * Er[i]; hr[i] += db * Ek[i]; }
+          for (int i = 0; i < d; i++) {
+            ACC(ge, ged, nek[t], i, db * Er[i]);
+            ACC(ge, ged, re, i, db * Ek[i]);
+          }
         }
+#undef ACC
       }
       /* Adagrad over touched rows (untouched rows have g == 0: no-op). */
       for (int64_t u = 0; u < ntn; u++) {
         int64_t row = touched_n[u];
         float *p = ntab + row * d, *a = nacc + row * d, *g = gn + row * d;
+        double *gd = gnd ? gnd + row * d : NULL;
         for (int i = 0; i < d; i++) {
-          float na = a[i] + g[i] * g[i];
+          float gi = gd ? (float)gd[i] : g[i];
+          float na = a[i] + gi * gi;
           a[i] = na;
-          p[i] = p[i] - (lr * g[i]) / (sqrtf(na) + eps);
+          p[i] = p[i] - (lr * gi) / (sqrtf(na) + eps);
           g[i] = 0.0f;
+          if (gd) gd[i] = 0.0;
         }
         tn[row] = 0;
       }
       for (int64_t u = 0; u < nte; u++) {
         int64_t row = touched_e[u];
         float *p = etab + row * d, *a = eacc + row * d, *g = ge + row * d;
+        double *gd = ged ? ged + row * d : NULL;
         for (int i = 0; i < d; i++) {
-          float na = a[i] + g[i] * g[i];
+          float gi = gd ? (float)gd[i] : g[i];
+          float na = a[i] + gi * gi;
           a[i] = na;
-          p[i] = p[i] - (lr * g[i]) / (sqrtf(na) + eps);
+          p[i] = p[i] - (lr * gi) / (sqrtf(na) + eps);
           g[i] = 0.0f;
+          if (gd) gd[i] = 0.0;
         }
         te[row] = 0;
       }
@@ -968,7 +1001,8 @@ int hgref_train(int64_t n, int K, const int32_t *idx, const float *tgt, int d,
     }
   }
   if (epochs_run) *epochs_run = ep;
-  free(gn); free(ge); free(tn); free(te); free(touched_n); free(touched_e);
+  free(gn); free(ge); free(gnd); free(ged); free(tn); free(te);
+  free(touched_n); free(touched_e);
   free(a_k); free(b_k); free(sa); free(sb);
   return 0;
 }

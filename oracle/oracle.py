@@ -82,6 +82,7 @@ def lib():
     L.hgref_centroids.restype = _i64
     L.hgref_centroids.argtypes = [_i64, _i32p, _i32p, _i64, _i32p, _i32p,
                                   _f32p, _i64p, _vp, _vp]
+    L.hgref_train_set_dup_f64.argtypes = [_int]
     L.hgref_norm32.restype = ctypes.c_float
     L.hgref_norm32.argtypes = [_f32p, _f32p, _int, _int]
     L.hgref_norm64.restype = ctypes.c_double
@@ -255,9 +256,12 @@ ACT_SIGMOID, ACT_RELU = 0, 1
 
 def train(idx, tgt, K, node_tab, edge_tab, loss, act, batch=256, lr=0.01,
           eps=1e-7, max_epochs=10, perms=None, min_delta=1e-3, node_acc=None,
-          edge_acc=None):
+          edge_acc=None, dup_f64=False):
   """Keras-semantics Adagrad restatement. Tables are float32 (rows = max+2,
-  row 0 = padding). Returns (node_tab, edge_tab, epoch_losses)."""
+  row 0 = padding). dup_f64: a row's gradients summed in float64 and
+  rounded once (the exact member of the fp32 summation orders TF allows)
+  instead of float32 in emit order. Returns (node_tab, edge_tab,
+  epoch_losses, node_acc, edge_acc)."""
   idx = np.ascontiguousarray(idx, np.int32)
   tgt = np.ascontiguousarray(tgt, np.float32)
   nt = np.ascontiguousarray(node_tab, np.float32).copy()
@@ -276,6 +280,7 @@ def train(idx, tgt, K, node_tab, edge_tab, loss, act, batch=256, lr=0.01,
     pp = perms.ctypes.data
   losses = np.zeros(max(max_epochs, 1), np.float32)
   ran = ctypes.c_int(0)
+  lib().hgref_train_set_dup_f64(1 if dup_f64 else 0)
   lib().hgref_train(n, K, idx, tgt, d, nt.shape[0], et.shape[0], nt, et, na,
                     ea, loss, act, batch, lr, eps, max_epochs, pp, min_delta,
                     losses, ctypes.byref(ran))

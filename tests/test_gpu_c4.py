@@ -176,16 +176,24 @@ def test_c4_hobe_d256_epoch_deterministic_and_learning(ctx, g):
   _cache["hobe"] = ctx.model_get()
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 def test_c4_d256_window_vs_oracle(ctx, g):
   """Trainer parity on the real C4 stream: a 2M-record
   window of a shuffled epoch of the 10M/5M power-law HOBE stream, d = 256,
   on full-size tables (10M + 1 and 5M + 1 rows, device init), against
   hgref_train with the same initial rows and batch order. The hub edges
   make most batches take the MULTI pending-slot form (records naming two
-  rows the previous batch deferred); bar: max-abs <= 1e-5 on every touched
-  row, loss rtol 1e-4. The oracle trains compact tables holding only the
-  touched rows (row ids relabelled; the arithmetic is independent of ids)."""
+  rows the previous batch deferred). The oracle trains compact tables
+  holding only the touched rows (row ids relabelled; the arithmetic is
+  independent of ids).
+
+  Bar. Keras/TF leave the fp32 order of a row's duplicate-gradient sum
+  unspecified; over 7,813 hub-heavy batches the two oracle members -- fp32
+  in emit order and the exact (float64) sum -- themselves drift apart by
+  ~1e-5 (oracle/hgref.c hgref_train_set_dup_f64). The device sums
+  duplicates in 2^-44 fixed point (exact up to that quantum), so it is held
+  to <= 1e-5 max-abs against the exact-sum oracle on every touched row, and
+  to the oracle's own ambiguity against the fp32 one; losses rtol 1e-4."""
   from hypergraphembedding_amd import _hgx
   n, _, _ = _sample(ctx, g)
   idx, tgt = ctx.records_get()
@@ -213,13 +221,22 @@ def test_c4_d256_window_vs_oracle(ctx, g):
   cidx = idx.copy()
   cidx[:, ncols] = np.searchsorted(un, idx[:, ncols])
   cidx[:, ecols] = np.searchsorted(ue, idx[:, ecols])
-  ont, oet, ol, _, _ = O.train(cidx, tgt, K, nt0, et0, O.LOSS_MSE, O.ACT_RELU,
-                               batch=256, max_epochs=1, perms=perms,
-                               min_delta=-1e30)
-  assert np.allclose(gl, ol, rtol=1e-4), (gl, ol)
-  dn, de = np.abs(gn - ont).max(), np.abs(ge - oet).max()
-  print(f"max-abs node {dn:.3e} edge {de:.3e}")
-  assert dn <= 1e-5 and de <= 1e-5
+  del idx
+  res = {}
+  for f64 in (True, False):
+    ont, oet, ol, _, _ = O.train(cidx, tgt, K, nt0, et0, O.LOSS_MSE,
+                                 O.ACT_RELU, batch=256, max_epochs=1,
+                                 perms=perms, min_delta=-1e30, dup_f64=f64)
+    assert np.allclose(gl, ol, rtol=1e-4), (f64, gl, ol)
+    res[f64] = (ont, oet)
+  dev = {f64: max(np.abs(gn - res[f64][0]).max(), np.abs(ge - res[f64][1]).max())
+         for f64 in (True, False)}
+  amb = max(np.abs(res[True][0] - res[False][0]).max(),
+            np.abs(res[True][1] - res[False][1]).max())
+  print(f"max-abs device vs exact-sum oracle {dev[True]:.3e}, vs fp32 oracle "
+        f"{dev[False]:.3e}; the two oracles apart {amb:.3e}")
+  assert dev[True] <= 1e-5
+  assert dev[False] <= 2 * amb + 1e-6
   assert not np.array_equal(gn, nt0) and not np.array_equal(ge, et0)
 
 

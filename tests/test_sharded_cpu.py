@@ -191,10 +191,11 @@ def _chunk_worker(rank, world, port, out_path, n_chunks):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_chunked_sharded_sampling_equals_single_process(tmp_path, world):
-  """Row-range chunks sampled row-sharded over gloo ranks and all-gathered:
-  every rank holds, chunk by chunk, exactly the stream (ids, neighbour
-  lists, targets, kind-block order) a single process samples for that
-  chunk's rows -- so a replica never holds more than one chunk."""
+  """Strided row chunks sampled over gloo ranks (each rank a strided share
+  of the chunk's rows) and all-gathered: every rank holds, chunk by chunk,
+  exactly the stream (ids, neighbour lists, targets, kind-block order, rows
+  in order inside each block) a single process samples for that chunk's
+  rows -- so a replica never holds more than one chunk."""
   import torch.multiprocessing as mp
   sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
   from shard_emu import SampleEmu
@@ -207,10 +208,11 @@ def test_chunked_sharded_sampling_equals_single_process(tmp_path, world):
   emu = SampleEmu()
   emu.upload(inc)
   seen = 0
-  for c, ((n0, n1), (e0, e1)) in enumerate(chunks):
-    nq = np.zeros(inc.N, np.int32)
-    eq = np.zeros(inc.E, np.int32)
-    nq[n0:n1], eq[e0:e1] = 6, 6
+  from hypergraphembedding_amd.hg2v_sample import row_class_quota
+  for c, (off, stride) in enumerate(chunks):
+    assert (off, stride) == (c, 3)
+    nq = row_class_quota(np.full(inc.N, 6, np.int32), off, stride)
+    eq = row_class_quota(np.full(inc.E, 6, np.int32), off, stride)
     n = emu.sample_hobe(77, 3, 6, node_q=nq, edge_q=eq)
     ridx, rtgt = emu.records_get()
     seen += n
