@@ -49,6 +49,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MFMA_F32_PEAK_TFLOPS = 157.3  # f32-in MFMA = the FP32 vector peak (same guide)
 METRIC = ("training samples/sec + alg-dist SpMV GB/s, HOBE dim=128 at "
           "1/2/4/8 MI355X")
 PMC_TRAIN = os.path.join(ROOT, "profiles", "r03_final", "pmc_train.json")
@@ -70,6 +71,9 @@ def parse():
   p.add_argument("--cpu-records", type=int, default=4_000_000,
                  help="records of the bounded CPU-baseline slice")
   p.add_argument("--no-cpu", action="store_true")
+  p.add_argument("--no-c5", action="store_true",
+                 help="skip the C5 combiner leg (inside the C4 leg)")
+  p.add_argument("--c5-positives", type=int, default=1_000_000)
   p.add_argument("--no-c4", action="store_true",
                  help="skip the power-law 10M/5M measurements")
   p.add_argument("--no-extra", action="store_true",
@@ -607,7 +611,73 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
                   "algorithmic bytes of the GPU line",
         "vs_gpu": round((ca_s / 3 * 1e3) / (ms4 / args.alg_iters), 1)}
   c4["hobe_d256"] = hobe4
+  if not args.no_c5:
+    if rank == 0:
+      c4["c5_combiner"] = bench_c5(args, ctx, big)
+    sync()
   return c4
+
+
+def bench_c5(args, ctx, big):
+  """C5 (configs[4]) combiner: CombineEmbeddings' N_E_SUPERVISED MLP
+  (combine_embeddings_util.py:78-174) on the 10M/5M graph's own tables --
+  [FOBE | HOBE] d = 256 each (HOBE: the table the leg above trained; FOBE:
+  its uniform(-0.05, 0.05) init) -- and samples of the graph (a seeded
+  subset of the incidences labelled 1 plus 5x as many Python-random-exact
+  missing pairs, combine_embeddings_util.incidence_samples). One epoch
+  timed after a warm epoch: samples/s and TFLOP/s of the fp32 MFMA engine."""
+  from hypergraphembedding_amd import _hgx
+  from hypergraphembedding_amd.combine_embeddings_util import incidence_samples
+  import random as _random
+  d = 256
+  t = time.perf_counter()
+  hn, he = ctx.model_get()
+  rs = np.random.RandomState(21)
+  nt = np.empty((big.N, 2 * d), np.float32)
+  et = np.empty((big.E, 2 * d), np.float32)
+  nt[:, :d] = rs.uniform(-0.05, 0.05, (big.N, d))
+  et[:, :d] = rs.uniform(-0.05, 0.05, (big.E, d))
+  nt[:, d:] = hn[1:]
+  et[:, d:] = he[1:]
+  del hn, he
+  tables_s = time.perf_counter() - t
+  _random.seed(5)
+  t = time.perf_counter()
+  nr, er, lab = incidence_samples(big, args.c5_positives, np.random.RandomState(6))
+  samples_s = time.perf_counter() - t
+  mlp = _hgx.Mlp(ctx, _hgx.MLP_NE_SUPERVISED, 2 * d, d)
+  lims = [np.sqrt(6.0 / (k + n)) for k, n in mlp.shapes]
+  mlp.set_weights(np.concatenate([np.concatenate([rs.uniform(-l, l, k * n),
+                                                  np.zeros(n)])
+                                  for l, (k, n) in zip(lims, mlp.shapes)]
+                                 ).astype(np.float32))
+  mlp.set_tables(nt, et)
+  del nt, et
+  mlp.set_samples(nr, er, lab)
+  runs = []
+  for ep in range(2):
+    ctx.synchronize()
+    t = time.perf_counter()
+    mlp.fit(batch=args.batch, max_epochs=1, min_delta=-1e30, seed=ep + 1)
+    ctx.synchronize()
+    wall = time.perf_counter() - t
+    st = mlp.stats()
+    runs.append((st["ms"], st["samples"], st["flops"], wall))
+  mlp.close()
+  ms, n, flops, wall = runs[-1]
+  sps = n / (ms / 1e3)
+  tf = flops / (ms / 1e3) / 1e12
+  return {"workload": "N_E_SUPERVISED combiner, in = 512 ([FOBE | HOBE] "
+                      "d = 256), d = 256, batch 256, tables of every node "
+                      f"and edge of the 10M/5M graph, {n} samples "
+                      f"({args.c5_positives} incidences + 5x missing pairs)",
+          "samples": n, "epoch_ms": round(ms, 1),
+          "samples_per_s": round(sps, 1), "tflops": round(tf, 2),
+          "mfma_f32_peak_tflops": MFMA_F32_PEAK_TFLOPS,
+          "frac_of_mfma_peak": round(tf / MFMA_F32_PEAK_TFLOPS, 4),
+          "c4_epoch_s_implied": round(1.2e9 / sps, 1),
+          "host_prep_s": {"tables": round(tables_s, 2),
+                          "samples": round(samples_s, 2)}}
 
 
 if __name__ == "__main__":

@@ -42,7 +42,10 @@ COMBINATION_OPTIONS = [
 def CombineEmbeddings(args, hypergraph, embeddings, disable_pbar=False):
   """embedding.py:51-78: CONCATENATE, or the node/edge-classifier MLP
   combiners (N_E_SUPERVISED, N_E_SEMI_SUPERVISED) on the MI355X dense-MLP
-  engine (combine_embeddings_util.py)."""
+  engine (combine_embeddings_util.py). `hypergraph` may be an Incidence
+  and the embeddings ShardedEmbeddings (C5 scale); the optional
+  `args.combination_kwargs` dict (not in the reference) reaches the
+  classifier combiner (epochs, max_positives)."""
   assert len(embeddings) >= 1
   if len(embeddings) == 1:
     return embeddings[0]
@@ -54,7 +57,8 @@ def CombineEmbeddings(args, hypergraph, embeddings, disable_pbar=False):
     comb = CombineEmbeddingsViaNodeEdgeClassifier(
         hypergraph, embeddings, args.embedding_dimension,
         with_auto_encoder=strategy == "N_E_SEMI_SUPERVISED",
-        disable_pbar=disable_pbar)
+        disable_pbar=disable_pbar,
+        **(getattr(args, "combination_kwargs", None) or {}))
   else:
     raise ValueError("Args contains an illegal embedding-combination-strategy")
   comb.method_name = "_".join(args.embedding_method)
@@ -62,10 +66,18 @@ def CombineEmbeddings(args, hypergraph, embeddings, disable_pbar=False):
 
 
 def Embed(args, hypergraph, shortcut_embeddings=None):
-  """embedding.py:81-107."""
-  assert min(len(hypergraph.node), len(hypergraph.edge)) > \
-      args.embedding_dimension
+  """embedding.py:81-107. `hypergraph` is the reference's Hypergraph
+  message or an Incidence (proto_native.read_incidence: C4/C5 inputs Python
+  protobuf cannot hold). The optional `args.embedding_kwargs` dict (not in
+  the reference) maps a method name to extra keyword arguments of its
+  embedder (e.g. epochs, records_budget, row quotas for bounded runs)."""
+  if isinstance(hypergraph, Incidence):
+    n_nodes, n_edges = hypergraph.N, hypergraph.E
+  else:
+    n_nodes, n_edges = len(hypergraph.node), len(hypergraph.edge)
+  assert min(n_nodes, n_edges) > args.embedding_dimension
   assert len(args.embedding_method) >= 1
+  extra = getattr(args, "embedding_kwargs", None) or {}
   embeddings = []
   for method in args.embedding_method:
     if shortcut_embeddings is not None and method in shortcut_embeddings:
@@ -73,13 +85,11 @@ def Embed(args, hypergraph, shortcut_embeddings=None):
       continue
     log.info("Embedding using method %s with %i dim", method,
              args.embedding_dimension)
+    kw = dict(extra.get(method, {}))
     if getattr(args, "embedding_debug_summary", None):
-      embeddings.append(EMBEDDING_OPTIONS[method](
-          hypergraph, args.embedding_dimension,
-          debug_summary_path=args.embedding_debug_summary))
-    else:
-      embeddings.append(EMBEDDING_OPTIONS[method](hypergraph,
-                                                  args.embedding_dimension))
+      kw["debug_summary_path"] = args.embedding_debug_summary
+    embeddings.append(EMBEDDING_OPTIONS[method](hypergraph,
+                                                args.embedding_dimension, **kw))
   embedding = CombineEmbeddings(args, hypergraph, embeddings)
   log.info("Embedding contains %i node and %i edge vectors",
            len(embedding.node), len(embedding.edge))
@@ -110,6 +120,17 @@ def _plot_distributions(path, records):
 # Records resident at once before the skeleton streams the record stream in
 # row chunks (68 B per record at K = 5: 2^30 records = 73 GB of HBM).
 RECORDS_BUDGET = 1 << 30
+
+
+def _bound(inc, per_row, row_quota, per_quota):
+  """Record bound per row: `per_row`, or with row quotas (node, edge) their
+  total times `per_quota` spread over the rows (the streaming decision and
+  the chunk count only use bound x rows)."""
+  if row_quota is None:
+    return per_row
+  tot = per_quota * (int(np.sum(row_quota[0], dtype=np.int64)) +
+                     int(np.sum(row_quota[1], dtype=np.int64)))
+  return max(1, -(-tot // max(inc.N + inc.E, 1)))
 
 
 def _row_chunks(inc, bound_per_row, budget):
@@ -166,17 +187,23 @@ def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
 def EmbedHg2vBoolean(hypergraph, dimension, num_neighbors=5, num_samples=200,
                      batch_size=256, epochs=10, neg_samples=0,
                      debug_summary_path=None, disable_pbar=False,
-                     records_budget=None):
+                     records_budget=None, row_quota=None):
   """FOBE: BooleanSamples + BooleanModel (embedding.py:308-329). A stream of
   more than `records_budget` records is sampled and trained in strided row
-  chunks (Hg2vModel.fit_streaming)."""
+  chunks (Hg2vModel.fit_streaming). row_quota = (node quotas, edge quotas)
+  (not in the reference) replaces int(weight * S) per row: bounded runs."""
   sampler_fn = lambda inc, ctx: sample_fobe(inc, num_neighbors, num_samples,
-                                            neg_samples, ctx=ctx)
+                                            neg_samples, ctx=ctx,
+                                            row_quota=row_quota)
 
   def chunk_sampler_fn(inc, ctx):
     ctx.upload(inc)
-    q = [_quotas(w, n) for w in (inc.node_weight, inc.edge_weight)
-         for n in (num_samples, neg_samples)]
+    if row_quota is not None:
+      q = [np.asarray(row_quota[0], np.int32), _quotas(inc.node_weight, neg_samples),
+           np.asarray(row_quota[1], np.int32), _quotas(inc.edge_weight, neg_samples)]
+    else:
+      q = [_quotas(w, n) for w in (inc.node_weight, inc.edge_weight)
+           for n in (num_samples, neg_samples)]
 
     def chunk(seed, offset, stride):
       nq, gnq, eq, geq = (row_class_quota(x, offset, stride) for x in q)
@@ -192,7 +219,8 @@ def EmbedHg2vBoolean(hypergraph, dimension, num_neighbors=5, num_samples=200,
   def bound_per_row(inc):
     wmax = float(max(np.max(inc.node_weight, initial=0.0),
                      np.max(inc.edge_weight, initial=0.0), 0.0))
-    return int(wmax * 2 * num_samples) + int(wmax * 3 * neg_samples) + 2
+    neg = int(wmax * 3 * neg_samples)
+    return _bound(inc, int(wmax * 2 * num_samples) + 2, row_quota, 2) + neg
 
   emb = _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors,
                                  sampler_fn, _hgx.LOSS_KLD, _hgx.ACT_SIGMOID,
@@ -321,7 +349,8 @@ def hobe_sharded(inc, dimension, num_neighbors=5, num_samples=200,
 def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
                      num_samples=200, batch_size=256, epochs=10,
                      debug_summary_path=None, disable_pbar=False,
-                     records_budget=None, group=None, edge_ranges=1):
+                     records_budget=None, group=None, edge_ranges=1,
+                     row_quota=None):
   """HOBE: alg-dist (k=10, 20 iterations) + AlgebraicDistanceSamples +
   UnweightedFloatModel (embedding.py:389-416). `alpha` is accepted and, as
   in the reference, not used (_alpha_scale is called with alpha=0).
@@ -329,9 +358,12 @@ def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
   sampled and trained in strided row chunks (Hg2vModel.fit_streaming).
   `group` (a torch.distributed process group, e.g. group.WORLD under
   torch.distributed.run, one GPU per rank): the multi-GPU pipeline
-  (hobe_sharded); every rank returns the same embedding."""
+  (hobe_sharded); every rank returns the same embedding. row_quota =
+  (node quotas, edge quotas) (not in the reference) replaces S on every
+  row: bounded runs (rows with quota 0 are not sampled)."""
   del alpha
   if group is not None:
+    assert row_quota is None, "row_quota is a single-process option"
     inc = (hypergraph if isinstance(hypergraph, Incidence)
            else Incidence.from_hypergraph(hypergraph))
     nt, et = hobe_sharded(inc, dimension, num_neighbors, num_samples,
@@ -351,14 +383,18 @@ def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
 
   def sampler_fn(inc, ctx):
     alg_dist(inc, ctx)
-    return sample_hobe(inc, num_neighbors, num_samples, ctx=ctx)
+    return sample_hobe(inc, num_neighbors, num_samples, ctx=ctx,
+                       row_quota=row_quota)
 
   def chunk_sampler_fn(inc, ctx):
     alg_dist(inc, ctx)
+    full = (row_quota if row_quota is not None else
+            (np.full(inc.N, num_samples, np.int32),
+             np.full(inc.E, num_samples, np.int32)))
 
     def chunk(seed, offset, stride):
-      nq = row_class_quota(np.full(inc.N, num_samples, np.int32), offset, stride)
-      eq = row_class_quota(np.full(inc.E, num_samples, np.int32), offset, stride)
+      nq = row_class_quota(full[0], offset, stride)
+      eq = row_class_quota(full[1], offset, stride)
       return ctx.sample_hobe(seed, num_neighbors, num_samples, node_q=nq,
                              edge_q=eq)
     return chunk
@@ -368,7 +404,8 @@ def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
                                  sampler_fn, _hgx.LOSS_MSE, _hgx.ACT_RELU,
                                  batch_size, epochs, debug_summary_path,
                                  disable_pbar, chunk_sampler_fn=chunk_sampler_fn,
-                                 bound_per_row=2 * num_samples,
+                                 bound_per_row=lambda inc: _bound(
+                                     inc, 2 * num_samples, row_quota, 2),
                                  records_budget=records_budget)
   emb.method_name = "HG2V_ALG_DIST"
   return emb

@@ -69,13 +69,18 @@ def records_from_arrays(idx, tgt, K):
 
 
 def sample_fobe(inc, num_neighbors, num_samples, neg_samples=0, ctx=None,
-                seed=None):
-  """BooleanSamples on the device; returns DeviceRecords."""
+                seed=None, row_quota=None):
+  """BooleanSamples on the device; returns DeviceRecords. row_quota =
+  (node quotas, edge quotas) replaces int(weight * S) per row (bounded
+  runs; rows with quota 0 are not sampled)."""
   assert num_neighbors >= 1
   ctx = ctx or get_context()
   ctx.upload(inc)
-  nq = _quotas(inc.node_weight, num_samples)
-  eq = _quotas(inc.edge_weight, num_samples)
+  if row_quota is not None:
+    nq, eq = (np.asarray(q, np.int32) for q in row_quota)
+  else:
+    nq = _quotas(inc.node_weight, num_samples)
+    eq = _quotas(inc.edge_weight, num_samples)
   nnq = neq = None
   if neg_samples > 0:
     nnq = _quotas(inc.node_weight, neg_samples)
@@ -86,17 +91,22 @@ def sample_fobe(inc, num_neighbors, num_samples, neg_samples=0, ctx=None,
 
 
 def sample_hobe(inc, num_neighbors, num_samples, ctx=None, seed=None,
-                alg_coords=None):
+                alg_coords=None, row_quota=None):
   """AlgebraicDistanceSamples on the device (alg coords must be resident on
-  ctx, e.g. from algebraic_distance.AlgebraicDistance, or given)."""
+  ctx, e.g. from algebraic_distance.AlgebraicDistance, or given). row_quota
+  = (node quotas, edge quotas) instead of S on every row (bounded runs)."""
   assert num_neighbors >= 0
   assert num_samples >= 0
   ctx = ctx or get_context()
   if alg_coords is not None:
     ctx.upload(inc)
     ctx.alg_set(*alg_coords)
-  n = ctx.sample_hobe(numpy_seed() if seed is None else seed, num_neighbors,
-                      num_samples)
+  seed = numpy_seed() if seed is None else seed
+  if row_quota is not None:
+    n = ctx.sample_hobe(seed, num_neighbors, num_samples,
+                        node_q=row_quota[0], edge_q=row_quota[1])
+  else:
+    n = ctx.sample_hobe(seed, num_neighbors, num_samples)
   return DeviceRecords(ctx, inc, n, num_neighbors)
 
 

@@ -363,3 +363,47 @@ def test_c5_combiner_full_size_tables(ctx, g):
   jn = mlp.predict(1, rs.randint(0, g.N, 4096).astype(np.int32), None)
   assert jn.shape == (4096, D) and np.isfinite(jn).all()
   mlp.close()
+
+
+@pytest.mark.timeout(1200)
+def test_c5_embed_operator_surface_full_graph(g):
+  """the reference's operator surface at C4/C5 size.
+  Embed(args, Incidence) with [HG2V_BOOLEAN, HG2V_ALG_DIST] at d = 256 and
+  the default N_E_SUPERVISED combination on the 10M/5M graph, bounded by
+  the extension kwargs (one epoch per embedder on the 0.5% row quota, one
+  combiner epoch on 340k positives + 1.7M missing pairs drawn over the
+  whole graph): every embedder returns a ShardedEmbedding (10M x 256 is
+  past protobuf's limit), the combiner takes them as tables, and its host
+  preparation (gathering 10M + 5M rows of both embeddings, concatenating,
+  positives from the CSR, the Python-random-exact missing pairs) stays
+  under 60 s."""
+  import random
+  import time
+  from types import SimpleNamespace
+  from hypergraphembedding_amd import Embed, combine_embeddings_util as C
+  from hypergraphembedding_amd.proto_native import ShardedEmbedding
+  nq, eq = _quotas(g)
+  kw = dict(epochs=1, row_quota=(nq, eq))
+  args = SimpleNamespace(
+      embedding_dimension=D, embedding_method=["HG2V_BOOLEAN", "HG2V_ALG_DIST"],
+      embedding_combination_strategy="N_E_SUPERVISED",
+      embedding_kwargs={"HG2V_BOOLEAN": kw, "HG2V_ALG_DIST": kw},
+      combination_kwargs=dict(epochs=1, max_positives=340_000))
+  np.random.seed(0)
+  random.seed(0)
+  t = time.time()
+  emb = Embed(args, g)
+  total = time.time() - t
+  st = dict(C.last_timings)
+  print(f"Embed C5: {total:.1f} s; combiner {st}")
+  assert isinstance(emb, ShardedEmbedding)
+  assert emb.dim == D and emb.method_name == "HG2V_BOOLEAN_HG2V_ALG_DIST"
+  assert np.array_equal(emb.node_ids, g.node_ids)
+  assert np.array_equal(emb.edge_ids, g.edge_ids)
+  assert emb.node_tab.shape == (g.N, D) and emb.edge_tab.shape == (g.E, D)
+  rs = np.random.RandomState(3)
+  for tab in (emb.node_tab, emb.edge_tab):
+    rows = tab[rs.choice(tab.shape[0], 10_000, replace=False)]
+    assert np.isfinite(rows).all() and rows.min() >= 0 and rows.max() <= 1
+  assert st["samples"] >= 2_000_000
+  assert st["prep_s"] < 60

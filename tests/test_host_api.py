@@ -273,3 +273,30 @@ def test_combine_concatenate():
   args.embedding_combination_strategy = "NOT_A_STRATEGY"
   with pytest.raises(ValueError):
     CombineEmbeddings(args, h, embs)
+
+
+def test_incidence_samples_equal_the_proto_path():
+  """The combiner's array-level samples (positives straight from the CSR,
+  SampleMissingConnections' native draws fed the CSR arrays) equal the
+  proto path's (node map order, Python-random-exact draws) on the proto of
+  the same graph with ascending ids -- the C5 preparation without a
+  Python loop per incidence."""
+  import random
+  from hypergraphembedding_amd import _hgx
+  from hypergraphembedding_amd.combine_embeddings_util import (
+      incidence_samples, proto_samples)
+  from hypergraphembedding_amd.hypergraph_util import CreateRandomHyperGraph
+  from hypergraphembedding_amd.proto import Hypergraph
+  random.seed(3)
+  hg0 = CreateRandomHyperGraph(300, 80, 0.03)
+  inc = Incidence.from_hypergraph(hg0)
+  hg = Hypergraph()
+  hg.ParseFromString(_hgx.write_hypergraph_bytes(inc).tobytes())
+  assert list(hg.node) == sorted(hg.node)
+  for seed in (0, 1):
+    random.seed(seed)
+    a = incidence_samples(inc)
+    random.seed(seed)
+    b = proto_samples(hg, list(hg.node), list(hg.edge))
+    for x, y in zip(a, b):
+      assert np.array_equal(x, y)
