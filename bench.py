@@ -474,6 +474,16 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
     ctx.alg_run(args.alg_iters)
     ms4 = ctx.alg_stats()[0]
   gbps4 = b_iter4 * args.alg_iters / (ms4 * 1e-3) / 1e9
+  # the ceiling the sweep is bound by: random row gathers, not stream
+  # bandwidth. Two gathers per incidence per iteration (node
+  # half, edge half); the device's random 64-B-row rate at the two tables'
+  # sizes, best over rows in flight, measured here on the same box.
+  ach = 2.0 * big.nnz * args.alg_iters / (ms4 * 1e-3)
+  probe = {}
+  for tab_mb in (big.E * 64 >> 20, big.N * 64 >> 20):
+    probe[f"{tab_mb}MB"] = max(ctx.probe_gather(tab_mb << 20, 16, f)
+                               for f in (4, 8, 16))
+  ceiling = min(probe.values())
   c4 = {"graph": "power-law 10M nodes / 5M edges, node degree 1+Poisson(19), "
                  "edge choice ~ rank^-0.8, seed 0 (libhgx host generator)",
         "nodes": big.N, "edges": big.E, "nnz": big.nnz,
@@ -482,6 +492,15 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
         "ms_per_iter": round(ms4 / args.alg_iters, 3),
         "gbps": round(gbps4, 1), "bytes_per_iter": b_iter4,
         "frac_of_hbm_peak": round(gbps4 / HBM_PEAK_GBPS, 4),
+        "gather_ceiling": {
+            "achieved_g_gathers_per_s": round(ach / 1e9, 2),
+            "probe_g_rows_per_s": {k: round(v / 1e9, 2) for k, v in probe.items()},
+            "ceiling_g_rows_per_s": round(ceiling / 1e9, 2),
+            "frac_of_ceiling": round(ach / ceiling, 3),
+            "note": "random 64-B row gathers (hgx_probe_gather: quads of "
+                    "lanes, 4/8/16 rows in flight, best) from tables of the "
+                    "edge and node coordinate sizes; above 1.0 = hot-edge "
+                    "L2 hits; 60% of HBM peak would need ~550 G rows/s"},
         "sharded": world > 1, "exchange": exch4 or None,
         "graph_gen_s": round(c4_gen, 1)}
   # ---- HOBE d=256 on the same graph: the north star's 10M/5M workload ----

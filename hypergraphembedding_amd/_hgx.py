@@ -76,6 +76,7 @@ SIGNATURES = {
     "hgx_jaccard_centroids": (_int, [_vp, _int, _pi64, _vp, _vp, _vp]),
     "hgx_records_set": (_int, [_vp, _i64, _int, _vp, _vp]),
     "hgx_records_info": (_int, [_vp, _pi64, _pint]),
+    "hgx_records_copy": (_int, [_vp, _vp]),
     "hgx_records_get": (_int, [_vp, _vp, _vp]),
     "hgx_records_blocks": (_int, [_vp, _pint, _vp]),
     "hgx_records_export": (_int, [_vp, _vp, _vp]),
@@ -83,6 +84,7 @@ SIGNATURES = {
     "hgx_model_init": (_int, [_vp, _int, _i64, _i64, _u64, _vp, _vp]),
     "hgx_model_get": (_int, [_vp, _vp, _vp]),
     "hgx_model_get_rows": (_int, [_vp, _int, _i64, _vp, _vp]),
+    "hgx_probe_gather": (_int, [_vp, _i64, _int, _int, _int, _pdbl]),
     "hgx_train": (_int, [_vp, _int, _int, _f32, _f32, _int, _int, _f32, _u64,
                          _vp, _vp, _pint]),
     "hgx_train_last_stats": (_int, [_vp, _pdbl, _pi64, _pi64]),
@@ -219,7 +221,7 @@ class Context:
   def set_tuning(self, key, value):
     """Pick between exact implementations (hgx_set_tuning): sample_reject_w,
     sample_mode3, train_fused, train_lanes, train_tb, train_prep_overlap,
-    train_prep_cus, alg_long, alg_ks, alg_push, mlp_fuse_head."""
+    train_prep_cus, alg_long, alg_ks, alg_push, mlp_fuse_head, stream_cus."""
     self._chk(lib().hgx_set_tuning(self.h, key.encode(), int(value)))
 
   # ---- incidence ----
@@ -343,6 +345,13 @@ class Context:
                                     _ptr(n), _ptr(e)))
     return sn, se, n, e
 
+  def probe_gather(self, table_bytes, row_floats=16, in_flight=8, reps=3):
+    """Random-row gather rate (rows/s) of the device (hgx_probe_gather)."""
+    v = ctypes.c_double()
+    self._chk(lib().hgx_probe_gather(self.h, int(table_bytes), row_floats,
+                                     in_flight, reps, ctypes.byref(v)))
+    return v.value
+
   # ---- samplers / records ----
   def sample_fobe(self, seed, K, node_q, edge_q, neg_node_q=None,
                   neg_edge_q=None):
@@ -422,6 +431,10 @@ class Context:
     assert R % 2 == 0 and R >= 4 and tgt.shape == (n, 3)
     self._chk(lib().hgx_records_set(self.h, n, (R - 4) // 2, _ptr(idx),
                                     _ptr(tgt)))
+
+  def records_copy_from(self, other):
+    """This context's records := `other`'s (device to device, same GPU)."""
+    self._chk(lib().hgx_records_copy(self.h, other.h))
 
   def records_info(self):
     n, K = ctypes.c_int64(), ctypes.c_int()

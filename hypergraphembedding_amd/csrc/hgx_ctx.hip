@@ -148,6 +148,35 @@ extern "C" int hgx_set_tuning(hgx_ctx *ctx, const char *key, int64_t value) {
     HGX_CHECK(ctx, value == 0 || (value % 4 == 0 && value <= 20), HGX_EINVAL,
               "alg_ks must be 0 or a multiple of 4 <= 20");
     t.alg_ks = (int)value;
+  } else if (k == "stream_cus") {
+    // The context's own stream on a CU subset: v > 0 the first
+    // round_up(v, 8) CU-mask bits, v < 0 every bit but those of |v|, 0 all.
+    // Mask bit i = CU i / 8 of XCD i % 8 (tools/cumask_probe.hip), so a
+    // multiple of 8 bits is the same CU count on every XCD. Two contexts on
+    // one device with +v / -v run concurrent work (e.g. the sampler of
+    // chunk c + 1 beside the trainer of chunk c) on disjoint CUs.
+    int ncu = 0;
+    HGX_HIP(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount,
+                                       ctx->device));
+    const int nb = (int)((std::abs(value) + 7) / 8 * 8);
+    HGX_CHECK(ctx, value == 0 || (nb > 0 && nb < ncu), HGX_EINVAL,
+              "stream_cus must be 0 or in (-%d, %d)", ncu, ncu);
+    HGX_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t ns = nullptr;
+    if (value == 0) {
+      HGX_HIP(ctx, hipStreamCreateWithFlags(&ns, hipStreamNonBlocking));
+    } else {
+      const int W = (ncu + 31) / 32;
+      std::vector<uint32_t> m(W, 0u);
+      for (int i = 0; i < ncu; i++)
+        if ((i < nb) == (value > 0)) m[i / 32] |= 1u << (i % 32);
+      HGX_HIP(ctx, hipExtStreamCreateWithCUMask(&ns, W, m.data()));
+    }
+    HGX_HIP(ctx, hipStreamSynchronize(ctx->own_stream));
+    const bool cur = ctx->stream == ctx->own_stream;
+    HGX_HIP(ctx, hipStreamDestroy(ctx->own_stream));
+    ctx->own_stream = ns;
+    if (cur) ctx->stream = ns;
   } else {
     return hgx_fail(ctx, HGX_EINVAL, "unknown tuning key '%s'", key);
   }

@@ -2098,6 +2098,35 @@ extern "C" int hgx_records_import(hgx_ctx *ctx, int64_t n, int K,
   return HGX_OK;
 }
 
+// The records of `src` (and their kind blocks) copied device to device into
+// `dst` on the same device: the hand-over of a chunk sampled on one context
+// (beside the training) to the training context.
+extern "C" int hgx_records_copy(hgx_ctx *dst, hgx_ctx *src) {
+  if (!dst || !src) return HGX_EINVAL;
+  HGX_CHECK(dst, dst->device == src->device, HGX_EINVAL,
+            "contexts on devices %d and %d", dst->device, src->device);
+  HGX_HIP(dst, hipSetDevice(dst->device));
+  HGX_HIP(dst, hipStreamSynchronize(src->stream));
+  const int64_t n = src->n_rec;
+  const int K = src->K, R = 4 + 2 * K;
+  HGX_TRY(hgx_ensure(dst, dst->rec_idx, sizeof(int32_t) * std::max<int64_t>(n, 1) * R));
+  HGX_TRY(hgx_ensure(dst, dst->rec_tgt, sizeof(float) * std::max<int64_t>(n, 1) * 3));
+  if (n > 0) {
+    HGX_HIP(dst, hipMemcpyAsync(dst->rec_idx.p, src->rec_idx.p,
+                                sizeof(int32_t) * n * R, hipMemcpyDeviceToDevice,
+                                dst->stream));
+    HGX_HIP(dst, hipMemcpyAsync(dst->rec_tgt.p, src->rec_tgt.p,
+                                sizeof(float) * n * 3, hipMemcpyDeviceToDevice,
+                                dst->stream));
+  }
+  HGX_HIP(dst, hipStreamSynchronize(dst->stream));
+  dst->n_rec = n;
+  dst->K = K;
+  dst->n_rec_blocks = src->n_rec_blocks;
+  for (int i = 0; i <= src->n_rec_blocks; i++) dst->rec_bounds[i] = src->rec_bounds[i];
+  return HGX_OK;
+}
+
 extern "C" int hgx_records_info(hgx_ctx *ctx, int64_t *n, int *K) {
   if (!ctx) return HGX_EINVAL;
   if (n) *n = ctx->n_rec;

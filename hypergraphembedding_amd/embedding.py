@@ -122,6 +122,19 @@ def _plot_distributions(path, records):
 RECORDS_BUDGET = 1 << 30
 
 
+# CUs of the sampling context when a streamed epoch samples chunk c + 1
+# beside chunk c's training (0: sample and train in turn on one context);
+# see DESIGN §4.3 for the measured split.
+STREAM_OVERLAP_CUS = 0
+
+
+class _SideSampler:
+  """The second context of an overlapped streamed epoch and its sampler."""
+
+  def __init__(self, ctx, sample):
+    self.ctx, self.sample = ctx, sample
+
+
 def _bound(inc, per_row, row_quota, per_quota):
   """Record bound per row: `per_row`, or with row quotas (node, edge) their
   total times `per_quota` spread over the rows (the streaming decision and
@@ -167,12 +180,30 @@ def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
     # the stream does not fit: sample and train strided row chunks in turn
     chunks = _row_chunks(inc, bound_per_row, budget)
     seed = numpy_seed()
-    prep = chunk_sampler_fn(inc, ctx)
-    model = Hg2vModel(inc.N + 1, inc.E + 1, dimension, num_neighbors, loss,
-                      act, ctx=ctx)
-    model.fit_streaming(lambda c: prep(seed, *chunks[c]), len(chunks),
-                        batch_size=fit_batch_size, epochs=fit_epochs)
-    node_w, edge_w = model.get_weights()
+    cus = STREAM_OVERLAP_CUS
+    side = None
+    if cus:
+      # chunk c + 1 sampled on a second context (its stream on `cus` CUs)
+      # while chunk c trains on this one (the other CUs); the host hands
+      # the chunks over (Hg2vModel.fit_streaming `side`)
+      side_ctx = _hgx.Context(ctx.device)
+      side_ctx.set_tuning("stream_cus", cus)
+      ctx.set_tuning("stream_cus", -cus)
+      prep = chunk_sampler_fn(inc, side_ctx)
+      side = _SideSampler(side_ctx, lambda c: prep(seed, *chunks[c]))
+    else:
+      prep = chunk_sampler_fn(inc, ctx)
+    try:
+      model = Hg2vModel(inc.N + 1, inc.E + 1, dimension, num_neighbors, loss,
+                        act, ctx=ctx)
+      model.fit_streaming(lambda c: prep(seed, *chunks[c]), len(chunks),
+                          batch_size=fit_batch_size, epochs=fit_epochs,
+                          side=side)
+      node_w, edge_w = model.get_weights()
+    finally:
+      if side is not None:
+        ctx.set_tuning("stream_cus", 0)
+        side.ctx.close()
     return coords_to_embedding(inc, node_w[1:], edge_w[1:], dimension, "")
   records = sampler_fn(inc, ctx)
   if debug_summary_path is not None:

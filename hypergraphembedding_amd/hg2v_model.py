@@ -39,7 +39,7 @@ class Hg2vModel:
 
   def fit_streaming(self, chunk_fn, n_chunks, batch_size=256, epochs=10,
                     min_delta=1e-3, lr=0.01, eps=1e-7, seed=None,
-                    chunk_perms=None):
+                    chunk_perms=None, side=None):
     """fit() over a record stream too large to keep resident (SURVEY §5:
     "stream samples in chunks"; the reference materialises every record,
     embedding.py:277-284). chunk_fn(c) makes chunk c resident on the context
@@ -50,29 +50,78 @@ class Hg2vModel:
     of Keras' global one over records that never coexist. The
     chunks are strided row classes (embedding._row_chunks), each a uniform
     slice of the graph, so a window mixes records of the whole id range;
-    model state
-    carries across chunks (one-epoch hgx_train calls), the epoch loss is the
-    record-weighted mean and EarlyStopping(min_delta, patience=0) applies to
-    it. chunk_perms[ep][c] (optional) fixes a chunk's record order.
+    model state carries across chunks (one-epoch hgx_train calls), the epoch
+    loss is the record-weighted mean and EarlyStopping(min_delta,
+    patience=0) applies to it. Epoch ep's chunk order and shuffle seeds come
+    from RandomState([seed, ep]). chunk_perms[ep][c] (optional) fixes a
+    chunk's record order.
+
+    side (optional): a second context on the same device that samples,
+    `side.ctx` with `side.sample(c)` -> record count (chunk_fn is then
+    unused). Chunk c + 1 is sampled on it while chunk c trains here (each
+    context's work on its own stream, on disjoint CUs when both have
+    stream_cus set); the host hands the chunk over (hgx_records_copy) once
+    both are done -- no cross-stream barrier packet ever waits in a queue.
+    Same records, order and seeds as the in-line form, so the same tables
+    bit for bit.
     Returns the epoch losses; total records per epoch may exceed 2^31."""
+    import threading
     import numpy as np
-    rs = np.random.RandomState(numpy_seed() % (2**32) if seed is None else seed)
-    best, losses = float("inf"), []
-    self.records_per_epoch = 0
-    for ep in range(epochs):
+    base = numpy_seed() % (2**32) if seed is None else seed
+
+    def plan(ep):
+      ers = np.random.RandomState([base, ep])
       order = (np.arange(n_chunks) if chunk_perms is not None
-               else rs.permutation(n_chunks))
-      lsum, n = 0.0, 0
-      for c in order:
-        m = chunk_fn(int(c))
-        if m == 0:
-          continue
-        perms = None if chunk_perms is None else chunk_perms[ep][int(c)][None, :]
+               else ers.permutation(n_chunks))
+      seeds = ers.randint(0, 2**62, size=n_chunks, dtype=np.int64)
+      return [int(c) for c in order], [int(x) for x in seeds]
+
+    def train(c, ep, shuffle_seed, out):
+      try:
+        perms = (None if chunk_perms is None
+                 else chunk_perms[ep][c][None, :])
         self.ctx.train(batch=batch_size, max_epochs=1, lr=lr, eps=eps,
                        loss=self.loss, act=self.act, min_delta=-1e30,
-                       shuffle_seed=int(rs.randint(0, 2**62, dtype=np.int64)),
-                       perms=perms)
-        lsum += self.ctx.train_loss_sum()
+                       shuffle_seed=shuffle_seed, perms=perms)
+        out.append(self.ctx.train_loss_sum())
+      except BaseException as e:  # re-raised by the caller
+        out.append(e)
+
+    best, losses = float("inf"), []
+    self.records_per_epoch = 0
+    ahead = None  # (epoch, chunk, records) sampled on `side` ahead of time
+    for ep in range(epochs):
+      order, seeds = plan(ep)
+      lsum, n = 0.0, 0
+      for i, c in enumerate(order):
+        if side is None:
+          m = chunk_fn(c)
+          if m == 0:
+            continue
+          out = []
+          train(c, ep, seeds[i], out)
+        else:
+          if ahead is not None and ahead[:2] == (ep, c):
+            m = ahead[2]
+          else:
+            m = side.sample(c)
+          ahead = None
+          if m == 0:
+            continue
+          self.ctx.records_copy_from(side.ctx)
+          nxt = ((ep, order[i + 1]) if i + 1 < len(order) else
+                 (ep + 1, plan(ep + 1)[0][0]) if ep + 1 < epochs else None)
+          out = []
+          th = threading.Thread(target=train, args=(c, ep, seeds[i], out))
+          th.start()
+          try:
+            if nxt is not None:
+              ahead = (nxt[0], nxt[1], side.sample(nxt[1]))
+          finally:
+            th.join()
+        if isinstance(out[0], BaseException):
+          raise out[0]
+        lsum += out[0]
         n += m
       self.records_per_epoch = n
       cur = lsum / max(n, 1)

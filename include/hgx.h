@@ -223,6 +223,8 @@ int hgx_sample_last_stats(hgx_ctx *ctx, int64_t *union_rows,
 int hgx_sample_uniform_rows(hgx_ctx *ctx, int64_t *rows);
 int hgx_records_set(hgx_ctx *ctx, int64_t n, int K, const int32_t *idx,
                     const float *tgt);
+/* the records of `src` copied device to device into `dst` (same device) */
+int hgx_records_copy(hgx_ctx *dst, hgx_ctx *src);
 int hgx_records_info(hgx_ctx *ctx, int64_t *n, int *K);
 int hgx_records_get(hgx_ctx *ctx, int32_t *idx, float *tgt);
 /* Kind blocks of the stream in the reference's record order (hgx_sample_*:
@@ -264,6 +266,14 @@ int hgx_weight_same_type(hgx_ctx *ctx, int side, int norm, double alpha,
  * = edge e's value, edge_major[e,v] = node v's); any output may be NULL */
 int hgx_weight_span(hgx_ctx *ctx, double alpha, float *node_span,
                     float *edge_span, float *node_major, float *edge_major);
+
+/* ---- diagnostics ----------------------------------------------------------- *
+ * Random-row gather rate of the device: rows of `row_floats` floats drawn
+ * uniformly from a table of `table_bytes`, quads of lanes one row, in_flight
+ * (4, 8, 16) rows per lane; best of `reps` launches, in rows per second.
+ * The ceiling bench.py holds the C4 alg-dist gather against. */
+int hgx_probe_gather(hgx_ctx *ctx, int64_t table_bytes, int row_floats,
+                     int in_flight, int reps, double *rows_per_s);
 
 /* ---- model + trainer ---------------------------------------------------- *
  * Replaces BooleanModel / UnweightedFloatModel (hg2v_model.py:51-203) and

@@ -213,3 +213,32 @@ def test_strided_streaming_matches_resident_training(ctx):
   mean = lambda mode: np.mean([x[1] for x in res[mode]])
   assert abs(mean("strided") - mean("resident")) <= 0.02
   assert mean("resident") > 0.55  # the embedding carries link information
+
+
+def test_overlapped_streaming_bitwise_equal_inline():
+  """chunk c + 1 sampled on a second context (its
+  stream on 128 CUs, the trainer's on the other 128) while chunk c trains
+  gives the in-line streamed epoch's tables bit for bit (same records, same
+  per-epoch order and shuffle seeds), over 2 epochs of >= 4 strided
+  chunks, through EmbedHg2vAlgDist's streaming path."""
+  from conftest import golden_incidence
+  from hypergraphembedding_amd import embedding
+  from hypergraphembedding_amd.synthetic import powerlaw_hypergraph
+  inc = powerlaw_hypergraph(N=20_000, E=10_000, seed=5)
+  out = {}
+  try:
+    for cus in (0, 128):
+      embedding.STREAM_OVERLAP_CUS = cus
+      np.random.seed(11)
+      emb = embedding.EmbedHg2vAlgDist(inc, 16, num_samples=20, epochs=2,
+                                       records_budget=300_000)
+      out[cus] = emb
+  finally:
+    embedding.STREAM_OVERLAP_CUS = 0
+  a, b = out[0], out[128]
+  assert len(a.node) == inc.N
+  for k in list(a.node)[:2000]:
+    assert list(a.node[k].values) == list(b.node[k].values)
+  for k in list(a.edge)[:2000]:
+    assert list(a.edge[k].values) == list(b.edge[k].values)
+  assert a.SerializeToString() == b.SerializeToString()
