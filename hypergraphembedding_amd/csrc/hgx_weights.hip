@@ -50,6 +50,12 @@
 
 #include "hgx_internal.h"
 
+// No implicit contraction anywhere in this file: alpha + (1 - alpha) * v
+// must stay two roundings (numpy's), and a float product added to a double
+// must not become a double fma (hipcc contracts by default, through the
+// __fadd_rn / __fmul_rn helpers too).
+#pragma clang fp contract(off)
+
 namespace {
 
 // np.linalg.norm of the float32 vector a - b (see the header)
@@ -69,7 +75,7 @@ __device__ float norm32(const float *__restrict__ a, const float *__restrict__ b
       for (; i < n64; i += 64) {
 #pragma unroll
         for (int t = 0; t < 64; t++) {
-          const float d = __fsub_rn(a[i + t], b[i + t]);
+          const float d = a[i + t] - b[i + t];
           a5[t] = __fmaf_rn(d, d, a5[t]);
         }
       }
@@ -77,29 +83,29 @@ __device__ float norm32(const float *__restrict__ a, const float *__restrict__ b
       for (int j = 0; j < 4; j++)
 #pragma unroll
         for (int l = 0; l < 8; l++)
-          acc[j * 8 + l] = __fadd_rn(a5[j * 16 + l], a5[j * 16 + l + 8]);
+          acc[j * 8 + l] = a5[j * 16 + l] + a5[j * 16 + l + 8];
     }
     for (; i < n1; i += 32) {
 #pragma unroll
       for (int t = 0; t < 32; t++) {
-        const float d = __fsub_rn(a[i + t], b[i + t]);
+        const float d = a[i + t] - b[i + t];
         acc[t] = __fmaf_rn(d, d, acc[t]);
       }
     }
     float s[8];
 #pragma unroll
     for (int l = 0; l < 8; l++)
-      s[l] = __fadd_rn(__fadd_rn(__fadd_rn(acc[l], acc[8 + l]), acc[16 + l]),
-                       acc[24 + l]);
+      s[l] = ((acc[l] + acc[8 + l]) + acc[16 + l]) + acc[24 + l];
     float h[4];
 #pragma unroll
-    for (int l = 0; l < 4; l++) h[l] = __fadd_rn(s[l], s[l + 4]);
-    tot = __fadd_rn(__fadd_rn(h[0], h[1]), __fadd_rn(h[2], h[3]));
+    for (int l = 0; l < 4; l++) h[l] = s[l] + s[l + 4];
+    tot = (h[0] + h[1]) + (h[2] + h[3]);
   }
   double dot = tot;
   for (; i < k; i++) {
-    const float d = __fsub_rn(a[i], b[i]);
-    dot = __dadd_rn(dot, (double)__fmul_rn(d, d));
+    const float d = a[i] - b[i];
+    const float p = d * d;
+    dot = dot + (double)p;
   }
   // correctly rounded float sqrt (v_sqrt_f32 is not): through double
   return (float)sqrt((double)(float)dot);
@@ -108,7 +114,7 @@ __device__ float norm32(const float *__restrict__ a, const float *__restrict__ b
 // ord = inf: max |a_d - b_d| (exact in any order)
 __device__ float ninf32(const float *a, const float *b, int k) {
   float m = 0.f;
-  for (int i = 0; i < k; i++) m = fmaxf(m, fabsf(__fsub_rn(a[i], b[i])));
+  for (int i = 0; i < k; i++) m = fmaxf(m, fabsf(a[i] - b[i]));
   return m;
 }
 
@@ -165,12 +171,12 @@ __global__ void scale_f32_kernel(int64_t n, float *__restrict__ v,
                                  const unsigned *__restrict__ mm, float a32,
                                  float b32) {
   const float mn = __uint_as_float(mm[0]);
-  const float delta = __fsub_rn(__uint_as_float(mm[1]), mn);
+  const float delta = __uint_as_float(mm[1]) - mn;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
        t += (int64_t)gridDim.x * blockDim.x) {
-    const float o = delta == 0.f ? 0.f
-                                 : __fsub_rn(1.f, __fdiv_rn(__fsub_rn(v[t], mn), delta));
-    v[t] = __fadd_rn(a32, __fmul_rn(b32, o));
+    const float o = delta == 0.f ? 0.f : 1.f - __fdiv_rn(v[t] - mn, delta);
+    const float p = b32 * o;  // two roundings: contraction is off
+    v[t] = a32 + p;
   }
 }
 
@@ -191,7 +197,7 @@ __global__ __launch_bounds__(256) void span_kernel(
     const int64_t work = (int64_t)(e - b) * k;
     for (int64_t w = lane; w < work; w += 64) {
       const int j = b + (int)(w / k), d = (int)(w % k);
-      const float df = __fsub_rn(other[(size_t)col[j] * ks + 1 + d], m[d]);
+      const float df = other[(size_t)col[j] * ks + 1 + d] - m[d];
       hi = fmaxf(hi, df);
       lo = fminf(lo, df);
     }
@@ -199,7 +205,7 @@ __global__ __launch_bounds__(256) void span_kernel(
     lo = hgx::wave_min(lo);
     // (+ 0: a zero span is +0, so the unsigned bit order of the min / max
     // atomics is the float order)
-    const float s = __fadd_rn(__fsub_rn(hi, lo), 0.f);
+    const float s = (hi - lo) + 0.f;
     if (lane == 0) span[r] = s;
     wlo = fminf(wlo, s);
     whi = fmaxf(whi, s);

@@ -231,7 +231,8 @@ def sample_sharded(inc, num_neighbors, num_samples, ctx=None, seed=0,
   del gi, gt, li, lt
   if world > 1:
     # the ranks' rows interleave: restore row order inside every block
-    cols = _ROW_COL[kind]
+    # (FOBE: 4 blocks, or 9 with negatives)
+    cols = _ROW_COL[kind][:allsz.shape[1]]
     assert len(cols) == allsz.shape[1], (kind, allsz.shape)
     for j, col in enumerate(cols):
       b0, b1 = int(gbounds[j]), int(gbounds[j + 1])
