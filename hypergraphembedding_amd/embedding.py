@@ -123,9 +123,12 @@ RECORDS_BUDGET = 1 << 30
 
 
 # CUs of the sampling context when a streamed epoch samples chunk c + 1
-# beside chunk c's training (0: sample and train in turn on one context);
-# see DESIGN §4.3 for the measured split.
-STREAM_OVERLAP_CUS = 0
+# beside chunk c's training (0: sample and train in turn on one context).
+# 192 of MI355X's 256: the trainer keeps 64 CUs (one per workgroup of a
+# batch step). Full C4 HOBE epoch (profiles/r04/c4_epoch/): 350 s in turn,
+# 261 s at 192 / 262 s at 160 / 286 s at 128 sampler CUs, the batch step
+# 9.28 -> 9.42 us, tables bit-identical.
+STREAM_OVERLAP_CUS = 192
 
 
 class _SideSampler:

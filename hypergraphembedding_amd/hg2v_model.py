@@ -84,11 +84,13 @@ class Hg2vModel:
                        loss=self.loss, act=self.act, min_delta=-1e30,
                        shuffle_seed=shuffle_seed, perms=perms)
         out.append(self.ctx.train_loss_sum())
+        self.chunk_stats.append((ep, c) + tuple(self.ctx.train_stats()))
       except BaseException as e:  # re-raised by the caller
         out.append(e)
 
     best, losses = float("inf"), []
     self.records_per_epoch = 0
+    self.chunk_stats = []  # (epoch, chunk, step ms, records, batches)
     ahead = None  # (epoch, chunk, records) sampled on `side` ahead of time
     for ep in range(epochs):
       order, seeds = plan(ep)
