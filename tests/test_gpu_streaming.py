@@ -223,7 +223,7 @@ def test_strided_streaming_matches_resident_training(ctx):
 
 def test_overlapped_streaming_bitwise_equal_inline():
   """chunk c + 1 sampled on a second context (its
-  stream on 128 CUs, the trainer's on the other 128) while chunk c trains
+  stream on 128 or 192 CUs, the trainer's on the rest) while chunk c trains
   gives the in-line streamed epoch's tables bit for bit (same records, same
   per-epoch order and shuffle seeds), over 2 epochs of >= 4 strided
   chunks, through EmbedHg2vAlgDist's streaming path."""
@@ -232,15 +232,17 @@ def test_overlapped_streaming_bitwise_equal_inline():
   from hypergraphembedding_amd.synthetic import powerlaw_hypergraph
   inc = powerlaw_hypergraph(N=20_000, E=10_000, seed=5)
   out = {}
+  keep = embedding.STREAM_OVERLAP_CUS
   try:
-    for cus in (0, 128):
+    for cus in (0, 128, 192):
       embedding.STREAM_OVERLAP_CUS = cus
       np.random.seed(11)
       emb = embedding.EmbedHg2vAlgDist(inc, 16, num_samples=20, epochs=2,
                                        records_budget=300_000)
       out[cus] = emb
   finally:
-    embedding.STREAM_OVERLAP_CUS = 0
+    embedding.STREAM_OVERLAP_CUS = keep
+  assert out[128].SerializeToString() == out[192].SerializeToString()
   a, b = out[0], out[128]
   assert len(a.node) == inc.N
   for k in list(a.node)[:2000]:
