@@ -61,6 +61,10 @@ struct Tuning {
   // forms the joint layers' deltas (one launch per batch fewer), 0 its own
   // launch
   int mlp_fuse_head = 1;
+  // combiner MLP training: 1 batch b + 1's input rows gathered (with their
+  // dropout) by extra workgroups of batch b's hidden-layer launch, so its
+  // first layer and weight gradient read a dense operand; 0 both gather
+  int mlp_prefetch = 1;
   // trainer: chunk c + 1 prepared (train_prep / train_place) on a second
   // stream while chunk c trains (1), on the same stream one chunk ahead
   // (2: queued before chunk c's batches, so the host never waits on the
@@ -243,10 +247,15 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
   return z ^ (z >> 31);
 }
+// rand64's counter-independent part: rand64(seed, stream, ctr) =
+// mix64(rand64_key(seed, stream) + ctr), for loops that hoist it
+__host__ __device__ __forceinline__ uint64_t rand64_key(uint64_t seed, uint64_t stream) {
+  return mix64(seed ^ mix64(stream + 0x632be59bd9b4e019ull));
+}
 __host__ __device__ __forceinline__ uint64_t rand64(uint64_t seed,
                                                     uint64_t stream,
                                                     uint64_t ctr) {
-  return mix64(mix64(seed ^ mix64(stream + 0x632be59bd9b4e019ull)) + ctr);
+  return mix64(rand64_key(seed, stream) + ctr);
 }
 // uniform integer in [0, n) (multiply-high on 64 random bits: bias < n/2^64)
 __device__ __forceinline__ uint32_t bounded(uint64_t r, uint32_t n) {

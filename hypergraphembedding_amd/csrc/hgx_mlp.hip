@@ -59,6 +59,36 @@ constexpr int kTile = 32;     // output tile edge
 constexpr int kChunk = 64;    // reduction chunk staged in LDS
 constexpr int kThreads = 256; // 4 waves
 constexpr int kMaxJobs = 12;
+
+// Diagnostic build only (HGX_MLP_DIAG_TIME=1, tools/build_variant.sh): thread
+// 0 of every workgroup of the NCH-instantiated GEMM kernels stamps the 100 MHz
+// real-time counter at phase boundaries (waiting for its own loads / stores at
+// each one, which serialises what the product overlaps) and adds the phase
+// times to per-kernel sums that hgx_mlp_fit prints to stderr.
+#ifndef HGX_MLP_DIAG_TIME
+#define HGX_MLP_DIAG_TIME 0
+#endif
+#if HGX_MLP_DIAG_TIME
+__device__ unsigned long long g_mlp_t[8][8];
+__device__ unsigned long long g_mlp_n[8];
+#define TSTAMP(i)                                             \
+  do {                                                        \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+    ts[i] = __builtin_amdgcn_s_memrealtime();                 \
+  } while (0)
+#define TDECL unsigned long long ts[8] = {}
+#define TFLUSH(kind, n)                                                   \
+  do {                                                                    \
+    if (threadIdx.x == 0) {                                               \
+      for (int q = 1; q < (n); q++) atomicAdd(&g_mlp_t[kind][q], ts[q] - ts[0]); \
+      atomicAdd(&g_mlp_n[kind], 1ull);                                    \
+    }                                                                     \
+  } while (0)
+#else
+#define TSTAMP(i) (void)0
+#define TDECL (void)0
+#define TFLUSH(kind, n) (void)0
+#endif
 constexpr int kMcap = 4096;   // activation rows (training uses the first 256)
 
 enum { ACT_SIGMOID = HGX_ACT_SIGMOID, ACT_RELU = HGX_ACT_RELU };
@@ -143,39 +173,93 @@ __device__ __forceinline__ float4 src_load4(const Src &s, const Ctx &c, int m,
   return v;
 }
 
+// A source's fields read once into scalar registers (NCH-instantiated
+// kernels). The asm pins keep them there: without them the compiler re-reads
+// each field from the kernel-argument table inside every uniform branch that
+// uses it, one scalar round trip per chunk (150+ s_load in mlp_fwd<8>).
+template <class T> __device__ __forceinline__ T spin(T v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+// pinned pointers are typed global (address space 1): a pointer through the
+// asm would otherwise be generic and its loads flat_load
+typedef const __attribute__((address_space(1))) float *gfp;
+typedef const __attribute__((address_space(1))) int *gip;
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) f4v *gf4p;
+__device__ __forceinline__ float4 ldg4(gfp p) {
+  const f4v v = *reinterpret_cast<gf4p>(p);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ gfp gpin(const float *p) {
+  return (gfp)spin((uint64_t)p);
+}
+__device__ __forceinline__ gip gpin(const int *p) {
+  return (gip)spin((uint64_t)p);
+}
+struct SrcK {
+  gfp x, t0, t1, safe;  // t0 / t1: the tables of columns < c1 / >= c1
+  gip j0, j1;           // their id arrays (a valid one either way)
+  int ldx, l0, l1, c1, width, gather, drop, w64;
+  uint64_t dkey;  // hgx::rand64_key(seed, dstream)
+};
+__device__ __forceinline__ SrcK src_k(const Src &s, const Ctx &c) {
+  SrcK k;
+  k.gather = spin(s.gather);
+  k.drop = spin(s.drop);
+  k.c1 = spin(s.c1);
+  k.width = spin(s.width);
+  k.ldx = spin(s.ldx);
+  k.x = gpin(s.x);
+  k.t0 = gpin(s.c1 > 0 ? s.t0 : s.t1);
+  k.t1 = gpin(s.c1 < s.width ? s.t1 : s.t0);
+  k.j0 = gpin(s.c1 > 0 ? s.i0 : s.i1);
+  k.j1 = gpin(s.c1 < s.width ? s.i1 : s.i0);
+  k.l0 = spin(s.c1 > 0 ? s.ld0 : s.ld1);
+  k.l1 = spin(s.c1 < s.width ? s.ld1 : s.ld0);
+  k.safe = s.gather ? k.t0 : k.x;
+  k.w64 = (k.width + 63) >> 6;
+  k.dkey = spin(hgx::rand64_key(c.dseed, s.dstream));
+  return k;
+}
+
 // One operand row resolved once per kernel (the sample ids of a gathered
 // source loaded up front), so the per-chunk loads of that row depend on no
 // other load and several chunks can be in flight.
 struct SrcRow {
-  const float *p0, *p1;  // dense row / table-0 row, table-1 row
+  gfp p0, p1;  // dense row / table-0 row, table-1 row
   int64_t pos;
   bool ok;
 };
-// the rows m and m + off of a tile: rows past M resolve to row 0 of
-// the batch (never read: src_raw4 masks them), and all four id loads are
-// unconditional inside one uniform branch, so they share one round trip
-__device__ __forceinline__ void src_rows2(const Src &s, const Ctx &c, int m,
-                                          SrcRow &a, SrcRow &b, int off = 16) {
-  a.ok = m < c.M;
-  b.ok = m + off < c.M;
-  a.pos = c.pbase + m;
-  b.pos = c.pbase + m + off;
-  a.p0 = a.p1 = b.p0 = b.p1 = nullptr;
+// R rows of a tile: rows past M resolve to row 0 of the batch (never read:
+// src_raw4 masks them). One uniform branch around all of them, and every id
+// load unconditional inside it, so all ids share one round trip.
+template <int R>
+__device__ __forceinline__ void src_rows(const SrcK &s, const Ctx &c, const int (&m)[R],
+                                         SrcRow (&r)[R]) {
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    r[i].ok = m[i] < c.M;
+    r[i].pos = c.pbase + m[i];
+    r[i].p0 = r[i].p1 = nullptr;
+  }
   if (!s.gather) {
-    a.p0 = s.x + (int64_t)(a.ok ? m : 0) * s.ldx;
-    b.p0 = s.x + (int64_t)(b.ok ? m + off : 0) * s.ldx;
+#pragma unroll
+    for (int i = 0; i < R; i++) r[i].p0 = s.x + (int64_t)(r[i].ok ? m[i] : 0) * s.ldx;
     return;
   }
-  const int64_t pa = a.ok ? a.pos : c.pbase, pb = b.ok ? b.pos : c.pbase;
-  const int *j0 = s.c1 > 0 ? s.i0 : s.i1;       // a valid id array either way
-  const int *j1 = s.c1 < s.width ? s.i1 : s.i0;
-  const int a0 = j0[pa], a1 = j1[pa], b0 = j0[pb], b1 = j1[pb];
-  const float *t0 = s.c1 > 0 ? s.t0 : s.t1, *t1 = s.c1 < s.width ? s.t1 : s.t0;
-  const int l0 = s.c1 > 0 ? s.ld0 : s.ld1, l1 = s.c1 < s.width ? s.ld1 : s.ld0;
-  a.p0 = t0 + (int64_t)a0 * l0;
-  a.p1 = t1 + (int64_t)a1 * l1;
-  b.p0 = t0 + (int64_t)b0 * l0;
-  b.p1 = t1 + (int64_t)b1 * l1;
+  int a0[R], a1[R];
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    const int64_t pa = r[i].ok ? r[i].pos : c.pbase;
+    a0[i] = s.j0[pa];
+    a1[i] = s.j1[pa];
+  }
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    r[i].p0 = s.t0 + (int64_t)a0[i] * s.l0;
+    r[i].p1 = s.t1 + (int64_t)a1[i] * s.l1;
+  }
 }
 // src_load4 of a resolved row in two steps, so that no lane-divergent
 // branch separates a load from its use (a join over loaded registers makes
@@ -183,20 +267,18 @@ __device__ __forceinline__ void src_rows2(const Src &s, const Ctx &c, int m,
 // valid dummy row when the element is outside the operand), src_fix4 zeroes
 // and applies the dropout mask when the chunk is consumed. Same values as
 // src_load4.
-__device__ __forceinline__ float4 src_raw4(const Src &s, const SrcRow &r,
-                                           int k4) {
+__device__ __forceinline__ float4 src_raw4(const SrcK &s, const SrcRow &r, int k4) {
   const bool in = r.ok && k4 < s.width;
-  const float *a = s.gather ? (k4 < s.c1 ? r.p0 + k4 : r.p1 + (k4 - s.c1))
-                            : r.p0 + k4;
-  const float *safe = s.gather ? (s.c1 > 0 ? s.t0 : s.t1) : s.x;
-  return *reinterpret_cast<const float4 *>(in ? a : safe);
+  gfp a = s.gather ? (k4 < s.c1 ? r.p0 + k4 : r.p1 + (k4 - s.c1)) : r.p0 + k4;
+  return ldg4(in ? a : s.safe);
 }
-__device__ __forceinline__ float4 src_fix4(const Src &s, const Ctx &c,
-                                           const SrcRow &r, int k4, float4 v,
-                                           bool use_drop) {
+__device__ __forceinline__ float4 src_fix4(const SrcK &s, const SrcRow &r, int k4,
+                                           float4 v, bool use_drop) {
   if (!(r.ok && k4 < s.width)) return make_float4(0.f, 0.f, 0.f, 0.f);
   if (s.gather && use_drop && s.drop) {
-    const unsigned b = drop_bits4(s, c, r.pos, k4);
+    // drop_bits4 with rand64's invariant part precomputed (same bits)
+    const uint64_t q = (uint64_t)r.pos * (uint64_t)s.w64 + (k4 >> 6);
+    const unsigned b = (unsigned)(hgx::mix64(s.dkey + q) >> (k4 & 63)) & 0xFu;
     v.x = (b & 1) ? v.x * 2.0f : 0.0f;
     v.y = (b & 2) ? v.y * 2.0f : 0.0f;
     v.z = (b & 4) ? v.z * 2.0f : 0.0f;
@@ -300,17 +382,58 @@ struct FwdJob {
   float *dZ;
   int lddz;
   float *part;        // one loss partial per tile
+  // prefetch job (pf = 1, no GEMM; combiner training): the next batch's
+  // rows of the gathered, dropped-out input `a` -- sample positions pfbase ..
+  // pfbase + pfM, the kPfRows rows zero past pfM -- into pfX (row stride
+  // pfld), which that batch's first layer and its weight gradient then read
+  // as a dense operand: the same values in the same places as the gather
+  int pf, pfM, pfld;
+  int64_t pfbase;
+  float *pfX;
 };
+constexpr int kPfRows = 256;             // rows of a prefetch buffer (max batch)
+constexpr int kPfItems = 4 * kThreads;   // float4 items per prefetch workgroup
 template <class J> struct Jobs {
   int n;
   int start[kMaxJobs + 1];
   J j[kMaxJobs];
 };
 
+// the job of workgroup bid: start[] is read whole and unconditionally (one
+// scalar round trip, not one per job as a search loop's dependent loads)
 __device__ __forceinline__ int find_job(const int *start, int n, int bid) {
   int q = 0;
-  while (q + 1 < n && bid >= start[q + 1]) q++;
+#pragma unroll
+  for (int i = 1; i < kMaxJobs; i++) q += (int)((bid >= start[i]) & (i < n));
   return q;
+}
+
+// One workgroup of a prefetch job: items tile * kPfItems + t + 256 i of the
+// (row, float4 column) space, every id load and then every row load issued
+// before the first store.
+__device__ __forceinline__ void fwd_prefetch(const FwdJob &J, const Ctx &c, int tile) {
+  Ctx cn = c;
+  cn.pbase = J.pfbase;
+  cn.M = J.pfM;
+  const SrcK sa = src_k(J.a, cn);
+  const int w4 = J.pfld >> 2;
+  int m[4], k4[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int idx = tile * kPfItems + threadIdx.x + kThreads * i;
+    m[i] = idx / w4;
+    k4[i] = (idx - m[i] * w4) * 4;
+  }
+  SrcRow r[4];
+  src_rows(sa, cn, m, r);
+  float4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) v[i] = src_raw4(sa, r[i], k4[i]);
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    if (m[i] < kPfRows)
+      *reinterpret_cast<float4 *>(J.pfX + (int64_t)m[i] * J.pfld + k4[i]) =
+          src_fix4(sa, r[i], k4[i], v[i], true);
 }
 
 // NCH > 0: exactly NCH reduction chunks, every chunk's operands loaded up
@@ -322,29 +445,41 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd(Jobs<FwdJob> js, Ctx c) {
   const int qj = find_job(js.start, js.n, blockIdx.x);
   const FwdJob &J = js.j[qj];
   const int tile = blockIdx.x - js.start[qj];
+  if (J.pf) {
+    fwd_prefetch(J, c, tile);
+    return;
+  }
   const int m0 = (tile / J.tiles_n) * kTile, n0 = (tile % J.tiles_n) * kTile;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  TDECL;
+  TSTAMP(0);
+  // the epilogue's bias, loaded before the GEMM (reduce_tile's column j)
+  const float bias = J.b[n0 + (lane & 31)];
   f32x16 acc = {};
   if constexpr (NCH > 0) {
-    SrcRow row0, unused;
-    src_rows2(J.a, c, m0 + (t & 31), row0, unused, 0);
+    const SrcK sa = src_k(J.a, c);
+    SrcRow rr[1];
+    src_rows(sa, c, {m0 + (t & 31)}, rr);
+    const SrcRow &row0 = rr[0];
+    TSTAMP(1);
     const int q4 = 4 * (t >> 5);  // pattern R2
     float4 ra0[NCH], ra1[NCH], rb0[NCH], rb1[NCH];
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
       const int r0 = ch * kChunk;
-      ra0[ch] = src_raw4(J.a, row0, r0 + q4);
-      ra1[ch] = src_raw4(J.a, row0, r0 + q4 + 32);
+      ra0[ch] = src_raw4(sa, row0, r0 + q4);
+      ra1[ch] = src_raw4(sa, row0, r0 + q4 + 32);
       const float *wp = J.W + (int64_t)(r0 + (t >> 3)) * J.ldw + n0 + 4 * (t & 7);
       rb0[ch] = *reinterpret_cast<const float4 *>(wp);
       rb1[ch] = *reinterpret_cast<const float4 *>(wp + (int64_t)32 * J.ldw);
     }
+    TSTAMP(2);
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
       float *As = lds[ch & 1][0], *Bs = lds[ch & 1][1];
       const int k4 = ch * kChunk + q4;
-      store_R2(As, src_fix4(J.a, c, row0, k4, ra0[ch], true),
-               src_fix4(J.a, c, row0, k4 + 32, ra1[ch], true));
+      store_R2(As, src_fix4(sa, row0, k4, ra0[ch], true),
+               src_fix4(sa, row0, k4 + 32, ra1[ch], true));
       store_C(Bs, rb0[ch], rb1[ch]);
       __syncthreads();
       mma_chunk(As, Bs, acc, w, lane);
@@ -372,9 +507,10 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd(Jobs<FwdJob> js, Ctx c) {
   }
   float v[4];
   int i0, j;
+  TSTAMP(3);
   reduce_tile(&lds[0][0][0], acc, v, i0, j);
+  TSTAMP(4);
   const int n = n0 + j;
-  const float bias = J.b[n];
   float lsum = 0.f;
 #pragma unroll
   for (int e = 0; e < 4; e++) {
@@ -402,6 +538,10 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd(Jobs<FwdJob> js, Ctx c) {
     if (t == 0)
       J.part[tile] = J.lw * (((wsum[0] + wsum[1]) + wsum[2]) + wsum[3]) /
                      ((float)J.Nreal * (float)c.M);
+  }
+  if constexpr (NCH > 0) {
+    TSTAMP(5);
+    TFLUSH(NCH == 8 ? (J.a.gather ? 0 : 2) : (NCH == 6 ? 1 : 6), 6);
   }
 }
 
@@ -587,6 +727,17 @@ __global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c, Head
   const int m0 = (tile / J.tiles_n) * kTile, k0 = (tile % J.tiles_n) * kTile;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int nch0 = J.tm[0].R / kChunk;
+  TDECL;
+  TSTAMP(0);
+  // the epilogue's activations, loaded before the GEMM (reduce_tile's
+  // rows i0 .. i0 + 3 of column j; clamped, used only where in range)
+  float ypre[4];
+  {
+    const int i0p = 8 * w + 4 * (lane >> 5), kp = min(k0 + (lane & 31), J.Kreal - 1);
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+      ypre[e] = J.Y[(int64_t)min(m0 + i0p + e, c.M - 1) * J.ldy + kp];
+  }
   f32x16 acc = {};
   if constexpr (NCH > 0) {
     // all NCH chunks' loads up front, unconditional (rows past M read row 0
@@ -595,29 +746,37 @@ __global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c, Head
     const int row = t & 31, ma = m0 + row, q4 = 4 * (t >> 5);
     const bool oka = ma < c.M;
     float4 ra0[NCH], ra1[NCH], rb0[NCH], rb1[NCH];
+    // both terms' fields pinned in scalar registers (see SrcK)
+    const gfp dzt[2] = {gpin(J.tm[0].dz), gpin(J.tm[1].dz)};
+    const gfp Wt[2] = {gpin(J.tm[0].W), gpin(J.tm[1].W)};
+    const int lddzt[2] = {spin(J.tm[0].lddz), spin(J.tm[1].lddz)};
+    const int ldwt[2] = {spin(J.tm[0].ldw), spin(J.tm[1].ldw)};
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
       const bool first = ch < nch0;
-      const float *dz = first ? J.tm[0].dz : J.tm[1].dz;
-      const float *W = first ? J.tm[0].W : J.tm[1].W;
-      const int lddz = first ? J.tm[0].lddz : J.tm[1].lddz;
-      const int ldw = first ? J.tm[0].ldw : J.tm[1].ldw;
+      const gfp dz = first ? dzt[0] : dzt[1];
+      const gfp W = first ? Wt[0] : Wt[1];
+      const int lddz = first ? lddzt[0] : lddzt[1];
+      const int ldw = first ? ldwt[0] : ldwt[1];
       const int r4 = (first ? ch : ch - nch0) * kChunk + q4;
-      const float *dr = dz + (int64_t)(oka ? ma : 0) * lddz + r4;
-      const float *wr = W + (int64_t)(k0 + row) * ldw + r4;
+      const gfp dr = dz + (int64_t)(oka ? ma : 0) * lddz + r4;
+      const gfp wr = W + (int64_t)(k0 + row) * ldw + r4;
       if (!(FH && first)) {
-        ra0[ch] = *reinterpret_cast<const float4 *>(dr);
-        ra1[ch] = *reinterpret_cast<const float4 *>(dr + 32);
+        ra0[ch] = ldg4(dr);
+        ra1[ch] = ldg4(dr + 32);
       }
-      rb0[ch] = *reinterpret_cast<const float4 *>(wr);
-      rb1[ch] = *reinterpret_cast<const float4 *>(wr + 32);
+      rb0[ch] = ldg4(wr);
+      rb1[ch] = ldg4(wr + 32);
     }
+    TSTAMP(1);
     if constexpr (FH) {
       float lsum = 0.f;
       const bool gst = qj == 0 && k0 == 0;
       head_wave(hj, c, m0 + w * 8, lane, gst, s_hd, w * 8, kHdLd, lsum);
+      TSTAMP(6);
       if (gst) head_partial(hj, c, m0 / kTile, lsum);
       __syncthreads();
+      TSTAMP(7);
 #pragma unroll
       for (int ch = 0; ch < NCH; ch++) {
         if (ch < nch0) {
@@ -627,6 +786,7 @@ __global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c, Head
         }
       }
     }
+    TSTAMP(2);
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
@@ -665,16 +825,19 @@ __global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c, Head
   }
   float v[4];
   int i0, j;
+  TSTAMP(3);
   reduce_tile(&lds[0][0][0], acc, v, i0, j);
+  TSTAMP(4);
   const int k = k0 + j;
 #pragma unroll
   for (int e = 0; e < 4; e++) {
     const int m = m0 + i0 + e;
-    // unconditional load (clamped), so the four rows' loads are in flight
-    // together; the value is used only where the original read it
-    const float yv = J.Y[(int64_t)min(m, c.M - 1) * J.ldy + min(k, J.Kreal - 1)];
-    const float d = (m < c.M && k < J.Kreal) ? v[e] * act_d(J.act, yv) : 0.f;
+    const float d = (m < c.M && k < J.Kreal) ? v[e] * act_d(J.act, ypre[e]) : 0.f;
     J.dZ[(int64_t)m * J.ldo + k] = d;
+  }
+  if constexpr (NCH > 0) {
+    TSTAMP(5);
+    TFLUSH(FH ? 3 : 4, FH ? 8 : 6);
   }
 }
 
@@ -685,7 +848,46 @@ struct WgJob {
   int lddz;
   float *W, *aW, *b, *ab;
   int ldw, tiles_n;
+  int gemm_tiles;     // tiles past these are the bias's (one per column tile)
 };
+
+// A bias workgroup of WGRAD: column sums of dZ over the batch rows for columns
+// n0 .. n0 + 31 (8 row groups per column, each summed in row order, then the
+// groups in order) and the bias's Adagrad step. Its own workgroups, run beside
+// the GEMM tiles, with every load issued up front: at the end of the first
+// column's GEMM tiles (as before) its dependent round trips were the launch's tail.
+__device__ __forceinline__ void wgrad_bias(const WgJob &J, const Ctx &c, int n0, float *bs) {
+  const int t = threadIdx.x, col = t & 31, grp = t >> 5;
+  float bb = 0.f, ba = 0.f;
+  if (t < 32) {
+    bb = J.b[n0 + t];
+    ba = J.ab[n0 + t];
+  }
+  float dv[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++)
+    dv[i] = J.dZ[(int64_t)min(grp + 8 * i, c.M - 1) * J.lddz + n0 + col];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; i++)
+    if (grp + 8 * i < c.M) s += dv[i];
+  for (int m = grp + 256; m < c.M; m += 8) s += J.dZ[(int64_t)m * J.lddz + n0 + col];
+  bs[grp * 32 + col] = s;
+  __syncthreads();
+  if (t < 32) {
+    float g = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; q++) g += bs[q * 32 + t];
+    const int nn = n0 + t;
+    if (c.grad_only) {
+      J.b[nn] = g;
+      return;
+    }
+    const float na = ba + g * g;
+    J.ab[nn] = na;
+    J.b[nn] = bb - (c.lr * g) / (sqrtf(na) + c.eps);
+  }
+}
 
 template <int NCH>
 __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
@@ -693,6 +895,10 @@ __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
   const int qj = find_job(js.start, js.n, blockIdx.x);
   const WgJob &J = js.j[qj];
   const int tile = blockIdx.x - js.start[qj];
+  if (tile >= J.gemm_tiles) {
+    wgrad_bias(J, c, (tile - J.gemm_tiles) * kTile, &lds[0][0][0]);
+    return;
+  }
   const int k0 = (tile / J.tiles_n) * kTile, n0 = (tile % J.tiles_n) * kTile;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   // the Adagrad operands of the 4 elements this thread updates (reduce_tile's
@@ -708,31 +914,40 @@ __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
     }
   }
   f32x16 acc = {};
+  TDECL;
+  TSTAMP(0);
   if constexpr (NCH > 0) {
     // the reduction runs over the batch rows: every chunk's input rows
     // resolved (ids in one round trip), then all chunks' loads up front
-    SrcRow ra[NCH], rb[NCH];
+    const SrcK sa = src_k(J.a, c);
+    int mr[2 * NCH];
 #pragma unroll
-    for (int ch = 0; ch < NCH; ch++)
-      src_rows2(J.a, c, ch * kChunk + (t >> 3), ra[ch], rb[ch], 32);
+    for (int ch = 0; ch < NCH; ch++) {
+      mr[2 * ch] = ch * kChunk + (t >> 3);
+      mr[2 * ch + 1] = ch * kChunk + (t >> 3) + 32;
+    }
+    SrcRow rows[2 * NCH];
+    src_rows(sa, c, mr, rows);
+    TSTAMP(1);
     const int kk = k0 + 4 * (t & 7);
     float4 xa0[NCH], xa1[NCH], d0[NCH], d1[NCH];
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
       const int m = ch * kChunk + (t >> 3);
-      xa0[ch] = src_raw4(J.a, ra[ch], kk);
-      xa1[ch] = src_raw4(J.a, rb[ch], kk);
+      xa0[ch] = src_raw4(sa, rows[2 * ch], kk);
+      xa1[ch] = src_raw4(sa, rows[2 * ch + 1], kk);
       const float *dp = J.dZ + n0 + 4 * (t & 7);
       d0[ch] = *reinterpret_cast<const float4 *>(dp + (int64_t)(m < c.M ? m : 0) * J.lddz);
       d1[ch] = *reinterpret_cast<const float4 *>(dp + (int64_t)(m + 32 < c.M ? m + 32 : 0) * J.lddz);
     }
+    TSTAMP(2);
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
       const int m = ch * kChunk + (t >> 3);
       float *As = lds[ch & 1][0], *Bs = lds[ch & 1][1];
-      store_C(As, src_fix4(J.a, c, ra[ch], kk, xa0[ch], true),
-              src_fix4(J.a, c, rb[ch], kk, xa1[ch], true));
+      store_C(As, src_fix4(sa, rows[2 * ch], kk, xa0[ch], true),
+              src_fix4(sa, rows[2 * ch + 1], kk, xa1[ch], true));
       store_C(Bs, m < c.M ? d0[ch] : z4, m + 32 < c.M ? d1[ch] : z4);
       __syncthreads();
       mma_chunk(As, Bs, acc, w, lane);
@@ -763,7 +978,9 @@ __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
   }
   float v[4];
   int i0, j;
+  TSTAMP(3);
   reduce_tile(&lds[0][0][0], acc, v, i0, j);
+  TSTAMP(4);
   const int n = n0 + j;
 #pragma unroll
   for (int e = 0; e < 4; e++) {
@@ -779,38 +996,9 @@ __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
     J.aW[q] = na;
     J.W[q] = pW[e] - (c.lr * g) / (sqrtf(na) + c.eps);
   }
-  if (k0 != 0) return;
-  // bias: column sums of dZ over the batch rows (8 row groups per column)
-  __syncthreads();
-  float *bs = &lds[0][0][0];
-  {
-    const int col = t & 31, grp = t >> 5;
-    // rows grp, grp + 8, ... summed in that order; 8 loads in flight
-    float s = 0.f;
-    int m = grp;
-    for (; m + 56 < c.M; m += 64) {
-      float dv[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) dv[u] = J.dZ[(int64_t)(m + 8 * u) * J.lddz + n0 + col];
-#pragma unroll
-      for (int u = 0; u < 8; u++) s += dv[u];
-    }
-    for (; m < c.M; m += 8) s += J.dZ[(int64_t)m * J.lddz + n0 + col];
-    bs[grp * 32 + col] = s;
-  }
-  __syncthreads();
-  if (t < 32) {
-    float g = 0.f;
-#pragma unroll
-    for (int grp = 0; grp < 8; grp++) g += bs[grp * 32 + t];
-    const int nn = n0 + t;
-    if (c.grad_only) {
-      J.b[nn] = g;
-      return;
-    }
-    const float na = J.ab[nn] + g * g;
-    J.ab[nn] = na;
-    J.b[nn] = J.b[nn] - (c.lr * g) / (sqrtf(na) + c.eps);
+  if constexpr (NCH > 0) {
+    TSTAMP(5);
+    TFLUSH(5, 6);
   }
 }
 
@@ -882,6 +1070,7 @@ struct hgx_mlp {
   int ldJ = 0;
   // epoch scratch
   DevBuf perm, p_node, p_edge, p_label, keys, part, bloss, sort_tmp, idx_a, idx_b;
+  DevBuf xpf[2];  // prefetched input rows, alternating by batch (run_batch)
   hipEvent_t e0 = nullptr, e1 = nullptr;
   double ms = 0, flops = 0;
   int64_t samples = 0, batches = 0;
@@ -970,7 +1159,7 @@ int launch_fwd(hgx_ctx *ctx, const FwdJob *jobs, const int *tiles, int n,
                const Ctx &c) {
   int nch = n > 0 ? jobs[0].K / kChunk : 0;
   for (int q = 1; q < n; q++)
-    if (jobs[q].K != jobs[0].K) nch = 0;
+    if (!jobs[q].pf && jobs[q].K != jobs[0].K) nch = 0;
   switch (nch) {
     case 2: return launch_jobs(ctx, mlp_fwd<2>, jobs, tiles, n, c);
     case 3: return launch_jobs(ctx, mlp_fwd<3>, jobs, tiles, n, c);
@@ -1081,6 +1270,7 @@ WgJob wg_job(const hgx_mlp *m, int li, const Src &a, const DevBuf &dz, int lddz)
   j.ab = l.ab.as<float>();
   j.ldw = l.Np;
   j.tiles_n = l.Np / kTile;
+  j.gemm_tiles = (l.Kp / kTile) * j.tiles_n;
   return j;
 }
 
@@ -1101,9 +1291,14 @@ double layer_flops(const MlpLayer &l, int M, bool dx) {
 
 // Launches of one batch (training) or one chunk (predict, train = false).
 // pn/pe: sample ids by position; slot: this batch's loss partials.
+// Prefetch (combiner training): xin, when set, holds this batch's dropped-out
+// input rows ([node | edge] blocks of kPfRows rows, stride ldt), written by the
+// previous batch; xout, when set, receives the rows of the batch at position
+// next_pbase (next_M samples) from this batch's hidden-layer launch.
 int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
               const float *plab, uint32_t dstream, bool train, int upto,
-              float *slot, float *yout) {
+              float *slot, float *yout, float *xin = nullptr, float *xout = nullptr,
+              int64_t next_pbase = 0, int next_M = 0) {
   hgx_ctx *ctx = m->ctx;
   const int tm = (c.M + kTile - 1) / kTile;
   std::vector<MlpLayer> &L = m->L;
@@ -1136,8 +1331,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
     if (!train) return HGX_OK;
     WgJob wj[2] = {wg_job(m, l1, in, m->D_hn, L[l1].Np),
                    wg_job(m, l2, dense(m->A_hn, L[l1].Np, L[l1].Np), m->D_4, L[l2].Np)};
-    int wt[2] = {(L[l1].Kp / kTile) * (L[l1].Np / kTile),
-                 (L[l2].Kp / kTile) * (L[l2].Np / kTile)};
+    int wt[2] = {wj[0].gemm_tiles + wj[0].tiles_n, wj[1].gemm_tiles + wj[1].tiles_n};
     return launch_wgrad(ctx, wj, wt, 2, c);
   }
   // combiners
@@ -1145,8 +1339,17 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
   const int a = m->pre_n, b = m->pre_e, jn = m->joint_n, je = m->joint_e,
             hd = m->hidden, lb = m->label;
   const int NpJ = L[jn].Np;  // J = [J_n | J_e], each NpJ wide
-  const Src in_n = gather_src(m, 0, pn, pe, dstream, train);
-  const Src in_e = gather_src(m, 1, pn, pe, dstream, train);
+  Src in_n = gather_src(m, 0, pn, pe, dstream, train);
+  Src in_e = gather_src(m, 1, pn, pe, dstream, train);
+  if (xin) {
+    const int64_t side = (int64_t)kPfRows * m->ldt;
+    in_n = Src{};
+    in_n.x = xin;
+    in_e = Src{};
+    in_e.x = xin + side;
+    in_n.ldx = in_e.ldx = m->ldt;
+    in_n.width = in_e.width = m->ldt;
+  }
   {  // stage 1: pre layers
     const int which = upto;  // predict: 1 = node side only, 2 = edge only
     FwdJob f[2];
@@ -1174,10 +1377,24 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
     if (which == 1 || which == 2) return HGX_OK;
   }
   {  // stage 3: merged hidden (+ post layers)
-    FwdJob f[3];
-    int tl[3], n = 0;
+    FwdJob f[5];
+    int tl[5], n = 0;
     f[n] = fwd_job(m, hd, dense(m->A_j, m->ldJ, 2 * NpJ), m->A_hm.as<float>(), L[hd].Np);
     tl[n++] = tiles(hd);
+    if (xout) {  // the next batch's input rows, on the CUs this launch leaves idle
+      for (int q = 0; q < 2; q++) {
+        FwdJob p{};
+        p.pf = 1;
+        p.K = f[0].K;
+        p.a = gather_src(m, q, pn, pe, dstream, true);
+        p.pfX = xout + (int64_t)q * kPfRows * m->ldt;
+        p.pfld = m->ldt;
+        p.pfbase = next_pbase;
+        p.pfM = next_M;
+        f[n] = p;
+        tl[n++] = (kPfRows * (m->ldt / 4) + kPfItems - 1) / kPfItems;
+      }
+    }
     if (ae) {
       f[n] = fwd_job(m, m->post_n, dense(m->A_j, m->ldJ, NpJ), m->A_pn.as<float>(),
                      L[m->post_n].Np);
@@ -1299,7 +1516,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
   std::vector<int> wt;
   auto add = [&](int li, const Src &x, const DevBuf &dz) {
     wj.push_back(wg_job(m, li, x, dz, L[li].Np));
-    wt.push_back((L[li].Kp / kTile) * (L[li].Np / kTile));
+    wt.push_back(wj.back().gemm_tiles + wj.back().tiles_n);
   };
   add(a, in_n, m->D_hn);
   add(b, in_e, m->D_he);
@@ -1442,7 +1659,8 @@ int hgx_mlp_destroy(hgx_mlp *m) {
                     &m->A_re, &m->A_y, &m->D_hn, &m->D_he, &m->D_jn, &m->D_je,
                     &m->D_hm, &m->D_4, &m->D_pn, &m->D_pe, &m->D_rn, &m->D_re,
                     &m->perm, &m->p_node, &m->p_edge, &m->p_label, &m->keys,
-                    &m->part, &m->bloss, &m->sort_tmp, &m->idx_a, &m->idx_b};
+                    &m->part, &m->bloss, &m->sort_tmp, &m->idx_a, &m->idx_b,
+                    &m->xpf[0], &m->xpf[1]};
   for (DevBuf *b : bufs) hgx_release(*b);
   if (m->e0) hipEventDestroy(m->e0);
   if (m->e1) hipEventDestroy(m->e1);
@@ -1588,6 +1806,11 @@ int hgx_mlp_fit(hgx_mlp *m, int batch, int max_epochs, float lr, float eps,
   HGX_TRY(hgx_ensure(ctx, m->p_label, sizeof(float) * n));
   HGX_TRY(hgx_ensure(ctx, m->part, sizeof(float) * (size_t)kLossChunk * nslot));
   HGX_TRY(hgx_ensure(ctx, m->bloss, sizeof(double) * nb));
+  // combiners: batch bi + 1's input rows are gathered during batch bi
+  const bool prefetch = m->kind != HGX_MLP_LP_CLASSIFIER && ctx->tune.mlp_prefetch;
+  if (prefetch)
+    for (DevBuf &x : m->xpf)
+      HGX_TRY(hgx_ensure(ctx, x, sizeof(float) * 2 * kPfRows * (size_t)m->ldt));
   int *perm = m->perm.as<int>();
   unsigned long long *kin = nullptr, *kout = nullptr;
   int *vin = nullptr;
@@ -1648,9 +1871,13 @@ int hgx_mlp_fit(hgx_mlp *m, int batch, int max_epochs, float lr, float eps,
         c.lr = lr;
         c.eps = eps;
         c.grad_only = grad_at >= 0 && ep * nb + bi >= grad_at;
+        const int64_t nx = (bi + 1) * batch;
+        float *xin = prefetch && bi > 0 ? m->xpf[bi & 1].as<float>() : nullptr;
+        float *xout = prefetch && bi + 1 < nb ? m->xpf[(bi + 1) & 1].as<float>() : nullptr;
         HGX_TRY(run_batch(m, c, m->p_node.as<int>(), m->p_edge.as<int>(),
                           m->p_label.as<float>(), dstream, true, 0,
-                          m->part.as<float>() + (bi - c0) * nslot, nullptr));
+                          m->part.as<float>() + (bi - c0) * nslot, nullptr, xin, xout, nx,
+                          (int)std::min<int64_t>(batch, n - nx)));
         m->flops += batch_flops(m, c.M);
       }
       hipLaunchKernelGGL(mlp_loss_reduce, dim3((unsigned)((c1 - c0 + 255) / 256)),
@@ -1682,6 +1909,21 @@ int hgx_mlp_fit(hgx_mlp *m, int batch, int max_epochs, float lr, float eps,
     }
   }
   if (epochs_run) *epochs_run = ran;
+#if HGX_MLP_DIAG_TIME
+  {
+    unsigned long long t[8][8], nn[8];
+    hipMemcpyFromSymbol(t, HIP_SYMBOL(g_mlp_t), sizeof(t));
+    hipMemcpyFromSymbol(nn, HIP_SYMBOL(g_mlp_n), sizeof(nn));
+    const char *nm[8] = {"fwd8 gather", "fwd6", "fwd8 dense", "bwd FH", "bwd", "wgrad", "fwd other", "-"};
+    for (int k = 0; k < 7; k++)
+      if (nn[k]) {
+        fprintf(stderr, "[mlp diag] %-12s wg %10llu  us to:", nm[k], nn[k]);
+        for (int q = 1; q < 8; q++)
+          if (q < 6 || t[k][q]) fprintf(stderr, " %6.2f", t[k][q] * 0.01 / nn[k]);
+        fprintf(stderr, "\n");
+      }
+  }
+#endif
   return HGX_OK;
 }
 

@@ -80,6 +80,10 @@ int hgx_synchronize(hgx_ctx *ctx);
  *   "mlp_fuse_head"    combiner MLP training: 1 the label head computed in
  *                      the launch forming the joint layers' deltas (default,
  *                      bit-identical), 0 its own launch
+ *   "mlp_prefetch"     combiner MLP training: 1 batch b + 1's dropped-out
+ *                      input rows gathered by extra workgroups of batch b's
+ *                      hidden-layer launch (default, bit-identical), 0 the
+ *                      first layer and its weight gradient gather them
  *   "train_prep_overlap" trainer: 1 prepare chunk c + 1 (train_prep /
  *                      train_place) on a second stream while chunk c trains,
  *                      0 in line before each chunk (default); the same

@@ -119,6 +119,35 @@ def test_fused_head_equals_head_launch(ctx, kind, I, D):
   np.testing.assert_array_equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("kind,I,D,batch", [(1, 40, 24, 256), (2, 70, 33, 100),
+                                            (1, 512, 256, 256), (2, 19, 7, 64)])
+def test_prefetch_equals_gather(ctx, kind, I, D, batch):
+  """Combiner training gathers batch b + 1's dropped-out input rows inside
+  batch b's hidden-layer launch (tuning mlp_prefetch, default 1); the first
+  layer and its weight gradient then read them densely. Trained weights and
+  epoch losses are bit for bit those of gathering in place (ragged last
+  batch included: 900 samples)."""
+  rng, nt, et, nr, er, lab = make_case(kind, I, D, 900, 6)
+  w0 = None
+  res = []
+  for pf in (1, 0):
+    ctx.set_tuning("mlp_prefetch", pf)
+    try:
+      m = _hgx.Mlp(ctx, kind, I, D)
+      if w0 is None:
+        w0 = glorot(m.shapes, np.random.default_rng(3), 0.1)
+      m.set_weights(w0)
+      m.set_tables(nt, et)
+      m.set_samples(nr, er, lab)
+      losses = m.fit(batch=batch, max_epochs=2, min_delta=-1e30, seed=9)
+      res.append((m.get_weights(), np.asarray(losses)))
+      m.close()
+    finally:
+      ctx.set_tuning("mlp_prefetch", 1)
+  np.testing.assert_array_equal(res[0][0], res[1][0])
+  np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
 def test_small_batches_and_single_sample(ctx):
   m, _, wg, wc, gl, cl = run_both(ctx, 2, 20, 12, 301, 1, batch=100)
   assert np.abs(wg - wc).max() == 0.0

@@ -28,6 +28,8 @@ def main():
   p.add_argument("--rows", type=int, default=1_000_000)
   p.add_argument("--dim", type=int, default=256)
   p.add_argument("--epochs", type=int, default=2)
+  p.add_argument("--tune", action="append", default=[],
+                 help="KEY=VALUE for hgx_set_tuning (repeatable)")
   a = p.parse_args()
   from hypergraphembedding_amd import _hgx
   d, ind = a.dim, 2 * a.dim
@@ -38,6 +40,9 @@ def main():
   er = rs.randint(0, a.rows // 2, a.samples).astype(np.int32)
   lab = (rs.random_sample(a.samples) < 1.0 / 6).astype(np.float32)
   ctx = _hgx.Context(0)
+  for kv in a.tune:
+    k, v = kv.split("=")
+    ctx.set_tuning(k, int(v))
   mlp = _hgx.Mlp(ctx, _hgx.MLP_NE_SUPERVISED, ind, d)
   lims = [np.sqrt(6.0 / (k + n)) for k, n in mlp.shapes]
   w0 = np.concatenate([np.concatenate([rs.uniform(-l, l, k * n), np.zeros(n)])
