@@ -573,9 +573,15 @@ constexpr int kHeadKH = 8;
 // global memory; S (optional): dZprev also into LDS rows mb - m0 of S (row
 // stride sld floats), every column k < K (rows past M zero). lsum: lane 0's
 // sum of the squared errors of the wave's valid rows, in row order.
-__device__ __forceinline__ void head_wave(const HeadJob &h, const Ctx &c, int mb,
-                                          int lane, bool gstore, float *S, int srow,
-                                          int sld, float &lsum) {
+// ACT / ACTP >= 0: the head's / the previous layer's activation known at
+// compile time (straight-line code the scheduler can interleave across the
+// 8 rows: with one wave per SIMD a per-row activation branch left every
+// dependent VALU step exposed); -1: read from h.
+template <int ACT = -1, int ACTP = -1, int KH = kHeadKH>
+__device__ __forceinline__ void head_wave_t(const HeadJob &h, const Ctx &c, int mb,
+                                            int lane, bool gstore, float *S, int srow,
+                                            int sld, float &lsum) {
+  const int act = ACT >= 0 ? ACT : h.act, act_prev = ACTP >= 0 ? ACTP : h.act_prev;
   // Every load is issued, and consumed, before the first store: on this
   // architecture the vector-memory counter also counts stores, so a load
   // waited for after a store waits for that store too. The same arithmetic
@@ -587,13 +593,13 @@ __device__ __forceinline__ void head_wave(const HeadJob &h, const Ctx &c, int mb
   for (int s = 0; s < 8; s++)
     lab[s] = h.loss ? h.label[c.pbase + min(mb + s, c.M - 1)] : 0.f;
   const float bias = h.b[0];
-  const bool regs = h.K <= 64 * kHeadKH;
-  float zs[8], wv[kHeadKH], hv[kHeadKH][8];
+  const bool regs = h.K <= 64 * KH;
+  float zs[8], wv[KH], hv[KH][8];
 #pragma unroll
   for (int s = 0; s < 8; s++) zs[s] = 0.f;
   if (regs) {
 #pragma unroll
-    for (int kk = 0; kk < kHeadKH; kk++) {
+    for (int kk = 0; kk < KH; kk++) {
       const int k = min(lane + 64 * kk, h.K - 1);
       wv[kk] = h.W[(int64_t)k * h.ldw];
 #pragma unroll
@@ -601,7 +607,7 @@ __device__ __forceinline__ void head_wave(const HeadJob &h, const Ctx &c, int mb
         hv[kk][s] = h.H[(int64_t)min(mb + s, c.M - 1) * h.ldh + k];
     }
 #pragma unroll
-    for (int kk = 0; kk < kHeadKH; kk++) {
+    for (int kk = 0; kk < KH; kk++) {
       const bool in = lane + 64 * kk < h.K;
 #pragma unroll
       for (int s = 0; s < 8; s++)
@@ -623,12 +629,12 @@ __device__ __forceinline__ void head_wave(const HeadJob &h, const Ctx &c, int mb
 #pragma unroll
   for (int s = 0; s < 8; s++) {
     const bool valid = mb + s < c.M;
-    ys[s] = act_f(h.act, (valid ? zs[s] : 0.f) + bias);
+    ys[s] = act_f(act, (valid ? zs[s] : 0.f) + bias);
     float dz = 0.f;
     if (h.loss && valid) {
       const float diff = ys[s] - lab[s];
       if (lane == 0) lsum += diff * diff;
-      dz = h.lw * 2.0f * diff / (float)c.M * act_d(h.act, ys[s]);
+      dz = h.lw * 2.0f * diff / (float)c.M * act_d(act, ys[s]);
     }
     dzs[s] = dz;
   }
@@ -644,13 +650,13 @@ __device__ __forceinline__ void head_wave(const HeadJob &h, const Ctx &c, int mb
   if (!h.loss) return;
   if (regs) {
 #pragma unroll
-    for (int kk = 0; kk < kHeadKH; kk++) {
+    for (int kk = 0; kk < KH; kk++) {
       const int k = lane + 64 * kk;
       if (k < h.K) {
 #pragma unroll
         for (int s = 0; s < 8; s++) {
           const int m = mb + s;
-          const float v = m < c.M ? dzs[s] * wv[kk] * act_d(h.act_prev, hv[kk][s]) : 0.f;
+          const float v = m < c.M ? dzs[s] * wv[kk] * act_d(act_prev, hv[kk][s]) : 0.f;
           if (gstore) h.dZprev[(int64_t)m * h.ldp + k] = v;
           if (S) S[(srow + s) * sld + k] = v;
         }
@@ -664,11 +670,30 @@ __device__ __forceinline__ void head_wave(const HeadJob &h, const Ctx &c, int mb
         const int m = mb + s;
         const bool valid = m < c.M;
         const float hvv = h.H[(int64_t)min(m, c.M - 1) * h.ldh + k];
-        const float v = valid ? dzs[s] * wk * act_d(h.act_prev, hvv) : 0.f;
+        const float v = valid ? dzs[s] * wk * act_d(act_prev, hvv) : 0.f;
         if (gstore) h.dZprev[(int64_t)m * h.ldp + k] = v;
         if (S) S[(srow + s) * sld + k] = v;
       }
     }
+  }
+}
+
+// head_wave_t with the combiners' and the classifier's (sigmoid head over a
+// relu layer) activations compiled in and the input's 64-column groups
+// counted exactly (KH = 2 / 4: no clamped duplicate loads taking
+// vector-memory counter slots), any other case read at run time
+__device__ __forceinline__ void head_wave(const HeadJob &h, const Ctx &c, int mb, int lane,
+                                          bool gstore, float *S, int srow, int sld,
+                                          float &lsum) {
+  if (h.act == ACT_SIGMOID && h.act_prev == ACT_RELU) {
+    if (h.K <= 128)
+      head_wave_t<ACT_SIGMOID, ACT_RELU, 2>(h, c, mb, lane, gstore, S, srow, sld, lsum);
+    else if (h.K <= 256)
+      head_wave_t<ACT_SIGMOID, ACT_RELU, 4>(h, c, mb, lane, gstore, S, srow, sld, lsum);
+    else
+      head_wave_t<ACT_SIGMOID, ACT_RELU>(h, c, mb, lane, gstore, S, srow, sld, lsum);
+  } else {
+    head_wave_t<>(h, c, mb, lane, gstore, S, srow, sld, lsum);
   }
 }
 
