@@ -879,8 +879,8 @@ struct WgJob {
 // A bias workgroup of WGRAD: column sums of dZ over the batch rows for columns
 // n0 .. n0 + 31 (8 row groups per column, each summed in row order, then the
 // groups in order) and the bias's Adagrad step. Its own workgroups, run beside
-// the GEMM tiles, with every load issued up front: at the end of the first
-// column's GEMM tiles (as before) its dependent round trips were the launch's tail.
+// the GEMM tiles, with every load issued up front: appended to the k0 = 0 GEMM
+// tiles (before r04) its dependent load rounds were the launch's tail.
 __device__ __forceinline__ void wgrad_bias(const WgJob &J, const Ctx &c, int n0, float *bs) {
   const int t = threadIdx.x, col = t & 31, grp = t >> 5;
   float bb = 0.f, ba = 0.f;
