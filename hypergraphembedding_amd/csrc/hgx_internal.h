@@ -62,8 +62,9 @@ struct Tuning {
   // launch
   int mlp_fuse_head = 1;
   // combiner MLP training: 1 batch b + 1's input rows gathered (with their
-  // dropout) by extra workgroups of batch b's hidden-layer launch, so its
-  // first layer and weight gradient read a dense operand; 0 both gather
+  // dropout) by extra workgroups of batch b's hidden-layer launch (2: of its
+  // joint-layer launch), so its first layer and weight gradient read a dense
+  // operand; 0 both gather
   int mlp_prefetch = 1;
   // trainer: chunk c + 1 prepared (train_prep / train_place) on a second
   // stream while chunk c trains (1), on the same stream one chunk ahead

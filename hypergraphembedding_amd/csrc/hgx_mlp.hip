@@ -1375,10 +1375,26 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
     in_n.ldx = in_e.ldx = m->ldt;
     in_n.width = in_e.width = m->ldt;
   }
+  // the next batch's input rows, on the CUs a launch leaves idle (tuning
+  // mlp_prefetch: 1 the hidden layer's launch, 2 the joint layers')
+  auto add_prefetch = [&](FwdJob *f, int *tl, int &n) {
+    for (int q = 0; q < 2; q++) {
+      FwdJob p{};
+      p.pf = 1;
+      p.K = f[0].K;
+      p.a = gather_src(m, q, pn, pe, dstream, true);
+      p.pfX = xout + (int64_t)q * kPfRows * m->ldt;
+      p.pfld = m->ldt;
+      p.pfbase = next_pbase;
+      p.pfM = next_M;
+      f[n] = p;
+      tl[n++] = (kPfRows * (m->ldt / 4) + kPfItems - 1) / kPfItems;
+    }
+  };
   {  // stage 1: pre layers
     const int which = upto;  // predict: 1 = node side only, 2 = edge only
-    FwdJob f[2];
-    int tl[2], n = 0;
+    FwdJob f[4];
+    int tl[4], n = 0;
     if (which != 2) {
       f[n] = fwd_job(m, a, in_n, m->A_hn.as<float>(), L[a].Np);
       tl[n++] = tiles(a);
@@ -1398,6 +1414,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
                      m->ldJ);
       tl[n++] = tiles(je);
     }
+    if (xout && ctx->tune.mlp_prefetch == 2) add_prefetch(f, tl, n);
     HGX_TRY(launch_fwd(ctx, f, tl, n, c));
     if (which == 1 || which == 2) return HGX_OK;
   }
@@ -1406,20 +1423,7 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
     int tl[5], n = 0;
     f[n] = fwd_job(m, hd, dense(m->A_j, m->ldJ, 2 * NpJ), m->A_hm.as<float>(), L[hd].Np);
     tl[n++] = tiles(hd);
-    if (xout) {  // the next batch's input rows, on the CUs this launch leaves idle
-      for (int q = 0; q < 2; q++) {
-        FwdJob p{};
-        p.pf = 1;
-        p.K = f[0].K;
-        p.a = gather_src(m, q, pn, pe, dstream, true);
-        p.pfX = xout + (int64_t)q * kPfRows * m->ldt;
-        p.pfld = m->ldt;
-        p.pfbase = next_pbase;
-        p.pfM = next_M;
-        f[n] = p;
-        tl[n++] = (kPfRows * (m->ldt / 4) + kPfItems - 1) / kPfItems;
-      }
-    }
+    if (xout && ctx->tune.mlp_prefetch == 1) add_prefetch(f, tl, n);
     if (ae) {
       f[n] = fwd_job(m, m->post_n, dense(m->A_j, m->ldJ, NpJ), m->A_pn.as<float>(),
                      L[m->post_n].Np);

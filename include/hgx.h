@@ -82,7 +82,8 @@ int hgx_synchronize(hgx_ctx *ctx);
  *                      bit-identical), 0 its own launch
  *   "mlp_prefetch"     combiner MLP training: 1 batch b + 1's dropped-out
  *                      input rows gathered by extra workgroups of batch b's
- *                      hidden-layer launch (default, bit-identical), 0 the
+ *                      hidden-layer launch (default, bit-identical), 2 of its
+ *                      joint-layer launch (measured 0.4% slower), 0 the
  *                      first layer and its weight gradient gather them
  *   "train_prep_overlap" trainer: 1 prepare chunk c + 1 (train_prep /
  *                      train_place) on a second stream while chunk c trains,
