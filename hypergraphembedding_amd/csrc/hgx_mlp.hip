@@ -69,14 +69,21 @@ constexpr int kMaxJobs = 12;
 #define HGX_MLP_DIAG_TIME 0
 #endif
 #if HGX_MLP_DIAG_TIME
-__device__ unsigned long long g_mlp_t[8][8];
+__device__ unsigned long long g_mlp_t[8][12];
 __device__ unsigned long long g_mlp_n[8];
 #define TSTAMP(i)                                             \
   do {                                                        \
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
     ts[i] = __builtin_amdgcn_s_memrealtime();                 \
   } while (0)
-#define TDECL unsigned long long ts[8] = {}
+#define TDECL unsigned long long ts[12] = {}
+#define HSTAMP(i)                                                  \
+  do {                                                             \
+    if (tsp) {                                                     \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  \
+      tsp[i] = __builtin_amdgcn_s_memrealtime();                   \
+    }                                                              \
+  } while (0)
 #define TFLUSH(kind, n)                                                   \
   do {                                                                    \
     if (threadIdx.x == 0) {                                               \
@@ -86,6 +93,7 @@ __device__ unsigned long long g_mlp_n[8];
   } while (0)
 #else
 #define TSTAMP(i) (void)0
+#define HSTAMP(i) (void)0
 #define TDECL (void)0
 #define TFLUSH(kind, n) (void)0
 #endif
@@ -580,7 +588,8 @@ constexpr int kHeadKH = 8;
 template <int ACT = -1, int ACTP = -1, int KH = kHeadKH>
 __device__ __forceinline__ void head_wave_t(const HeadJob &h, const Ctx &c, int mb,
                                             int lane, bool gstore, float *S, int srow,
-                                            int sld, float &lsum) {
+                                            int sld, float &lsum,
+                                            unsigned long long *tsp = nullptr) {
   const int act = ACT >= 0 ? ACT : h.act, act_prev = ACTP >= 0 ? ACTP : h.act_prev;
   // Every load is issued, and consumed, before the first store: on this
   // architecture the vector-memory counter also counts stores, so a load
@@ -623,21 +632,39 @@ __device__ __forceinline__ void head_wave_t(const HeadJob &h, const Ctx &c, int 
       }
     }
   }
-#pragma unroll
-  for (int s = 0; s < 8; s++) zs[s] = hgx::group_allreduce_sum<64>(zs[s]);
+  HSTAMP(8);
+  // the 8 rows' wave sums interleaved (group_allreduce_sum<64>'s bits)
+  hgx::wave_allreduce_sum_n<8>(zs);
+  HSTAMP(9);
+  // Row s's output, error and delta computed by lanes s, s + 8, ... at once
+  // and read back per row: eight rows one after another left every step of
+  // the sigmoid and of two IEEE divisions exposed (the divisions' VCC
+  // hand-off keeps them from interleaving). The same arithmetic per row.
   float ys[8], dzs[8];
+  const bool loss = h.loss;
+  {
+    const int sr = lane & 7;
+    float zr = zs[0], lr = lab[0];
 #pragma unroll
-  for (int s = 0; s < 8; s++) {
-    const bool valid = mb + s < c.M;
-    ys[s] = act_f(act, (valid ? zs[s] : 0.f) + bias);
-    float dz = 0.f;
-    if (h.loss && valid) {
-      const float diff = ys[s] - lab[s];
-      if (lane == 0) lsum += diff * diff;
-      dz = h.lw * 2.0f * diff / (float)c.M * act_d(act, ys[s]);
+    for (int s = 1; s < 8; s++) {
+      zr = sr == s ? zs[s] : zr;
+      lr = sr == s ? lab[s] : lr;
     }
-    dzs[s] = dz;
+    const bool validr = mb + sr < c.M;
+    const float yr = act_f(act, (validr ? zr : 0.f) + bias);
+    const float diffr = yr - lr;
+    const float dzr =
+        loss && validr ? h.lw * 2.0f * diffr / (float)c.M * act_d(act, yr) : 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+      ys[s] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yr), s));
+      dzs[s] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dzr), s));
+      const float diff = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(diffr), s));
+      const bool on = loss && mb + s < c.M;
+      lsum = (on && lane == 0) ? lsum + diff * diff : lsum;
+    }
   }
+  HSTAMP(10);
   // stores
   if (gstore) {
 #pragma unroll
@@ -649,18 +676,28 @@ __device__ __forceinline__ void head_wave_t(const HeadJob &h, const Ctx &c, int 
   }
   if (!h.loss) return;
   if (regs) {
+    // every value first, then the LDS rows, then (one tile per row block)
+    // the global copy: no store waits behind a per-element branch
+    float dv[KH][8];
 #pragma unroll
-    for (int kk = 0; kk < KH; kk++) {
-      const int k = lane + 64 * kk;
-      if (k < h.K) {
+    for (int kk = 0; kk < KH; kk++)
 #pragma unroll
-        for (int s = 0; s < 8; s++) {
-          const int m = mb + s;
-          const float v = m < c.M ? dzs[s] * wv[kk] * act_d(act_prev, hv[kk][s]) : 0.f;
-          if (gstore) h.dZprev[(int64_t)m * h.ldp + k] = v;
-          if (S) S[(srow + s) * sld + k] = v;
-        }
-      }
+      for (int s = 0; s < 8; s++)
+        dv[kk][s] = mb + s < c.M ? dzs[s] * wv[kk] * act_d(act_prev, hv[kk][s]) : 0.f;
+    if (S) {
+#pragma unroll
+      for (int kk = 0; kk < KH; kk++)
+        if (lane + 64 * kk < h.K)
+#pragma unroll
+          for (int s = 0; s < 8; s++) S[(srow + s) * sld + lane + 64 * kk] = dv[kk][s];
+    }
+    if (gstore) {
+#pragma unroll
+      for (int kk = 0; kk < KH; kk++)
+        if (lane + 64 * kk < h.K)
+#pragma unroll
+          for (int s = 0; s < 8; s++)
+            h.dZprev[(int64_t)(mb + s) * h.ldp + lane + 64 * kk] = dv[kk][s];
     }
   } else {
     for (int k = lane; k < h.K; k += 64) {
@@ -684,16 +721,16 @@ __device__ __forceinline__ void head_wave_t(const HeadJob &h, const Ctx &c, int 
 // vector-memory counter slots), any other case read at run time
 __device__ __forceinline__ void head_wave(const HeadJob &h, const Ctx &c, int mb, int lane,
                                           bool gstore, float *S, int srow, int sld,
-                                          float &lsum) {
+                                          float &lsum, unsigned long long *tsp = nullptr) {
   if (h.act == ACT_SIGMOID && h.act_prev == ACT_RELU) {
     if (h.K <= 128)
-      head_wave_t<ACT_SIGMOID, ACT_RELU, 2>(h, c, mb, lane, gstore, S, srow, sld, lsum);
+      head_wave_t<ACT_SIGMOID, ACT_RELU, 2>(h, c, mb, lane, gstore, S, srow, sld, lsum, tsp);
     else if (h.K <= 256)
-      head_wave_t<ACT_SIGMOID, ACT_RELU, 4>(h, c, mb, lane, gstore, S, srow, sld, lsum);
+      head_wave_t<ACT_SIGMOID, ACT_RELU, 4>(h, c, mb, lane, gstore, S, srow, sld, lsum, tsp);
     else
-      head_wave_t<ACT_SIGMOID, ACT_RELU>(h, c, mb, lane, gstore, S, srow, sld, lsum);
+      head_wave_t<ACT_SIGMOID, ACT_RELU>(h, c, mb, lane, gstore, S, srow, sld, lsum, tsp);
   } else {
-    head_wave_t<>(h, c, mb, lane, gstore, S, srow, sld, lsum);
+    head_wave_t<>(h, c, mb, lane, gstore, S, srow, sld, lsum, tsp);
   }
 }
 
@@ -797,7 +834,11 @@ __global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c, Head
     if constexpr (FH) {
       float lsum = 0.f;
       const bool gst = qj == 0 && k0 == 0;
+#if HGX_MLP_DIAG_TIME
+      head_wave(hj, c, m0 + w * 8, lane, gst, s_hd, w * 8, kHdLd, lsum, ts);
+#else
       head_wave(hj, c, m0 + w * 8, lane, gst, s_hd, w * 8, kHdLd, lsum);
+#endif
       TSTAMP(6);
       if (gst) head_partial(hj, c, m0 / kTile, lsum);
       __syncthreads();
@@ -862,7 +903,7 @@ __global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c, Head
   }
   if constexpr (NCH > 0) {
     TSTAMP(5);
-    TFLUSH(FH ? 3 : 4, FH ? 8 : 6);
+    TFLUSH(FH ? 3 : 4, FH ? 11 : 6);
   }
 }
 
@@ -1940,14 +1981,14 @@ int hgx_mlp_fit(hgx_mlp *m, int batch, int max_epochs, float lr, float eps,
   if (epochs_run) *epochs_run = ran;
 #if HGX_MLP_DIAG_TIME
   {
-    unsigned long long t[8][8], nn[8];
+    unsigned long long t[8][12], nn[8];
     hipMemcpyFromSymbol(t, HIP_SYMBOL(g_mlp_t), sizeof(t));
     hipMemcpyFromSymbol(nn, HIP_SYMBOL(g_mlp_n), sizeof(nn));
     const char *nm[8] = {"fwd8 gather", "fwd6", "fwd8 dense", "bwd FH", "bwd", "wgrad", "fwd other", "-"};
     for (int k = 0; k < 7; k++)
       if (nn[k]) {
         fprintf(stderr, "[mlp diag] %-12s wg %10llu  us to:", nm[k], nn[k]);
-        for (int q = 1; q < 8; q++)
+        for (int q = 1; q < 11; q++)
           if (q < 6 || t[k][q]) fprintf(stderr, " %6.2f", t[k][q] * 0.01 / nn[k]);
         fprintf(stderr, "\n");
       }
