@@ -520,12 +520,22 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd(Jobs<FwdJob> js, Ctx c) {
   TSTAMP(4);
   const int n = n0 + j;
   float lsum = 0.f;
+  // the four outputs first, with the activation chosen once per workgroup
+  // (straight-line, so the four sigmoids and divisions interleave), then
+  // the stores
+  float ya[4];
+  if (J.act == ACT_SIGMOID) {
+#pragma unroll
+    for (int e = 0; e < 4; e++) ya[e] = act_f(ACT_SIGMOID, v[e] + bias);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; e++) ya[e] = act_f(ACT_RELU, v[e] + bias);
+  }
 #pragma unroll
   for (int e = 0; e < 4; e++) {
     const int m = m0 + i0 + e;
-    float y = act_f(J.act, v[e] + bias);
     const bool valid = m < c.M && n < J.Nreal;
-    if (!valid) y = 0.f;
+    const float y = valid ? ya[e] : 0.f;
     J.Y[(int64_t)m * J.ldy + n] = y;
     if (J.loss) {
       float dz = 0.f;
@@ -1048,19 +1058,27 @@ __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
   reduce_tile(&lds[0][0][0], acc, v, i0, j);
   TSTAMP(4);
   const int n = n0 + j;
+  if (c.grad_only) {
 #pragma unroll
-  for (int e = 0; e < 4; e++) {
-    const int64_t q = (int64_t)(k0 + i0 + e) * J.ldw + n;
-    const float g = v[e];
-    if (c.grad_only) {
-      J.W[q] = g;
-      continue;
+    for (int e = 0; e < 4; e++) J.W[(int64_t)(k0 + i0 + e) * J.ldw + n] = v[e];
+  } else {
+    // the four Adagrad steps first (their square roots and divisions
+    // interleave), then the stores. Plain sqrtf is correctly rounded on
+    // gfx950 (__fsqrt_rn is not: 15% of 1M inputs off by an ulp,
+    // tools/fp_check.hip), as the CPU side's is
+    float na[4], nw[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const float g = v[e];
+      na[e] = pA[e] + g * g;
+      nw[e] = pW[e] - (c.lr * g) / (sqrtf(na[e]) + c.eps);
     }
-    // plain sqrtf is correctly rounded on gfx950 (__fsqrt_rn is not: 15% of
-    // 1M inputs off by an ulp, tools/fp_check.hip), as the CPU side's is
-    const float na = pA[e] + g * g;
-    J.aW[q] = na;
-    J.W[q] = pW[e] - (c.lr * g) / (sqrtf(na) + c.eps);
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int64_t q = (int64_t)(k0 + i0 + e) * J.ldw + n;
+      J.aW[q] = na[e];
+      J.W[q] = nw[e];
+    }
   }
   if constexpr (NCH > 0) {
     TSTAMP(5);
