@@ -74,6 +74,8 @@ def parse():
   p.add_argument("--no-c5", action="store_true",
                  help="skip the C5 combiner leg (inside the C4 leg)")
   p.add_argument("--c5-positives", type=int, default=1_000_000)
+  p.add_argument("--c5-cpu-samples", type=int, default=100_000,
+                 help="samples of the C5 combiner's CPU-baseline slice")
   p.add_argument("--no-c4", action="store_true",
                  help="skip the power-law 10M/5M measurements")
   p.add_argument("--no-extra", action="store_true",
@@ -99,7 +101,23 @@ _AFFINITY = frozenset(os.sched_getaffinity(0))
 
 
 def cpu_threads():
-  return max(1, min(16, len(_AFFINITY)))
+  """Threads of the CPU legs: every core of the process's affinity, capped by
+  OMP_NUM_THREADS where the environment sets one (the GPU pool sets it to
+  its per-GPU CPU share, 16: the host's other cores belong to the other
+  GPUs' jobs). The affinity size is reported beside it (affinity_cores)."""
+  cap = os.environ.get("OMP_NUM_THREADS", "")
+  n = len(_AFFINITY)
+  if cap.isdigit() and int(cap) > 0:
+    n = min(n, int(cap))
+  return max(1, n)
+
+
+def cpu_share_note(threads):
+  cap = os.environ.get("OMP_NUM_THREADS")
+  return {"cores_used": threads, "affinity_cores": len(_AFFINITY),
+          "omp_num_threads_env": cap,
+          "policy": "all affinity cores, capped by OMP_NUM_THREADS (the "
+                    "pool's per-GPU CPU share) when set"}
 
 
 def restore_affinity():
@@ -294,6 +312,19 @@ def main():
                                          batch=args.batch, epochs=1,
                                          threads=threads), 3)
     cpu_s = float(np.median(runs))
+    # thread scaling of the same trainer on the first 500k records: how the
+    # port's rate grows with cores (the per-core rate a larger host share
+    # would multiply)
+    ms_ = min(m, 500_000)
+    scaling = {}
+    for tt in sorted({1 << i for i in range(threads.bit_length())} | {threads}):
+      r_ = timed_runs(lambda: O.train_mt(cidx[:ms_], ctgt[:ms_],
+                                         args.num_neighbors, nt, et,
+                                         O.LOSS_MSE, O.ACT_RELU,
+                                         batch=args.batch, epochs=1,
+                                         threads=tt), 1)
+      scaling[str(tt)] = round(ms_ / r_[0], 1)
+    restore_affinity()
     m1 = min(m, 500_000)
     t = time.perf_counter()
     O.train(cidx[:m1], ctgt[:m1], args.num_neighbors, nt, et, O.LOSS_MSE,
@@ -309,6 +340,8 @@ def main():
                      f"oracle/cpu_train_mt.c on {threads} OpenMP threads, "
                      f"median of 3 runs ({cpu_s:.1f} s)",
            "runs_records_per_s": [round(m / r, 1) for r in runs],
+           "threads": cpu_share_note(threads),
+           "thread_scaling_records_per_s": scaling,
            "single_thread_value": round(m1 / cpu1_s, 1),
            "single_thread_sample": f"first {m1} of those records, "
                                    f"oracle/hgref.c hgref_train, {cpu1_s:.1f} s"}
@@ -606,6 +639,7 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
     restore_affinity()
     hobe4["cpu_port_records_per_s"] = round(m4 / cpu4_s, 1)
     hobe4["cpu_port_cores"] = threads
+    hobe4["cpu_port_threads"] = cpu_share_note(threads)
     hobe4["cpu_port_sample"] = (f"{m4} random records of this stream, d={d4}, "
                                 f"tables {big.N + 1} + {big.E + 1} rows, 1 epoch, "
                                 f"oracle/cpu_train_mt.c on {threads} OpenMP "
@@ -624,6 +658,7 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
         "ms_per_iter": round(ca_s / 3 * 1e3, 1),
         "gbps": round(b_iter4 * 3 / ca_s / 1e9, 2),
         "cores": threads, "kind": "port", "dtype": "f64",
+        "threads": cpu_share_note(threads),
         "sample": "3 iterations on the whole power-law 10M/5M graph, "
                   "oracle/hgref.c hgref_algdist (float64 like the reference, "
                   f"OpenMP over rows), {ca_s:.1f} s; gbps in the fp32 "
@@ -666,10 +701,19 @@ def bench_c5(args, ctx, big):
   samples_s = time.perf_counter() - t
   mlp = _hgx.Mlp(ctx, _hgx.MLP_NE_SUPERVISED, 2 * d, d)
   lims = [np.sqrt(6.0 / (k + n)) for k, n in mlp.shapes]
-  mlp.set_weights(np.concatenate([np.concatenate([rs.uniform(-l, l, k * n),
-                                                  np.zeros(n)])
-                                  for l, (k, n) in zip(lims, mlp.shapes)]
-                                 ).astype(np.float32))
+  w0 = np.concatenate([np.concatenate([rs.uniform(-l, l, k * n), np.zeros(n)])
+                       for l, (k, n) in zip(lims, mlp.shapes)]).astype(np.float32)
+  mlp.set_weights(w0)
+  # the CPU baseline's slice: its samples and only the table rows they read
+  # (relabelled; the arithmetic does not depend on row ids)
+  cpu_slice = None
+  if not args.no_cpu and args.c5_cpu_samples > 0:
+    m = min(args.c5_cpu_samples, lab.size)
+    sel = np.random.RandomState(22).choice(lab.size, m, replace=False)
+    un, inv_n = np.unique(nr[sel], return_inverse=True)
+    ue, inv_e = np.unique(er[sel], return_inverse=True)
+    cpu_slice = (nt[un], et[ue], inv_n.astype(np.int32), inv_e.astype(np.int32),
+                 lab[sel].copy())
   mlp.set_tables(nt, et)
   del nt, et
   mlp.set_samples(nr, er, lab)
@@ -686,6 +730,31 @@ def bench_c5(args, ctx, big):
   ms, n, flops, wall = runs[-1]
   sps = n / (ms / 1e3)
   tf = flops / (ms / 1e3) / 1e12
+  cpu5 = None
+  if cpu_slice is not None:
+    # CPU baseline (reference fit: combine_embeddings_util.py:151-157): the
+    # Keras-semantics restatement oracle/mlpref.c (-O3 AVX2, OpenMP over
+    # output rows; the checker the device is bit-exact against) on a random
+    # slice of the same samples, one epoch of batch 256
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    threads = cpu_threads()
+    O.mlp_set_threads(threads)
+    cn, ce, cnr, cer, clab = cpu_slice
+    t = time.perf_counter()
+    O.mlp_fit(_hgx.MLP_NE_SUPERVISED, 2 * d, d, w0, cn, ce, cnr, cer, clab,
+              np.arange(clab.size)[None, :], batch=args.batch, min_delta=-1e30,
+              seed=1)
+    c_s = time.perf_counter() - t
+    restore_affinity()
+    c_sps = clab.size / c_s
+    cpu5 = {"value": round(c_sps, 1), "unit": "samples/s", "cores": threads,
+            "threads": cpu_share_note(threads), "kind": "port",
+            "gflops": round(flops / n * c_sps / 1e9, 2),
+            "sample": f"{clab.size} random samples of this leg (one epoch, "
+                      f"batch {args.batch}), oracle/mlpref.c on {threads} "
+                      f"OpenMP threads, {c_s:.1f} s",
+            "gpu_vs_cpu": round(sps / c_sps, 1)}
   return {"workload": "N_E_SUPERVISED combiner, in = 512 ([FOBE | HOBE] "
                       "d = 256), d = 256, batch 256, tables of every node "
                       f"and edge of the 10M/5M graph, {n} samples "
@@ -696,7 +765,8 @@ def bench_c5(args, ctx, big):
           "frac_of_mfma_peak": round(tf / MFMA_F32_PEAK_TFLOPS, 4),
           "c4_epoch_s_implied": round(1.2e9 / sps, 1),
           "host_prep_s": {"tables": round(tables_s, 2),
-                          "samples": round(samples_s, 2)}}
+                          "samples": round(samples_s, 2)},
+          "cpu_baseline": cpu5}
 
 
 if __name__ == "__main__":

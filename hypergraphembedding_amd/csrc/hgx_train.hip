@@ -2109,8 +2109,11 @@ extern "C" int hgx_records_copy(hgx_ctx *dst, hgx_ctx *src) {
   HGX_HIP(dst, hipStreamSynchronize(src->stream));
   const int64_t n = src->n_rec;
   const int K = src->K, R = 4 + 2 * K;
-  HGX_TRY(hgx_ensure(dst, dst->rec_idx, sizeof(int32_t) * std::max<int64_t>(n, 1) * R));
-  HGX_TRY(hgx_ensure(dst, dst->rec_tgt, sizeof(float) * std::max<int64_t>(n, 1) * 3));
+  HGX_CHECK(dst, src->n_rec_blocks >= 0 && src->n_rec_blocks <= hgx_ctx::kMaxRecBlocks,
+            HGX_EINVAL, "source has %d record blocks", src->n_rec_blocks);
+  // the same one-element slack as every other record writer
+  HGX_TRY(hgx_ensure(dst, dst->rec_idx, sizeof(int32_t) * (n * R + 1)));
+  HGX_TRY(hgx_ensure(dst, dst->rec_tgt, sizeof(float) * (n * 3 + 1)));
   if (n > 0) {
     HGX_HIP(dst, hipMemcpyAsync(dst->rec_idx.p, src->rec_idx.p,
                                 sizeof(int32_t) * n * R, hipMemcpyDeviceToDevice,

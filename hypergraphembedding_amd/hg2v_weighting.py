@@ -32,7 +32,7 @@ import scipy.sparse
 
 from . import _hgx
 from .hypergraph_util import Incidence
-from .runtime import get_context
+from .runtime import scratch_context
 
 
 def _to_csr(inc, node_major, edge_major):
@@ -53,9 +53,9 @@ def _to_csr(inc, node_major, edge_major):
 
 def _weights(hypergraph, which, alpha):
   inc = Incidence.from_hypergraph(hypergraph)
-  ctx = get_context()
-  ctx.upload(inc)
-  n, e = ctx.incidence_weights(which, alpha)
+  with scratch_context() as ctx:  # the reference functions have no side effects
+    ctx.upload(inc)
+    n, e = ctx.incidence_weights(which, alpha)
   return _to_csr(inc, n, e)
 
 
@@ -97,15 +97,16 @@ def _rows_of(side_map, ids):
   return np.array([side_map[int(i)].values for i in ids], np.float32)
 
 
-def _with_embedding(hypergraph, ref_embedding):
+def _with_embedding(hypergraph, ref_embedding, ctx):
+  """Upload the hypergraph and the embedding's rows (as the alg coordinates)
+  to the private context `ctx`; returns the compressed incidence."""
   inc = Incidence.from_hypergraph(hypergraph)
   X = _rows_of(ref_embedding.node, inc.node_ids)
   Y = _rows_of(ref_embedding.edge, inc.edge_ids)
   assert X.shape[1] == Y.shape[1] and X.shape[1] > 0
-  ctx = get_context()
   ctx.upload(inc)
   ctx.alg_set(X, Y)
-  return inc, ctx
+  return inc
 
 
 def _nonzero(m):
@@ -119,8 +120,9 @@ def WeightByDistance(hypergraph, alpha, ref_embedding, norm, disable_pbar=False)
   del disable_pbar
   assert 0 <= alpha <= 1
   kind = _norm_kind(norm)
-  inc, ctx = _with_embedding(hypergraph, ref_embedding)
-  n, e = ctx.weight_distance(kind, float(alpha))
+  with scratch_context() as ctx:
+    inc = _with_embedding(hypergraph, ref_embedding, ctx)
+    n, e = ctx.weight_distance(kind, float(alpha))
   return tuple(_nonzero(m) for m in _to_csr(inc, n, e))
 
 
@@ -142,11 +144,12 @@ def WeightBySameTypeDistance(hypergraph, alpha, ref_embedding, norm,
   del disable_pbar
   assert 0 <= alpha <= 1
   kind = _norm_kind(norm)
-  inc, ctx = _with_embedding(hypergraph, ref_embedding)
   out = []
-  for side, ids in ((0, inc.node_ids), (1, inc.edge_ids)):
-    rp, col, val = ctx.weight_same_type(side, kind, float(alpha))
-    out.append(_pattern_csr(ids, rp, col, val))
+  with scratch_context() as ctx:
+    inc = _with_embedding(hypergraph, ref_embedding, ctx)
+    for side, ids in ((0, inc.node_ids), (1, inc.edge_ids)):
+      rp, col, val = ctx.weight_same_type(side, kind, float(alpha))
+      out.append(_pattern_csr(ids, rp, col, val))
   return tuple(out)
 
 
@@ -161,18 +164,21 @@ def WeightByDistanceCluster(hypergraph, alpha, ref_embedding, norm, dim):
   return scipy.sparse.csr_matrix(W), scipy.sparse.csr_matrix(H.T)
 
 
-def _spans_on_device(hypergraph, embedding):
-  """Context holding the spans' embedding: the given one, or (as the
-  reference's default) a 5-d, 10-iteration alg-dist of the hypergraph
-  (hg2v_weighting.py:256-262) relaxed on the device."""
-  if embedding is not None:
-    assert set(hypergraph.node) == set(embedding.node)
-    assert set(hypergraph.edge) == set(embedding.edge)
-    return _with_embedding(hypergraph, embedding)
-  from .algebraic_distance import AlgebraicDistance
-  inc = Incidence.from_hypergraph(hypergraph)
-  _, _, ctx = AlgebraicDistance(inc, 5, 10)
-  return inc, ctx
+def _spans_on_device(hypergraph, embedding, alpha):
+  """(node spans, edge spans, span weights per incidence node-major and
+  edge-major) of the given embedding, or (as the reference's default) of a
+  5-d, 10-iteration alg-dist of the hypergraph (hg2v_weighting.py:256-262)
+  relaxed on the device; on a private context."""
+  with scratch_context() as ctx:
+    if embedding is not None:
+      assert set(hypergraph.node) == set(embedding.node)
+      assert set(hypergraph.edge) == set(embedding.edge)
+      inc = _with_embedding(hypergraph, embedding, ctx)
+    else:
+      from .algebraic_distance import AlgebraicDistance
+      inc = Incidence.from_hypergraph(hypergraph)
+      AlgebraicDistance(inc, 5, 10, ctx=ctx)
+    return (inc,) + ctx.weight_span(float(alpha))
 
 
 def ComputeSpans(hypergraph, embedding=None, run_in_parallel=True,
@@ -181,8 +187,7 @@ def ComputeSpans(hypergraph, embedding=None, run_in_parallel=True,
   hypergraph's ids (float32 spans, as np.subtract of the embedding's float
   fields computes them)."""
   del run_in_parallel, disable_pbar
-  inc, ctx = _spans_on_device(hypergraph, embedding)
-  sn, se, _, _ = ctx.weight_span(0.0)
+  inc, sn, se, _, _ = _spans_on_device(hypergraph, embedding, 0.0)
   return (dict(zip(inc.node_ids.tolist(), sn.tolist())),
           dict(zip(inc.edge_ids.tolist(), se.tolist())))
 
@@ -192,8 +197,7 @@ def WeightByAlgebraicSpan(hypergraph, alpha, embedding=None):
   edge2weight = A^T x the nodes'). `embedding` (not in the reference's
   signature) fixes ComputeSpans' embedding instead of its random alg-dist."""
   assert 0 <= alpha <= 1
-  inc, ctx = _spans_on_device(hypergraph, embedding)
-  _, _, n, e = ctx.weight_span(float(alpha))
+  inc, _, _, n, e = _spans_on_device(hypergraph, embedding, alpha)
   return tuple(_nonzero(m) for m in _to_csr(inc, n, e))
 
 

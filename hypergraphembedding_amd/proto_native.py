@@ -27,9 +27,9 @@ exceed the limit: the tables plus the message surface callers use (``dim``,
 ``shards()`` / ``write(path)``.
 """
 
-import glob
 import mmap
 import os
+import re
 
 import numpy as np
 
@@ -220,7 +220,22 @@ def shard_name(path, i, n):
 
 
 def _shard_files(path):
-  return glob.glob(glob.escape(str(path)) + "-[0-9]*-of-[0-9]*")
+  """Files named exactly as shard_name(path, i, n) names them (i < n, both
+  at least five digits): not `path-1-00000-of-00002`, a shard of another
+  embedding saved at `path-1`."""
+  path = str(path)
+  d, base = os.path.split(path)
+  pat = re.compile(re.escape(base) + r"-(\d{5,})-of-(\d{5,})")
+  out = []
+  try:
+    names = os.listdir(d or ".")
+  except FileNotFoundError:
+    return out
+  for name in names:
+    m = pat.fullmatch(name)
+    if m and int(m.group(1)) < int(m.group(2)):
+      out.append(os.path.join(d, name) if d else name)
+  return out
 
 
 def _clear_outputs(path):

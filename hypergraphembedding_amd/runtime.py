@@ -6,6 +6,7 @@ through one native context per device; the device is LOCAL_RANK (one process
 per GPU under torch.distributed.run) unless set explicitly.
 """
 
+import contextlib
 import os
 import threading
 
@@ -31,6 +32,18 @@ def get_context(device=None):
       ctx = _hgx.Context(dev)
       _contexts[dev] = ctx
     return ctx
+
+
+@contextlib.contextmanager
+def scratch_context(device=None):
+  """A private context for a side-effect-free call (it neither reads nor
+  replaces the incidence, coordinates or records a caller left on the
+  process-wide context), closed on exit."""
+  ctx = _hgx.Context(default_device() if device is None else int(device))
+  try:
+    yield ctx
+  finally:
+    ctx.close()
 
 
 def numpy_seed():

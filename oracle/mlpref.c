@@ -33,6 +33,7 @@
  * does not depend on the thread count.
  */
 #include <math.h>
+#include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -474,6 +475,12 @@ static double train_batch(Net *n, const Tabs *t, Bufs *b, int M, const int32_t *
   free(dJn);
   free(dJe);
   return loss;
+}
+
+/* OpenMP threads of the following calls (bench.py's CPU baseline; the
+   results do not depend on it) */
+void mlpref_set_threads(int threads) {
+  if (threads > 0) omp_set_num_threads(threads);
 }
 
 int mlpref_num_weights(int kind, int in, int out, int64_t *nw) {

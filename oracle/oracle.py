@@ -348,11 +348,17 @@ def _mlp_lib():
                              ctypes.c_float, ctypes.c_float, ctypes.c_float,
                              ctypes.c_uint64, _i64p, _i64, _f32p,
                              ctypes.POINTER(ctypes.c_int)]
+    L.mlpref_set_threads.argtypes = [_int]
     L.mlpref_predict.restype = _int
     L.mlpref_predict.argtypes = [_int, _int, _int, _f32p, _i64, _f32p, _i64,
                                  _f32p, _int, _i64, _vp, _vp, _f32p]
     _mlp = L
   return _mlp
+
+
+def mlp_set_threads(threads):
+  """OpenMP threads of mlpref.c's loops (timing only; results unchanged)."""
+  _mlp_lib().mlpref_set_threads(int(threads))
 
 
 def mlp_num_weights(kind, in_dim, out_dim):

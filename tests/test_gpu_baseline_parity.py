@@ -10,9 +10,13 @@ hgref_train; tests/test_cpu_baseline.py pins it to hgref_train), since the
 scalar hgref_train would take ~8 minutes. Bar: epoch loss rtol 1e-4, per-row
 cosine p50 >= 0.9999 and p1 >= 0.999 on both tables.
 
-The C4 window (configs[3], 10M/5M power-law, d = 256, full-size tables,
-the MULTI form on >= 40% of the batches) is in tests/test_gpu_c4.py, where
-the graph is already built.
+C2 (configs[1]): the same for one full FOBE epoch (BooleanModel: KLD loss,
+sigmoid heads, hg2v_model.py:51-125, embedding.py:308-329) at d = 128 --
+the model and instantiation bench.py's c2_fobe_d128 leg times.
+
+The C4 windows (configs[3], 10M/5M power-law, d = 256, full-size tables,
+the MULTI form on >= 40% of the batches; HOBE and the FOBE half of C5) are
+in tests/test_gpu_c4.py, where the graph is already built.
 
 Keras itself is absent from the image: the trainer stays "parity unpinned"
 against the reference; these tests pin the device against the restatement
@@ -73,6 +77,50 @@ def test_c3_full_hobe_epoch_vs_oracle():
   tgt = np.ascontiguousarray(tgt[perm])
   del perm
   ont, oet, oloss = O.train_mt(idx, tgt, K, nt, et, O.LOSS_MSE, O.ACT_RELU,
+                               epochs=1, threads=_threads(), copy=False,
+                               exact=True)
+  assert np.isclose(gl[0], oloss, rtol=1e-4), (gl, oloss)
+  for g, o, name in ((gnt, ont, "node"), (get_, oet, "edge")):
+    c = row_cos(g[1:], o[1:])
+    p50, p1 = np.percentile(c, 50), np.percentile(c, 1)
+    print(f"{name}: cosine p50 {p50:.8f} p1 {p1:.8f} min {c.min():.8f} "
+          f"max-abs {np.abs(g - o).max():.3e}")
+    assert p50 >= 0.9999 and p1 >= 0.999, (name, p50, p1)
+
+
+@pytest.mark.timeout(900)
+def test_c2_full_fobe_epoch_vs_oracle():
+  """every record of the C2 FOBE stream (~34M: nn, ee
+  and both node-edge blocks at S = 200, K = 5), d = 128, KLD + sigmoid, one
+  epoch on the device and by the checker with the same initial tables and
+  batch order."""
+  from hypergraphembedding_amd import _hgx
+  from hypergraphembedding_amd.synthetic import random_hypergraph
+  inc = random_hypergraph(seed=0)
+  K, S, d = 5, 200, 128
+  ctx = _hgx.Context(0)
+  try:
+    ctx.upload(inc)
+    n = ctx.sample_fobe(31, K, np.full(inc.N, S, np.int32),
+                        np.full(inc.E, S, np.int32))
+    assert n > 30_000_000
+    rs = np.random.RandomState(14)
+    nt = rs.uniform(-0.05, 0.05, (inc.N + 1, d)).astype(np.float32)
+    et = rs.uniform(-0.05, 0.05, (inc.E + 1, d)).astype(np.float32)
+    perm = rs.permutation(n)
+    ctx.model_init(d, inc.N + 1, inc.E + 1, node_tab=nt, edge_tab=et)
+    gl = ctx.train(batch=256, max_epochs=1, loss=_hgx.LOSS_KLD,
+                   act=_hgx.ACT_SIGMOID, perms=perm[None, :], min_delta=-1e30)
+    fused, split = ctx.train_path_stats()
+    assert split == 0 and fused == -(-n // 256)
+    gnt, get_ = ctx.model_get()
+    idx, tgt = ctx.records_get()
+  finally:
+    ctx.close()
+  idx = np.ascontiguousarray(idx[perm])
+  tgt = np.ascontiguousarray(tgt[perm])
+  del perm
+  ont, oet, oloss = O.train_mt(idx, tgt, K, nt, et, O.LOSS_KLD, O.ACT_SIGMOID,
                                epochs=1, threads=_threads(), copy=False,
                                exact=True)
   assert np.isclose(gl[0], oloss, rtol=1e-4), (gl, oloss)

@@ -89,8 +89,11 @@ def test_train_hobe_records_vs_oracle(ctx, d, batch, lanes):
   _check(o, g, init)
 
 
-@pytest.mark.parametrize("d,batch", [(16, 256), (256, 100), (2, 1)])
-def test_train_fobe_records_vs_oracle(ctx, d, batch):
+@pytest.mark.parametrize("d,batch", [(16, 256), (128, 256), (256, 100), (2, 1)])
+def test_train_fobe_records_vs_oracle(ctx, d, batch, lanes):
+  """BooleanModel (KLD + sigmoid) on the reference's FOBE stream with
+  negatives, every step geometry: d = 128 (C2's instantiation) as float4 x
+  32 lanes and float2 x 64 lanes (256- and 512-thread workgroups)."""
   z = golden("fobe_small_ns.npz")
   idx, tgt = z["idx"], z["tgt"]
   if batch == 1:  # the reference test's batch_size=1 (test_embedding.py:193)

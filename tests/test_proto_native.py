@@ -317,3 +317,32 @@ def test_overwrite_never_reads_a_stale_embedding(tmp_path):
     f.write(b"")
   with pytest.raises(FileExistsError):
     pn.read_embedding(path)
+
+
+def test_neighbouring_embedding_shards_untouched(tmp_path):
+  """shards of an embedding saved at `emb-1` are not shards of
+  `emb`: writing `emb` neither deletes them nor makes reading `emb` fail,
+  and `emb-1` still reads back whole."""
+  from hypergraphembedding_amd import proto_native as pn
+  other = str(tmp_path / "emb-1")
+  path = str(tmp_path / "emb")
+  nid, nt, eid, et = _emb_case(700, 350, 16, 5)
+  a = pn.ShardedEmbedding(nid, nt, eid, et, 16, "M", shard_bytes=28 * 1024)
+  files_other = a.write(other)
+  assert len(files_other) > 1
+  nid2, nt2, eid2, et2 = _emb_case(900, 450, 16, 6)
+  b = pn.ShardedEmbedding(nid2, nt2, eid2, et2, 16, "N", shard_bytes=28 * 1024)
+  files = b.write(path)
+  assert len(files) > 1
+  assert all(os.path.exists(f) for f in files_other)
+  assert pn.embedding_files(path) == files
+  assert pn.embedding_files(other) == files_other
+  for p, ids, tab in ((other, nid, nt), (path, nid2, nt2)):
+    back = pn.read_embedding(p)
+    o = np.argsort(ids)
+    assert np.array_equal(back.node_ids, ids[o])
+    assert np.array_equal(back.node_tab, tab[o])
+  # a one-file write of `emb` clears only its own shards
+  pn.ShardedEmbedding(nid2, nt2, eid2, et2, 16, "N").write(path)
+  assert all(os.path.exists(f) for f in files_other)
+  assert not any(os.path.exists(f) for f in files)
