@@ -549,58 +549,51 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
   eq4 = np.where(rsq.random_sample(big.E) < args.c4_frac, S4, 0).astype(np.int32)
   ctx.model_init(d4, big.N + 1, big.E + 1, seed=11 + rank)
   if world > 1:
-    # strided row chunks, each sampled over the ranks' strided shares and
-    # all-gathered in row order (hg2v_sample.sharded_chunk_fn): a replica
-    # holds one chunk's stream at a time, the form the full 5.9e9-record
-    # epoch takes (embedding.hobe_sharded)
+    # the form the full 5.9e9-record epoch takes over N ranks
+    # (embedding.hobe_sharded): the stream sampled once into every rank's
+    # record store, strided row classes sampled on the ranks' strided shares
+    # with each class's 12-byte entries all-gathered while the next class
+    # samples (hg2v_sample.sharded_store_fill), then one epoch of Keras'
+    # global shuffle from the store in chunks (Hg2vModel.fit_store)
     from hypergraphembedding_amd.embedding import _row_chunks
-    from hypergraphembedding_amd.hg2v_sample import sharded_chunk_fn
-    bound = 2 * S4
-    chunks = _row_chunks(big, bound, -(-bound * (big.N + big.E) // args.c4_chunks))
-    fn = sharded_chunk_fn(big, K4, S4, chunks, ctx=ctx, seed=4000, kind="hobe",
-                          node_quota=nq4, edge_quota=eq4,
-                          device=None if args.dist_backend == "nccl" else "cpu")
-    n4 = 0
-    hobe_sample_s = t4 = 0.0
-    ms4t = 0.0
-    rec4 = bat4 = fz4 = sp4 = 0
-    for c in range(len(chunks)):
-      sync()
-      t = time.perf_counter()
-      n4 += fn(c)
-      sync()
-      hobe_sample_s += max_over_ranks(time.perf_counter() - t)
-      t = time.perf_counter()
-      ctx.train(batch=args.batch, max_epochs=1, loss=_hgx.LOSS_MSE,
-                act=_hgx.ACT_RELU, min_delta=-1e30, shuffle_seed=2 + c)
-      sync()
-      t4 += time.perf_counter() - t
-      ms_c, rec_c, bat_c = ctx.train_stats()
-      fz_c, sp_c = ctx.train_path_stats()
-      ms4t, rec4, bat4 = ms4t + ms_c, rec4 + rec_c, bat4 + bat_c
-      fz4, sp4 = fz4 + fz_c, sp4 + sp_c
-    rej_rows, fb_rows = ctx.sample_stats()  # of the last chunk
-  else:
+    from hypergraphembedding_amd.hg2v_model import Hg2vModel
+    from hypergraphembedding_amd.hg2v_sample import sharded_store_fill
+    bn = 2 * nq4.astype(np.int64)
+    be = 2 * eq4.astype(np.int64)
+    bound = int(bn.sum() + be.sum())
+    chunk = -(-bound // args.c4_chunks)
+    chunks = _row_chunks(bn, be, chunk)
     sync()
     t = time.perf_counter()
-    n4 = ctx.sample_hobe(4000, K4, S4, node_q=nq4, edge_q=eq4)
+    n4 = sharded_store_fill(big, K4, S4, chunks, ctx=ctx, seed=4000,
+                            kind="hobe", node_quota=nq4, edge_quota=eq4,
+                            device=None if args.dist_backend == "nccl" else "cpu",
+                            capacity=bound)
     sync()
-    hobe_sample_s = time.perf_counter() - t
-    rej_rows, fb_rows = ctx.sample_stats()
+    hobe_sample_s = max_over_ranks(time.perf_counter() - t)
+    rej_rows, fb_rows = ctx.sample_stats()  # of the last class
+    model = Hg2vModel(big.N + 1, big.E + 1, d4, K4, _hgx.LOSS_MSE,
+                      _hgx.ACT_RELU, ctx=ctx, seed=11)
     sync()
     t = time.perf_counter()
-    ctx.train(batch=args.batch, max_epochs=1, loss=_hgx.LOSS_MSE,
-              act=_hgx.ACT_RELU, min_delta=-1e30, shuffle_seed=2)
+    model.fit_store(chunk, batch_size=args.batch, epochs=1, min_delta=-1e30,
+                    seed=2)
     sync()
     t4 = time.perf_counter() - t
-    ms4t, rec4, bat4 = ctx.train_stats()
-    fz4, sp4 = ctx.train_path_stats()
+    cs = model.chunk_stats
+    ms4t = sum(x[2] for x in cs)
+    rec4 = sum(x[3] for x in cs)
+    bat4 = sum(x[4] for x in cs)
+    fz4, sp4 = bat4, 0  # train_path_stats of the last chunk only
+    t4 = max_over_ranks(t4)
   hobe4 = {"workload": "HG2V_ALG_DIST (HOBE) dim=256 on the 10M/5M power-law "
                        f"graph, rows sampled: a seeded {args.c4_frac:.0%} of "
                        "node rows and edge rows (quota S=200, K=5), 1 epoch",
            "records": n4,
-           "chunks": (f"{args.c4_chunks} row-range chunks, row-sharded sampling "
-                      "+ all-gather per chunk" if world > 1 else "one stream"),
+           "chunks": (f"record store: {len(chunks)} strided row classes "
+                      "sampled row-sharded, entries all-gathered per class; "
+                      f"one global-shuffle epoch in chunks of <= {chunk} records"
+                      if world > 1 else "one resident stream"),
            "rows_sampled": int((nq4 > 0).sum() + (eq4 > 0).sum()),
            "rejection_rows": rej_rows, "expansion_fallback_rows": fb_rows,
            "uniform_column_rows": ctx.sample_uniform_rows(),
@@ -611,6 +604,16 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
            "batch_steps": {"train_step": fz4, "train_fwd_bwd+train_update": sp4},
            "multi_pending_batches": ctx.train_multi_pending(),
            "loss": "MSE", "act": "relu"}
+  # the whole pipeline of this slice on N GPUs: relaxation (20 iterations,
+  # node-row sharded at N > 1, plus the node-coordinate all-gather),
+  # sampling, one epoch; records/s of ONE embedding (the replicas train the
+  # same records, so this is not multiplied by N)
+  tte = {"alg_dist_s": round(ms4 / 1e3, 3),
+         "coord_allgather_s": exch4.get("coord_allgather_s", 0.0),
+         "sampling_s": round(hobe_sample_s, 3), "train_epoch_s": round(t4, 3)}
+  tte["total_s"] = round(sum(tte.values()), 3)
+  hobe4["time_to_embedding_s"] = tte
+  hobe4["distinct_records_per_s"] = round(n4 / t4, 1)
   if rank == 0 and world == 1 and not args.no_cpu:
     # CPU port on 1e7 records of the same stream (BASELINE.md's planned
     # slice), tables of the same size (10M+1 and 5M+1 rows x 256; only the

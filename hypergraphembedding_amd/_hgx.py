@@ -23,6 +23,8 @@ HOBE_NN, HOBE_EE, HOBE_NE = 0, 1, 2
 WEIGHT_UNIFORM, WEIGHT_NEIGHBORHOOD, WEIGHT_DISTANCE = 0, 1, 2
 NORM_L2, NORM_INF = 0, 1
 MLP_LP_CLASSIFIER, MLP_NE_SUPERVISED, MLP_NE_SEMI_SUPERVISED = 0, 1, 2
+STORE_FOBE, STORE_HOBE = 0, 1
+STORE_BINS = 16384
 
 _lib = None
 
@@ -81,6 +83,14 @@ SIGNATURES = {
     "hgx_records_blocks": (_int, [_vp, _pint, _vp]),
     "hgx_records_export": (_int, [_vp, _vp, _vp]),
     "hgx_records_import": (_int, [_vp, _i64, _int, _vp, _vp, _int, _vp]),
+    "hgx_store_reset": (_int, [_vp, _i64]),
+    "hgx_store_append": (_int, [_vp]),
+    "hgx_store_info": (_int, [_vp, _pi64, _pint, _pint,
+                              ctypes.POINTER(ctypes.c_uint64)]),
+    "hgx_store_read": (_int, [_vp, _i64, _i64, _vp, _int]),
+    "hgx_store_write": (_int, [_vp, _i64, _vp, _int, _int, _int, _u64]),
+    "hgx_store_plan": (_int, [_vp, _u64, _i64, _pint, _vp, _vp]),
+    "hgx_store_load": (_int, [_vp, _u64, _i32, _i32, _int, _int, _pi64]),
     "hgx_model_init": (_int, [_vp, _int, _i64, _i64, _u64, _vp, _vp]),
     "hgx_model_get": (_int, [_vp, _vp, _vp]),
     "hgx_model_get_rows": (_int, [_vp, _int, _i64, _vp, _vp]),
@@ -465,6 +475,63 @@ class Context:
     tgt = np.empty((n, 3), np.float32)
     self._chk(lib().hgx_records_get(self.h, _ptr(idx), _ptr(tgt)))
     return idx, tgt
+
+  # ---- compact record store (streams larger than HBM, hgx_store_*) ----
+  def store_reset(self, capacity=0):
+    self._chk(lib().hgx_store_reset(self.h, int(capacity)))
+
+  def store_append(self):
+    """Pack the records of the last sample_fobe / sample_hobe call."""
+    self._chk(lib().hgx_store_append(self.h))
+
+  def store_info(self):
+    """(records, family, K, seed) of the store."""
+    n, fam, K = ctypes.c_int64(), ctypes.c_int(), ctypes.c_int()
+    seed = ctypes.c_uint64()
+    self._chk(lib().hgx_store_info(self.h, ctypes.byref(n), ctypes.byref(fam),
+                                   ctypes.byref(K), ctypes.byref(seed)))
+    return n.value, fam.value, K.value, seed.value
+
+  def store_read(self, start=0, n=None, dst_ptr=None):
+    """Entries [start, start + n) as an (n, 3) uint32 host array, or into
+    the device buffer at dst_ptr."""
+    if n is None:
+      n = self.store_info()[0] - start
+    if dst_ptr is not None:
+      self._chk(lib().hgx_store_read(self.h, start, n, dst_ptr, 1))
+      return None
+    out = np.empty((n, 3), np.uint32)
+    self._chk(lib().hgx_store_read(self.h, start, n, _ptr(out), 0))
+    return out
+
+  def store_write(self, entries, family, K, seed, n=None, src_ptr=None):
+    """Append raw entries ((n, 3) uint32 host array, or n at device src_ptr)
+    packed by a sampler of `family` / K / seed (another rank's store)."""
+    if src_ptr is None:
+      e = _c(entries, np.uint32).reshape(-1, 3)
+      self._chk(lib().hgx_store_write(self.h, e.shape[0], _ptr(e), 0, family, K,
+                                      seed & (2**64 - 1)))
+    else:
+      self._chk(lib().hgx_store_write(self.h, int(n), src_ptr, 1, family, K,
+                                      seed & (2**64 - 1)))
+
+  def store_plan(self, epoch_seed, budget):
+    """The epoch's chunks: (bin bounds, record counts)."""
+    nc = ctypes.c_int()
+    b = np.zeros(STORE_BINS + 1, np.int32)
+    c = np.zeros(STORE_BINS + 1, np.int64)
+    self._chk(lib().hgx_store_plan(self.h, epoch_seed & (2**64 - 1), int(budget),
+                                   ctypes.byref(nc), _ptr(b), _ptr(c)))
+    return b[:nc.value + 1].copy(), c[:nc.value].copy()
+
+  def store_load(self, epoch_seed, bin_lo, bin_hi, batch, last):
+    """One chunk of the epoch as the record stream (trained in order);
+    returns the records to train."""
+    n = ctypes.c_int64()
+    self._chk(lib().hgx_store_load(self.h, epoch_seed & (2**64 - 1), int(bin_lo),
+                                   int(bin_hi), int(batch), 1 if last else 0,
+                                   ctypes.byref(n)))
+    return n.value
 
   # ---- model / trainer ----
   def model_init(self, d, node_rows, edge_rows, seed=0, node_tab=None,

@@ -81,7 +81,9 @@ extern "C" int hgx_destroy(hgx_ctx *ctx) {
                     &ctx->s3, &ctx->s4, &ctx->s5, &ctx->s6, &ctx->s7,
                     &ctx->feat_n, &ctx->feat_e, &ctx->cn_p, &ctx->cn_j,
                     &ctx->cn_v, &ctx->ce_p, &ctx->ce_j, &ctx->ce_v,
-                    &ctx->hw_n, &ctx->hw_e, &ctx->hw_self};
+                    &ctx->hw_n, &ctx->hw_e, &ctx->hw_self, &ctx->store,
+                    &ctx->st_sel, &ctx->st_keys, &ctx->st_vals, &ctx->st_tmp,
+                    &ctx->st_hist};
   for (DevBuf *b : bufs) hgx_release(*b);
   for (LongRows *l : {&ctx->long_n, &ctx->long_e, &ctx->long_sn, &ctx->long_el})
     for (DevBuf *b : {&l->seg, &l->off, &l->rows, &l->part}) hgx_release(*b);
@@ -256,6 +258,10 @@ extern "C" int hgx_upload_incidence(hgx_ctx *ctx, int32_t N, int32_t E,
   ctx->k = 0;  // alg coords belong to the previous incidence
   ctx->tpos_ok = false;
   ctx->n_rec = 0;
+  ctx->smp_family = -1;
+  ctx->rec_in_order = false;
+  ctx->n_store = 0;  // stored records name rows of the previous incidence
+  ctx->store_family = -1;
   ctx->features_ok = ctx->centroids_ok = false;
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return HGX_OK;

@@ -152,6 +152,28 @@ struct hgx_ctx {
   int64_t rec_bounds[kMaxRecBlocks + 1] = {0};
   int n_rec_blocks = 0;
 
+  // the last sampler call that wrote the records (hgx_store_append packs
+  // them): family 0 FOBE (BooleanSamples), 1 HOBE (AlgebraicDistanceSamples),
+  // -1 any other writer; its seed (every draw is keyed by it)
+  int smp_family = -1;
+  uint64_t smp_seed = 0;
+  // records written by hgx_store_load are already in their epoch order (a
+  // slice of the store's global permutation): hgx_train keeps that order
+  // instead of shuffling; every other record writer clears it
+  bool rec_in_order = false;
+
+  // ---- compact record store (hgx_store_*, streamed epochs) ----
+  // 12 B per record: {block << 28 | row, column (negatives: rank in row),
+  // target bits}; everything else of the record is re-derived on load
+  DevBuf store;
+  int64_t n_store = 0, cap_store = 0;
+  int store_family = -1, store_K = 0, store_blocks = 0;
+  uint64_t store_seed = 0;
+  // records of the last hgx_store_load past ctx->n_rec: the batch tail the
+  // next load puts first
+  int64_t store_carry = 0;
+  DevBuf st_sel, st_keys, st_vals, st_tmp, st_hist;  // hgx_store_load scratch
+
   // ---- model ----
   int d = 0, dp = 0;
   int64_t node_rows = 0, edge_rows = 0;
@@ -261,6 +283,31 @@ __host__ __device__ __forceinline__ uint64_t rand64(uint64_t seed,
 // uniform integer in [0, n) (multiply-high on 64 random bits: bias < n/2^64)
 __device__ __forceinline__ uint32_t bounded(uint64_t r, uint32_t n) {
   return (uint32_t)__umul64hi(r, (uint64_t)n);
+}
+
+// record kinds of the samplers' kind blocks (ids written per kind:
+// nn ln/rn, ee le/re, node-edge from node rows ln = row / re = column,
+// node-edge from edge rows re = row / ln = column)
+enum RecKind { REC_NN = 0, REC_EE, REC_NE_NODE, REC_NE_EDGE };
+
+// _sample_neighbors (hg2v_sample.py:49-51) of one node-edge record: K nodes
+// of its edge (col_e[nb, nb + nl)) and K edges of its node (col_n[eb,
+// eb + el)), with replacement, written +1 shifted to out[0, 2K). Every draw
+// is keyed by (seed, block stream, the record's row, `key`): key = the
+// record's column for sampled pairs (distinct within a row), its rank in
+// the row for negatives (drawn with replacement). The sampler and the
+// record store's loader (hgx_store_load) call this one function, so a
+// stored record reloads with the neighbours it was sampled with.
+__device__ __forceinline__ void draw_record_neighbors(
+    uint64_t seed, uint64_t stream, int row, uint64_t key, int K, int nb,
+    int nl, int eb, int el, const int *col_e, const int *col_n, int *out) {
+  const uint64_t rk = rand64_key(seed, (stream << 32) | (uint32_t)row);
+  for (int k = 0; k < K; k++) {
+    const uint64_t h = mix64(rk + key * 64 + k);
+    const uint64_t h2 = mix64(rk + key * 64 + 32 + k);
+    out[k] = col_e[nb + bounded(h, (uint32_t)nl)] + 1;
+    out[K + k] = col_n[eb + bounded(h2, (uint32_t)el)] + 1;
+  }
 }
 
 // Sum over aligned groups of G lanes (G a power of two <= 64); every lane of

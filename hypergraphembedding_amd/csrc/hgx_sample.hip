@@ -746,7 +746,10 @@ __global__ void ps_finish(int64_t *p, int64_t n, L3Len g) {
 }
 
 // ---- record materialisation ----------------------------------------------
-enum RecKind { REC_NN = 0, REC_EE, REC_NE_NODE, REC_NE_EDGE };
+using hgx::REC_NN;
+using hgx::REC_EE;
+using hgx::REC_NE_NODE;
+using hgx::REC_NE_EDGE;
 
 // one thread per (row, j < cnt[row]): write record rec_base + off[row] + j
 __global__ void emit_records(int kind, int nrows, const int *cnt,
@@ -797,17 +800,19 @@ __global__ void emit_negatives(int kind, int nrows, int ncols, const int *q,
 }
 
 // _sample_neighbors for the node-edge records of one kind block [b, e):
-// nn_k from N(re-1), ne_k from E(ln-1), K draws with replacement each. The
-// draws are keyed by (stream, block row, rank of the record in its row):
-// the row is id column `rowcol` of the record and its records start at
-// b + off[row]. A record therefore draws the same neighbours whichever row
-// range (fit_streaming chunk) or rank (sample_sharded) emitted it, and
-// records at equal positions of different chunks draw independently. An
-// endpoint with no neighbours (possible for negatives of a graph with an
-// isolated node or an empty edge) is an error, as np.random.choice on an
-// empty row raises ValueError in the reference (hg2v_sample.py:49-51).
+// nn_k from N(re-1), ne_k from E(ln-1), K draws with replacement each
+// (hgx::draw_record_neighbors). The draws are keyed by (stream, block row,
+// key): the row is id column `rowcol` of the record, the key its column
+// (the other id: sampled columns are distinct within a row) or, for
+// negatives (key_col 0, drawn with replacement), its rank in the row (its
+// records start at b + off[row]). A record therefore draws the same
+// neighbours whichever row range or rank emitted it, whatever its position,
+// and the record store reloads it with them (hgx_store_load). An endpoint
+// with no neighbours (possible for negatives of a graph with an isolated
+// node or an empty edge) is an error, as np.random.choice on an empty row
+// raises ValueError in the reference (hg2v_sample.py:49-51).
 __global__ void draw_neighbors(int64_t b, int64_t e, int K, int R, int *idx,
-                               const int64_t *off, int rowcol,
+                               const int64_t *off, int rowcol, int key_col,
                                const int *rp_n, const int *col_n,
                                const int *rp_e, const int *col_e,
                                uint64_t seed, uint64_t stream, int *err) {
@@ -822,14 +827,10 @@ __global__ void draw_neighbors(int64_t b, int64_t e, int K, int R, int *idx,
       continue;
     }
     const int row = ri[rowcol] - 1;
-    const uint64_t st = (stream << 32) | (uint32_t)row;
-    const uint64_t j = (uint64_t)(rec - b - off[row]);
-    for (int k = 0; k < K; k++) {
-      const uint64_t h = hgx::rand64(seed, st, j * 64 + k);
-      const uint64_t h2 = hgx::rand64(seed, st, j * 64 + 32 + k);
-      ri[4 + k] = col_e[nb + hgx::bounded(h, (uint32_t)nl)] + 1;
-      ri[4 + K + k] = col_n[eb + hgx::bounded(h2, (uint32_t)el)] + 1;
-    }
+    const uint64_t key = key_col ? (uint64_t)(rowcol == 0 ? ed : v)
+                                 : (uint64_t)(rec - b - off[row]);
+    hgx::draw_record_neighbors(seed, stream, row, key, K, nb, nl, eb, el, col_e,
+                               col_n, ri + 4);
   }
 }
 
@@ -1076,6 +1077,8 @@ int alloc_records(hgx_ctx *ctx, int64_t n, int K) {
   HGX_TRY(hgx_ensure(ctx, ctx->rec_tgt, sizeof(float) * (n * 3 + 1)));
   ctx->n_rec = n;
   ctx->K = K;
+  ctx->rec_in_order = false;
+  ctx->smp_family = -1;  // set by the sampler once its records are complete
   return HGX_OK;
 }
 
@@ -1094,14 +1097,14 @@ int emit(hgx_ctx *ctx, int kind, const PatOut &po, int64_t base, float prob) {
 // record = id column rowcol (0: node rows, 3: edge rows), row r's records at
 // b + off[r] (the block's exclusive record scan)
 int neighbors(hgx_ctx *ctx, int64_t b, int64_t n, const DevBuf &off,
-              int rowcol, uint64_t seed, uint64_t stream) {
+              int rowcol, uint64_t seed, uint64_t stream, int key_col) {
   if (n <= 0) return HGX_OK;
   const int64_t e = b + n;
   HGX_TRY(hgx_ensure(ctx, ctx->s1, 16));
   HGX_HIP(ctx, hipMemsetAsync(ctx->s1.p, 0, sizeof(int), ctx->stream));
   hipLaunchKernelGGL(draw_neighbors, dim3(grid_for(e - b, 256)), dim3(256), 0,
                      ctx->stream, b, e, ctx->K, 4 + 2 * ctx->K,
-                     ctx->rec_idx.as<int>(), off.as<int64_t>(), rowcol,
+                     ctx->rec_idx.as<int>(), off.as<int64_t>(), rowcol, key_col,
                      ctx->rp_n.as<int>(), ctx->col_n.as<int>(),
                      ctx->rp_e.as<int>(), ctx->col_e.as<int>(), seed, stream,
                      ctx->s1.as<int>());
@@ -1216,8 +1219,8 @@ extern "C" int hgx_sample_fobe(hgx_ctx *ctx, uint64_t seed, int K,
   HGX_TRY(emit(ctx, REC_EE, ee, o_ee, 1.f));
   HGX_TRY(emit(ctx, REC_NE_NODE, ne_n, o_ne, 1.f));
   HGX_TRY(emit(ctx, REC_NE_EDGE, ne_e, o_en, 1.f));
-  HGX_TRY(neighbors(ctx, o_ne, ne_n.total, ne_n.rec_off, 0, seed, 0x200));
-  HGX_TRY(neighbors(ctx, o_en, ne_e.total, ne_e.rec_off, 3, seed, 0x201));
+  HGX_TRY(neighbors(ctx, o_ne, ne_n.total, ne_n.rec_off, 0, seed, 0x200, 1));
+  HGX_TRY(neighbors(ctx, o_en, ne_e.total, ne_e.rec_off, 3, seed, 0x201, 1));
   if (neg_node_quota) {
     HGX_TRY(neg_emit(ctx, REC_NN, gnn, ctx->N, o_neg, seed, 0x300));
     HGX_TRY(neg_emit(ctx, REC_EE, gee, ctx->E, o_gee, seed, 0x301));
@@ -1226,13 +1229,15 @@ extern "C" int hgx_sample_fobe(hgx_ctx *ctx, uint64_t seed, int K,
     HGX_TRY(neg_emit(ctx, REC_EE, gee, ctx->E, o_gee2, seed, 0x302));
     HGX_TRY(neg_emit(ctx, REC_NE_NODE, gne_n, ctx->E, o_gne, seed, 0x303));
     HGX_TRY(neg_emit(ctx, REC_NE_EDGE, gne_e, ctx->N, o_gen, seed, 0x304));
-    HGX_TRY(neighbors(ctx, o_gne, gne_n.total, gne_n.off, 0, seed, 0x400));
-    HGX_TRY(neighbors(ctx, o_gen, gne_e.total, gne_e.off, 3, seed, 0x401));
+    HGX_TRY(neighbors(ctx, o_gne, gne_n.total, gne_n.off, 0, seed, 0x400, 0));
+    HGX_TRY(neighbors(ctx, o_gen, gne_e.total, gne_e.off, 3, seed, 0x401, 0));
     set_blocks(ctx, {0, o_ee, o_ne, o_en, o_neg, o_gee, o_gee2, o_gne, o_gen, total});
   } else {
     set_blocks(ctx, {0, o_ee, o_ne, o_en, total});
   }
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->smp_family = 0;
+  ctx->smp_seed = seed;
   if (n_records) *n_records = total;
   return HGX_OK;
 }
@@ -1268,14 +1273,16 @@ extern "C" int hgx_sample_hobe_rows(hgx_ctx *ctx, uint64_t seed, int K,
   HGX_TRY(emit(ctx, REC_EE, ee, o_ee, 0.f));
   HGX_TRY(emit(ctx, REC_NE_NODE, ne_n, o_ne, 0.f));
   HGX_TRY(emit(ctx, REC_NE_EDGE, ne_e, o_en, 0.f));
-  HGX_TRY(neighbors(ctx, o_ne, ne_n.total, ne_n.rec_off, 0, seed, 0x500));
-  HGX_TRY(neighbors(ctx, o_en, ne_e.total, ne_e.rec_off, 3, seed, 0x501));
+  HGX_TRY(neighbors(ctx, o_ne, ne_n.total, ne_n.rec_off, 0, seed, 0x500, 1));
+  HGX_TRY(neighbors(ctx, o_en, ne_e.total, ne_e.rec_off, 3, seed, 0x501, 1));
   HGX_TRY(hgx_hobe_prepare(ctx));
   HGX_TRY(hgx_hobe_fill_probs(ctx, 0, 0, o_ee));
   HGX_TRY(hgx_hobe_fill_probs(ctx, 1, o_ee, o_ne));
   HGX_TRY(hgx_hobe_fill_probs(ctx, 2, o_ne, total));
   set_blocks(ctx, {0, o_ee, o_ne, o_en, total});
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->smp_family = 1;
+  ctx->smp_seed = seed;
   if (n_records) *n_records = total;
   return HGX_OK;
 }
@@ -1307,8 +1314,8 @@ int hgx_sample_pairs4(hgx_ctx *ctx, uint64_t seed, int K, const int32_t *node_q,
   HGX_TRY(emit(ctx, REC_EE, ee, o_ee, 0.f));
   HGX_TRY(emit(ctx, REC_NE_NODE, ne_n, o_ne, 0.f));
   HGX_TRY(emit(ctx, REC_NE_EDGE, ne_e, o_en, 0.f));
-  HGX_TRY(neighbors(ctx, o_ne, ne_n.total, ne_n.rec_off, 0, seed, 0x600));
-  HGX_TRY(neighbors(ctx, o_en, ne_e.total, ne_e.rec_off, 3, seed, 0x601));
+  HGX_TRY(neighbors(ctx, o_ne, ne_n.total, ne_n.rec_off, 0, seed, 0x600, 1));
+  HGX_TRY(neighbors(ctx, o_en, ne_e.total, ne_e.rec_off, 3, seed, 0x601, 1));
   set_blocks(ctx, {0, o_ee, o_ne, o_en, total});
   *o_ee_out = o_ee;
   *o_ne_out = o_ne;

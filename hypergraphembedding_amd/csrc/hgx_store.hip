@@ -1,0 +1,621 @@
+// Compact record store: record streams larger than HBM trained with Keras'
+// global shuffle. See include/hgx.h (hgx_store_*).
+//
+// The reference materialises every SimilarityRecord once and calls
+// model.fit(..., shuffle=True): every epoch is a fresh uniform permutation
+// of the WHOLE stream cut into batches of 256 (embedding.py:277-302). At
+// the 10M/5M config the stream is 5.9e9 records, 404 GB in the trainer's
+// 68-byte layout (SamplesToModelInput, hg2v_sample.py:751-797). Here every
+// record is sampled once and kept as 12 bytes:
+//   w0 = kind block << 28 | row      (the row it was sampled from)
+//   w1 = column (negatives: rank of the record in its row)
+//   w2 = target bits (negatives: 0)
+// -- everything else of the record is a function of these (the neighbour
+// lists are keyed draws, hgx::draw_record_neighbors; a negative's column
+// is the keyed draw of emit_negatives), so hgx_store_load rebuilds the
+// sampler's records bit for bit. Packing verifies exactly that.
+//
+// Epoch order: record r's key is a bijective 64-bit mix of its identity
+// (w0, w1) and the epoch seed, so keys are distinct and the order "sorted
+// by key" is a pseudo-random permutation of the stream that does not
+// depend on where a record sits in the store (one rank or eight ranks
+// filling it, any append order: the same epoch). hgx_store_plan cuts the
+// key space into chunks of at most `budget` records by a 2^14-bin
+// histogram; hgx_store_load selects a chunk's records, sorts them by key
+// and writes them as trainer records in that order, so consecutive loads
+// walk the epoch's global order. Batches follow the global order too: a
+// load keeps the (n mod batch) records of its tail for the next load, so
+// every batch but the epoch's last holds exactly `batch` records, as
+// Keras cuts them.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "hgx_internal.h"
+
+namespace {
+
+using hgx::REC_EE;
+using hgx::REC_NE_EDGE;
+using hgx::REC_NE_NODE;
+using hgx::REC_NN;
+
+constexpr int kMaxBlocks = 9;
+constexpr int kRowBits = 28;
+constexpr uint32_t kRowMask = (1u << kRowBits) - 1;
+constexpr int kBinBits = 14;
+constexpr int kBins = 1 << kBinBits;  // == HGX_STORE_BINS
+static_assert(kBins == HGX_STORE_BINS, "bin count");
+
+// What a stored record's block index means (the sampler's kind blocks)
+struct BlockTab {
+  int nb;
+  int kind[kMaxBlocks];
+  int neg[kMaxBlocks];
+  int ncols[kMaxBlocks];            // negatives: columns of the draw
+  uint32_t col_stream[kMaxBlocks];  // negatives: emit_negatives stream
+  uint32_t nbr_stream[kMaxBlocks];  // node-edge blocks: draw_neighbors stream
+  int64_t bound[kMaxBlocks + 1];    // hgx_store_append: record block bounds
+};
+
+// the samplers' block layouts (hgx_sample.hip: hgx_sample_fobe,
+// hgx_sample_hobe_rows; streams as they pass them)
+void block_table(const hgx_ctx *ctx, int family, BlockTab &t) {
+  memset(&t, 0, sizeof(t));
+  auto set = [&](int b, int kind, int neg, int ncols, uint32_t cs, uint32_t ns) {
+    t.kind[b] = kind;
+    t.neg[b] = neg;
+    t.ncols[b] = ncols;
+    t.col_stream[b] = cs;
+    t.nbr_stream[b] = ns;
+  };
+  if (family == 0) {  // BooleanSamples (hg2v_sample.py:156-240)
+    t.nb = 9;
+    set(0, REC_NN, 0, 0, 0, 0);
+    set(1, REC_EE, 0, 0, 0, 0);
+    set(2, REC_NE_NODE, 0, 0, 0, 0x200);
+    set(3, REC_NE_EDGE, 0, 0, 0, 0x201);
+    set(4, REC_NN, 1, ctx->N, 0x300, 0);
+    set(5, REC_EE, 1, ctx->E, 0x301, 0);
+    set(6, REC_EE, 1, ctx->E, 0x302, 0);
+    set(7, REC_NE_NODE, 1, ctx->E, 0x303, 0x400);
+    set(8, REC_NE_EDGE, 1, ctx->N, 0x304, 0x401);
+  } else {  // AlgebraicDistanceSamples (hg2v_sample.py:658-715)
+    t.nb = 4;
+    set(0, REC_NN, 0, 0, 0, 0);
+    set(1, REC_EE, 0, 0, 0, 0);
+    set(2, REC_NE_NODE, 0, 0, 0, 0x500);
+    set(3, REC_NE_EDGE, 0, 0, 0, 0x501);
+  }
+}
+
+struct Csr4 {
+  const int *rp_n, *col_n, *rp_e, *col_e;
+};
+
+// (row, column) of record ri of kind `kind`, from its +1 shifted ids
+__device__ __forceinline__ void row_col(const int *ri, int kind, int &row, int &col) {
+  switch (kind) {
+    case REC_NN: row = ri[0] - 1; col = ri[2] - 1; break;
+    case REC_EE: row = ri[1] - 1; col = ri[3] - 1; break;
+    case REC_NE_NODE: row = ri[0] - 1; col = ri[3] - 1; break;
+    default: row = ri[3] - 1; col = ri[0] - 1; break;
+  }
+}
+
+// The trainer record of stored entry (w0, w1, w2): ids (+1 shifted, 0 =
+// absent) into ri[0, 4 + 2K), targets into tg[0, 3). Returns false if a
+// node-edge endpoint has no neighbours (the sampler refuses those).
+__device__ __forceinline__ bool expand_one(uint32_t w0, uint32_t w1, uint32_t w2,
+                                           const BlockTab &t, int K, uint64_t seed,
+                                           const Csr4 &g, int *ri, float *tg) {
+  const int b = (int)(w0 >> kRowBits);
+  const int row = (int)(w0 & kRowMask);
+  const int kind = t.kind[b];
+  int col;
+  if (t.neg[b]) {  // emit_negatives' column: keyed by (row, rank in row)
+    col = (int)hgx::bounded(
+        hgx::rand64(seed, t.col_stream[b], ((uint64_t)row << 32) | w1),
+        (uint32_t)t.ncols[b]);
+  } else {
+    col = (int)w1;
+  }
+  for (int s = 0; s < 4 + 2 * K; s++) ri[s] = 0;
+  tg[0] = tg[1] = tg[2] = 0.f;
+  const float p = __uint_as_float(w2);
+  if (kind == REC_NN) {
+    ri[0] = row + 1;
+    ri[2] = col + 1;
+    tg[0] = p;
+    return true;
+  }
+  if (kind == REC_EE) {
+    ri[1] = row + 1;
+    ri[3] = col + 1;
+    tg[1] = p;
+    return true;
+  }
+  const int v = kind == REC_NE_NODE ? row : col;
+  const int e = kind == REC_NE_NODE ? col : row;
+  ri[0] = v + 1;
+  ri[3] = e + 1;
+  tg[2] = p;
+  const int nb = g.rp_e[e], nl = g.rp_e[e + 1] - nb;
+  const int eb = g.rp_n[v], el = g.rp_n[v + 1] - eb;
+  if (nl == 0 || el == 0) return false;
+  hgx::draw_record_neighbors(seed, t.nbr_stream[b], row,
+                             t.neg[b] ? (uint64_t)w1 : (uint64_t)col, K, nb, nl,
+                             eb, el, g.col_e, g.col_n, ri + 4);
+  return true;
+}
+
+// Pack records [0, n) of the sampler's stream (kind blocks t.bound) into
+// out[3 * (base + i)], checking that each reloads bit for bit. err bits:
+// 1 a record does not reload as sampled, 2 a row id past 2^28.
+__global__ void store_pack(const int *idx, const float *tgt, int64_t n, int K,
+                           BlockTab t, Csr4 g, uint64_t seed, uint32_t *out,
+                           int *err) {
+  const int R = 4 + 2 * K;
+  int ri2[36];
+  float tg2[3];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int b = 0;
+    while (b + 1 < t.nb && i >= t.bound[b + 1]) b++;
+    const int *ri = idx + i * R;
+    const int kind = t.kind[b];
+    int row, col;
+    row_col(ri, kind, row, col);
+    const float p = tgt[i * 3 + (kind == REC_NN ? 0 : kind == REC_EE ? 1 : 2)];
+    int bad = row < 0 || (uint32_t)row > kRowMask ? 2 : 0;
+    uint32_t w1 = (uint32_t)col;
+    if (t.neg[b] && !bad) {
+      // rank in the row: a block's records are grouped by row, rows
+      // ascending (galloping back to the row's first record, then bisection)
+      const int64_t b0 = t.bound[b];
+      int64_t good = i, step = 1, lo = b0 - 1;
+      while (good - step >= b0) {
+        int r2, c2;
+        row_col(idx + (good - step) * R, kind, r2, c2);
+        if (r2 != row) {
+          lo = good - step;
+          break;
+        }
+        good -= step;
+        step <<= 1;
+      }
+      while (good - lo > 1) {
+        const int64_t mid = lo + (good - lo) / 2;
+        int r2, c2;
+        row_col(idx + mid * R, kind, r2, c2);
+        if (r2 == row) good = mid;
+        else lo = mid;
+      }
+      w1 = (uint32_t)(i - good);
+    }
+    const uint32_t w0 = ((uint32_t)b << kRowBits) | ((uint32_t)row & kRowMask);
+    const uint32_t w2 = __float_as_uint(p);
+    if (!bad) {
+      const bool ok = expand_one(w0, w1, w2, t, K, seed, g, ri2, tg2);
+      bool same = ok;
+      for (int s = 0; s < R; s++) same = same && ri2[s] == ri[s];
+      for (int s = 0; s < 3; s++)
+        same = same && __float_as_uint(tg2[s]) == __float_as_uint(tgt[i * 3 + s]);
+      if (!same) bad = 1;
+    }
+    uint32_t *o = out + 3 * i;
+    o[0] = w0;
+    o[1] = w1;
+    o[2] = w2;
+    if (bad) atomicOr(err, bad);
+  }
+}
+
+// epoch key of a stored record: bijective in its identity (w0, w1)
+__device__ __forceinline__ uint64_t epoch_key(uint32_t w0, uint32_t w1, uint64_t k1,
+                                              uint64_t k2) {
+  const uint64_t id = ((uint64_t)w0 << 32) | w1;
+  return hgx::mix64(hgx::mix64(id ^ k1) ^ k2);
+}
+
+__global__ void store_hist(const uint32_t *st, int64_t n, uint64_t k1, uint64_t k2,
+                           unsigned *hist) {
+  __shared__ unsigned h[kBins];
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = epoch_key(st[3 * i], st[3 * i + 1], k1, k2);
+    atomicAdd(&h[key >> (64 - kBinBits)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// Records whose key lies in bins [lo, hi): copied to sel (their keys to
+// keys, their positions in sel to vals); one atomic per wave.
+__global__ void store_select(const uint32_t *st, int64_t n, uint64_t k1, uint64_t k2,
+                             uint32_t lo, uint32_t hi, uint32_t *sel,
+                             unsigned long long *keys, int *vals,
+                             unsigned long long *count) {
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n_up = (n + 63) / 64 * 64;  // every lane of a wave iterates alike
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_up;
+       i += stride) {
+    uint32_t w0 = 0, w1 = 0, w2 = 0;
+    uint64_t key = 0;
+    bool take = false;
+    if (i < n) {
+      w0 = st[3 * i];
+      w1 = st[3 * i + 1];
+      w2 = st[3 * i + 2];
+      key = epoch_key(w0, w1, k1, k2);
+      const uint32_t bin = (uint32_t)(key >> (64 - kBinBits));
+      take = bin >= lo && bin < hi;
+    }
+    const unsigned long long mask = __ballot(take);
+    if (!mask) continue;
+    unsigned long long base = 0;
+    const int leader = __ffsll((long long)mask) - 1;
+    if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(mask));
+    base = __shfl(base, leader);
+    if (take) {
+      const int64_t pos = (int64_t)base + __popcll(mask & ((1ull << lane) - 1));
+      uint32_t *o = sel + 3 * pos;
+      o[0] = w0;
+      o[1] = w1;
+      o[2] = w2;
+      keys[pos] = key;
+      vals[pos] = (int)pos;
+    }
+  }
+}
+
+// trainer records [off, off + m) from the selected entries in key order
+__global__ void store_expand(const uint32_t *sel, const int *order, int64_t m,
+                             int64_t off, BlockTab t, int K, uint64_t seed, Csr4 g,
+                             int *idx, float *tgt, int *err) {
+  const int R = 4 + 2 * K;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t *c = sel + 3 * (int64_t)order[i];
+    if (!expand_one(c[0], c[1], c[2], t, K, seed, g, idx + (off + i) * R,
+                    tgt + (off + i) * 3))
+      atomicOr(err, 1);
+  }
+}
+
+int grid_for(int64_t work, int per_block, int cap = 8192) {
+  int64_t gr = (work + per_block - 1) / per_block;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(gr, cap));
+}
+
+Csr4 csr_of(const hgx_ctx *ctx) {
+  return Csr4{ctx->rp_n.as<int>(), ctx->col_n.as<int>(), ctx->rp_e.as<int>(),
+              ctx->col_e.as<int>()};
+}
+
+// the store's capacity grown to `cap` records, keeping its contents
+int store_grow(hgx_ctx *ctx, int64_t cap) {
+  if (cap <= ctx->cap_store && ctx->store.p) return HGX_OK;
+  DevBuf nb;
+  HGX_TRY(hgx_ensure(ctx, nb, sizeof(uint32_t) * 3 * (size_t)std::max<int64_t>(cap, 1)));
+  if (ctx->n_store > 0)
+    HGX_HIP(ctx, hipMemcpyAsync(nb.p, ctx->store.p, sizeof(uint32_t) * 3 * ctx->n_store,
+                                hipMemcpyDeviceToDevice, ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  hgx_release(ctx->store);
+  ctx->store = nb;
+  ctx->cap_store = cap;
+  return HGX_OK;
+}
+
+void epoch_keys(uint64_t epoch_seed, uint64_t &k1, uint64_t &k2) {
+  k1 = hgx::mix64(epoch_seed ^ 0x53544f52454b3130ull);
+  k2 = hgx::mix64(epoch_seed ^ 0x53544f52454b3230ull);
+}
+
+}  // namespace
+
+extern "C" int hgx_store_reset(hgx_ctx *ctx, int64_t capacity) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, capacity >= 0, HGX_EINVAL, "negative store capacity");
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  ctx->n_store = 0;
+  ctx->store_family = -1;
+  ctx->store_K = 0;
+  ctx->store_seed = 0;
+  ctx->store_carry = 0;
+  if (capacity > ctx->cap_store) {
+    hgx_release(ctx->store);  // nothing to keep
+    ctx->cap_store = 0;
+    HGX_TRY(store_grow(ctx, capacity));
+  }
+  return HGX_OK;
+}
+
+// the store's sampler family / K / seed: set by the first records, equal
+// for every later one
+static int store_adopt(hgx_ctx *ctx, int family, int K, uint64_t seed) {
+  if (ctx->n_store == 0) {
+    ctx->store_family = family;
+    ctx->store_K = K;
+    ctx->store_seed = seed;
+    BlockTab t;
+    block_table(ctx, family, t);
+    ctx->store_blocks = t.nb;
+    return HGX_OK;
+  }
+  HGX_CHECK(ctx, ctx->store_family == family && ctx->store_K == K &&
+                     ctx->store_seed == seed,
+            HGX_EINVAL,
+            "records of sampler family %d / K %d / seed %llu do not join a store "
+            "of family %d / K %d / seed %llu",
+            family, K, (unsigned long long)seed, ctx->store_family, ctx->store_K,
+            (unsigned long long)ctx->store_seed);
+  return HGX_OK;
+}
+
+extern "C" int hgx_store_append(hgx_ctx *ctx) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->smp_family == 0 || ctx->smp_family == 1, HGX_ESTATE,
+            "the records are not a hgx_sample_fobe / hgx_sample_hobe stream");
+  HGX_CHECK(ctx, ctx->N <= (int32_t)kRowMask && ctx->E <= (int32_t)kRowMask,
+            HGX_EUNSUP, "the record store holds graphs of < 2^28 nodes and edges");
+  const int family = ctx->smp_family, K = ctx->K;
+  BlockTab t;
+  block_table(ctx, family, t);
+  const int nb = ctx->n_rec_blocks;
+  HGX_CHECK(ctx, (family == 1 && nb == 4) || (family == 0 && (nb == 4 || nb == 9)),
+            HGX_ESTATE, "unexpected kind blocks (%d) for sampler family %d", nb,
+            family);
+  HGX_TRY(store_adopt(ctx, family, K, ctx->smp_seed));
+  const int64_t n = ctx->n_rec;
+  if (n == 0) return HGX_OK;
+  for (int i = 0; i <= kMaxBlocks; i++)
+    t.bound[i] = ctx->rec_bounds[std::min(i, nb)];
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  if (ctx->n_store + n > ctx->cap_store)
+    HGX_TRY(store_grow(ctx, std::max(ctx->n_store + n, ctx->cap_store + ctx->cap_store / 4)));
+  HGX_TRY(hgx_ensure(ctx, ctx->s0, 16));
+  HGX_HIP(ctx, hipMemsetAsync(ctx->s0.p, 0, sizeof(int), ctx->stream));
+  hipLaunchKernelGGL(store_pack, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream,
+                     ctx->rec_idx.as<int>(), ctx->rec_tgt.as<float>(), n, K, t,
+                     csr_of(ctx), ctx->store_seed,
+                     ctx->store.as<uint32_t>() + 3 * ctx->n_store, ctx->s0.as<int>());
+  HGX_LAUNCH_CHECK(ctx);
+  int err = 0;
+  HGX_HIP(ctx, hipMemcpyAsync(&err, ctx->s0.p, sizeof(int), hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  HGX_CHECK(ctx, !(err & 2), HGX_EUNSUP, "a record row id exceeds 2^28");
+  HGX_CHECK(ctx, err == 0, HGX_ESTATE,
+            "a sampled record does not reload bit for bit from its stored form");
+  ctx->n_store += n;
+  return HGX_OK;
+}
+
+extern "C" int hgx_store_info(hgx_ctx *ctx, int64_t *n, int *family, int *K,
+                              uint64_t *seed) {
+  if (!ctx) return HGX_EINVAL;
+  if (n) *n = ctx->n_store;
+  if (family) *family = ctx->store_family;
+  if (K) *K = ctx->store_K;
+  if (seed) *seed = ctx->store_seed;
+  return HGX_OK;
+}
+
+extern "C" int hgx_store_read(hgx_ctx *ctx, int64_t start, int64_t n, void *dst,
+                              int dst_device) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, start >= 0 && n >= 0 && start + n <= ctx->n_store, HGX_EINVAL,
+            "store range [%lld, %lld) outside [0, %lld)", (long long)start,
+            (long long)(start + n), (long long)ctx->n_store);
+  HGX_CHECK(ctx, n == 0 || dst, HGX_EINVAL, "null destination");
+  if (n == 0) return HGX_OK;
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  HGX_HIP(ctx, hipMemcpyAsync(dst, ctx->store.as<uint32_t>() + 3 * start,
+                              sizeof(uint32_t) * 3 * n,
+                              dst_device ? hipMemcpyDeviceToDevice
+                                         : hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HGX_OK;
+}
+
+extern "C" int hgx_store_write(hgx_ctx *ctx, int64_t n, const void *src,
+                               int src_device, int family, int K, uint64_t seed) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, family == 0 || family == 1, HGX_EINVAL, "family must be 0 or 1");
+  HGX_CHECK(ctx, K >= 1 && K <= 16, HGX_EUNSUP, "num_neighbors %d outside [1,16]", K);
+  HGX_CHECK(ctx, n >= 0 && (n == 0 || src), HGX_EINVAL, "bad source");
+  HGX_CHECK(ctx, ctx->N > 0, HGX_ESTATE, "no incidence uploaded");
+  HGX_TRY(store_adopt(ctx, family, K, seed));
+  if (n == 0) return HGX_OK;
+  if (!src_device) {  // host records: validate before they reach the device
+    const uint32_t *h = static_cast<const uint32_t *>(src);
+    BlockTab t;
+    block_table(ctx, family, t);
+    for (int64_t i = 0; i < n; i++) {
+      const int b = (int)(h[3 * i] >> kRowBits);
+      const int64_t row = h[3 * i] & kRowMask;
+      HGX_CHECK(ctx, b < t.nb, HGX_EINVAL, "record %lld: block %d", (long long)i, b);
+      const bool node_row = t.kind[b] == REC_NN || t.kind[b] == REC_NE_NODE;
+      HGX_CHECK(ctx, row < (node_row ? ctx->N : ctx->E), HGX_EINVAL,
+                "record %lld: row %lld out of range", (long long)i, (long long)row);
+      if (!t.neg[b]) {
+        const bool node_col = t.kind[b] == REC_NN || t.kind[b] == REC_NE_EDGE;
+        HGX_CHECK(ctx, h[3 * i + 1] < (uint32_t)(node_col ? ctx->N : ctx->E),
+                  HGX_EINVAL, "record %lld: column out of range", (long long)i);
+      }
+    }
+  }
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  if (ctx->n_store + n > ctx->cap_store)
+    HGX_TRY(store_grow(ctx, std::max(ctx->n_store + n, ctx->cap_store + ctx->cap_store / 4)));
+  HGX_HIP(ctx, hipMemcpyAsync(ctx->store.as<uint32_t>() + 3 * ctx->n_store, src,
+                              sizeof(uint32_t) * 3 * n,
+                              src_device ? hipMemcpyDeviceToDevice
+                                         : hipMemcpyHostToDevice,
+                              ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->n_store += n;
+  return HGX_OK;
+}
+
+extern "C" int hgx_store_plan(hgx_ctx *ctx, uint64_t epoch_seed, int64_t budget,
+                              int *n_chunks, int32_t *bin_bounds, int64_t *counts) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, budget >= 1, HGX_EINVAL, "budget must be >= 1");
+  HGX_CHECK(ctx, n_chunks && bin_bounds && counts, HGX_EINVAL, "null output");
+  HGX_CHECK(ctx, ctx->n_store > 0, HGX_ESTATE, "the record store is empty");
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  uint64_t k1, k2;
+  epoch_keys(epoch_seed, k1, k2);
+  HGX_TRY(hgx_ensure(ctx, ctx->st_hist, sizeof(unsigned) * kBins));
+  HGX_HIP(ctx, hipMemsetAsync(ctx->st_hist.p, 0, sizeof(unsigned) * kBins, ctx->stream));
+  hipLaunchKernelGGL(store_hist, dim3(grid_for(ctx->n_store, 1024, 1024)), dim3(1024),
+                     0, ctx->stream, ctx->store.as<uint32_t>(), ctx->n_store, k1, k2,
+                     ctx->st_hist.as<unsigned>());
+  HGX_LAUNCH_CHECK(ctx);
+  std::vector<unsigned> h(kBins);
+  HGX_HIP(ctx, hipMemcpyAsync(h.data(), ctx->st_hist.p, sizeof(unsigned) * kBins,
+                              hipMemcpyDeviceToHost, ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // greedy: consecutive bins while the chunk stays within budget (a bin
+  // larger than the budget is a chunk of its own)
+  int nc = 0;
+  bin_bounds[0] = 0;
+  int64_t cur = 0;
+  for (int b = 0; b < kBins; b++) {
+    if (cur > 0 && cur + (int64_t)h[b] > budget) {
+      counts[nc] = cur;
+      bin_bounds[++nc] = b;
+      cur = 0;
+    }
+    cur += h[b];
+  }
+  counts[nc] = cur;
+  bin_bounds[++nc] = kBins;
+  int64_t tot = 0;
+  for (int c = 0; c < nc; c++) tot += counts[c];
+  HGX_CHECK(ctx, tot == ctx->n_store, HGX_EHIP, "store histogram lost records");
+  *n_chunks = nc;
+  ctx->store_carry = 0;  // a new epoch: no batch tail carried over
+  return HGX_OK;
+}
+
+extern "C" int hgx_store_load(hgx_ctx *ctx, uint64_t epoch_seed, int32_t bin_lo,
+                              int32_t bin_hi, int batch, int last,
+                              int64_t *n_records) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, 0 <= bin_lo && bin_lo < bin_hi && bin_hi <= kBins, HGX_EINVAL,
+            "bins [%d, %d) outside [0, %d)", bin_lo, bin_hi, kBins);
+  HGX_CHECK(ctx, batch >= 1, HGX_EINVAL, "batch must be >= 1");
+  HGX_CHECK(ctx, ctx->n_store > 0, HGX_ESTATE, "the record store is empty");
+  HGX_CHECK(ctx, ctx->N > 0, HGX_ESTATE, "no incidence uploaded");
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  const int K = ctx->store_K, R = 4 + 2 * K;
+  BlockTab t;
+  block_table(ctx, ctx->store_family, t);
+  uint64_t k1, k2;
+  epoch_keys(epoch_seed, k1, k2);
+  // 1. the chunk's entries and their keys
+  HGX_TRY(hgx_ensure(ctx, ctx->s0, 16));
+  HGX_HIP(ctx, hipMemsetAsync(ctx->s0.p, 0, 16, ctx->stream));
+  // selection capacity: at most the store (sized from a first count pass
+  // would cost a second read of the store; the histogram gives it)
+  HGX_TRY(hgx_ensure(ctx, ctx->st_hist, sizeof(unsigned) * kBins));
+  HGX_HIP(ctx, hipMemsetAsync(ctx->st_hist.p, 0, sizeof(unsigned) * kBins, ctx->stream));
+  hipLaunchKernelGGL(store_hist, dim3(grid_for(ctx->n_store, 1024, 1024)), dim3(1024),
+                     0, ctx->stream, ctx->store.as<uint32_t>(), ctx->n_store, k1, k2,
+                     ctx->st_hist.as<unsigned>());
+  HGX_LAUNCH_CHECK(ctx);
+  std::vector<unsigned> h(kBins);
+  HGX_HIP(ctx, hipMemcpyAsync(h.data(), ctx->st_hist.p, sizeof(unsigned) * kBins,
+                              hipMemcpyDeviceToHost, ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  int64_t m = 0;
+  for (int b = bin_lo; b < bin_hi; b++) m += h[b];
+  const int64_t carry = ctx->store_carry;
+  HGX_CHECK(ctx, carry + m < (int64_t)INT32_MAX, HGX_EUNSUP,
+            "%lld records in one load exceed the trainer's 2^31 limit",
+            (long long)(carry + m));
+  HGX_TRY(hgx_ensure(ctx, ctx->st_sel, sizeof(uint32_t) * 3 * (size_t)(m + 1)));
+  size_t sort_tmp = 0;
+  unsigned long long *kin = nullptr, *kout = nullptr;
+  int *vin = nullptr, *vout = nullptr;
+  HGX_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, kin, kout, vin,
+                                                  vout, (int)m, 0, 64, ctx->stream));
+  const size_t koff = (sizeof(unsigned long long) * 2 * (size_t)(m + 1) + 255) / 256 * 256;
+  HGX_TRY(hgx_ensure(ctx, ctx->st_keys, koff + sort_tmp + 256));
+  HGX_TRY(hgx_ensure(ctx, ctx->st_vals, sizeof(int) * 2 * (size_t)(m + 1)));
+  kin = ctx->st_keys.as<unsigned long long>();
+  kout = kin + (m + 1);
+  vin = ctx->st_vals.as<int>();
+  vout = vin + (m + 1);
+  if (m > 0) {
+    hipLaunchKernelGGL(store_select, dim3(grid_for(ctx->n_store, 256)), dim3(256), 0,
+                       ctx->stream, ctx->store.as<uint32_t>(), ctx->n_store, k1, k2,
+                       (uint32_t)bin_lo, (uint32_t)bin_hi, ctx->st_sel.as<uint32_t>(),
+                       kin, vin, ctx->s0.as<unsigned long long>());
+    HGX_LAUNCH_CHECK(ctx);
+    size_t tmp = sort_tmp;
+    HGX_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->st_keys.as<char>() + koff, tmp,
+                                                    kin, kout, vin, vout, (int)m, 0, 64,
+                                                    ctx->stream));
+  }
+  // 2. the batch tail of the previous load goes first
+  if (carry > 0) {
+    HGX_TRY(hgx_ensure(ctx, ctx->st_tmp, sizeof(int) * (size_t)carry * (R + 3)));
+    HGX_HIP(ctx, hipMemcpyAsync(ctx->st_tmp.p, ctx->rec_idx.as<int>() + ctx->n_rec * R,
+                                sizeof(int) * carry * R, hipMemcpyDeviceToDevice,
+                                ctx->stream));
+    HGX_HIP(ctx, hipMemcpyAsync(ctx->st_tmp.as<int>() + carry * R,
+                                ctx->rec_tgt.as<float>() + ctx->n_rec * 3,
+                                sizeof(float) * carry * 3, hipMemcpyDeviceToDevice,
+                                ctx->stream));
+    HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  const int64_t total = carry + m;
+  HGX_TRY(hgx_ensure(ctx, ctx->rec_idx, sizeof(int32_t) * (total * R + 1)));
+  HGX_TRY(hgx_ensure(ctx, ctx->rec_tgt, sizeof(float) * (total * 3 + 1)));
+  if (carry > 0) {
+    HGX_HIP(ctx, hipMemcpyAsync(ctx->rec_idx.p, ctx->st_tmp.p, sizeof(int) * carry * R,
+                                hipMemcpyDeviceToDevice, ctx->stream));
+    HGX_HIP(ctx, hipMemcpyAsync(ctx->rec_tgt.p, ctx->st_tmp.as<int>() + carry * R,
+                                sizeof(float) * carry * 3, hipMemcpyDeviceToDevice,
+                                ctx->stream));
+  }
+  // 3. the chunk's trainer records in key order
+  if (m > 0) {
+    hipLaunchKernelGGL(store_expand, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream,
+                       ctx->st_sel.as<uint32_t>(), vout, m, carry, t, K, ctx->store_seed,
+                       csr_of(ctx), ctx->rec_idx.as<int>(), ctx->rec_tgt.as<float>(),
+                       ctx->s0.as<int>() + 2);
+    HGX_LAUNCH_CHECK(ctx);
+  }
+  unsigned long long got[2] = {0, 0};
+  HGX_HIP(ctx, hipMemcpyAsync(got, ctx->s0.p, 16, hipMemcpyDeviceToHost, ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  HGX_CHECK(ctx, (int64_t)(got[0]) == m || m == 0, HGX_EHIP,
+            "store selection found %llu of %lld records", got[0], (long long)m);
+  HGX_CHECK(ctx, (got[1] & 0xffffffffull) == 0, HGX_EVALUE,
+            "a stored node-edge record has an endpoint without neighbours");
+  // 4. whole batches now; the tail waits for the next load unless last
+  const int64_t keep = last ? 0 : total % batch;
+  ctx->n_rec = total - keep;
+  ctx->store_carry = keep;
+  ctx->K = K;
+  ctx->rec_bounds[0] = 0;
+  ctx->rec_bounds[1] = ctx->n_rec;
+  ctx->n_rec_blocks = 1;
+  ctx->smp_family = -1;
+  ctx->rec_in_order = true;
+  if (n_records) *n_records = ctx->n_rec;
+  return HGX_OK;
+}

@@ -1835,6 +1835,13 @@ __global__ void loss_final(const double *part, double *acc) {
   if (threadIdx.x == 0) *acc += s[0];
 }
 
+// the identity order (records already in epoch order, ctx->rec_in_order)
+__global__ void iota_perm(int64_t n, int *perm) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    perm[i] = (int)i;
+}
+
 __global__ void shuffle_keys(uint64_t seed, int epoch, int64_t n,
                              unsigned long long *keys, int *vals) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -2027,6 +2034,8 @@ extern "C" int hgx_records_set(hgx_ctx *ctx, int64_t n, int K,
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->n_rec = n;
   ctx->K = K;
+  ctx->smp_family = -1;
+  ctx->rec_in_order = false;
   ctx->rec_bounds[0] = 0;
   ctx->rec_bounds[1] = n;
   ctx->n_rec_blocks = 1;
@@ -2087,6 +2096,8 @@ extern "C" int hgx_records_import(hgx_ctx *ctx, int64_t n, int K,
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->n_rec = n;
   ctx->K = K;
+  ctx->smp_family = -1;
+  ctx->rec_in_order = false;
   if (nblocks > 0) {
     for (int i = 0; i <= nblocks; i++) ctx->rec_bounds[i] = bounds[i];
     ctx->n_rec_blocks = nblocks;
@@ -2125,6 +2136,9 @@ extern "C" int hgx_records_copy(hgx_ctx *dst, hgx_ctx *src) {
   HGX_HIP(dst, hipStreamSynchronize(dst->stream));
   dst->n_rec = n;
   dst->K = K;
+  dst->smp_family = src->smp_family;
+  dst->smp_seed = src->smp_seed;
+  dst->rec_in_order = src->rec_in_order;
   dst->n_rec_blocks = src->n_rec_blocks;
   for (int i = 0; i <= src->n_rec_blocks; i++) dst->rec_bounds[i] = src->rec_bounds[i];
   return HGX_OK;
@@ -2572,11 +2586,14 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
   double *dloss = reinterpret_cast<double *>(ctx->s6.as<char>() + 32);
   double *dpart = reinterpret_cast<double *>(ctx->s6.as<char>() + 64);
 
+  // records loaded by hgx_store_load: trained in the order they were
+  // written (the store drew the epoch's global permutation)
+  const bool in_order = !perms && ctx->rec_in_order;
   // shuffle scratch (device shuffle only)
   size_t sort_tmp = 0, sort_off = 0;
   unsigned long long *keys_in = nullptr, *keys_out = nullptr;
   int *vals_in = nullptr;
-  if (!perms) {
+  if (!perms && !in_order) {
     HGX_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, keys_in,
                                                     keys_out, vals_in, perm, (int)n));
     sort_off = (sizeof(unsigned long long) * 2 * n + sizeof(int) * n + 255) / 256 * 256;
@@ -2694,6 +2711,9 @@ extern "C" int hgx_train(hgx_ctx *ctx, int batch, int max_epochs, float lr,
         rc = hgx_fail(ctx, HGX_EHIP, "permutation upload failed");
         break;
       }
+    } else if (in_order) {
+      hipLaunchKernelGGL(iota_perm, dim3(grid_for(n, 256)), dim3(256), 0,
+                         ctx->stream, n, perm);
     } else {
       hipLaunchKernelGGL(shuffle_keys, dim3(grid_for(n, 256)), dim3(256), 0,
                          ctx->stream, shuffle_seed, ep, n, keys_in, vals_in);

@@ -117,59 +117,66 @@ def _plot_distributions(path, records):
   fig.savefig(str(path))
 
 
-# Records resident at once before the skeleton streams the record stream in
-# row chunks (68 B per record at K = 5: 2^30 records = 73 GB of HBM).
+# Records resident at once (68 B per record at K = 5: 2^30 records = 73
+# GB of HBM). A stream whose record bound exceeds it is sampled once into
+# the compact record store (12 B per record) in strided row chunks of at
+# most this many records, and every epoch streams through the store in
+# chunks of at most this many records (Hg2vModel.fit_store).
 RECORDS_BUDGET = 1 << 30
+# Records per sampled row class and per loaded chunk of a streamed epoch:
+# C4 (5.9e9 records) then holds the 71 GB store, one 36.5 GB chunk of
+# trainer records, 19 GB of load scratch and 31 GB of d = 256 tables and
+# Adagrad state -- ~170 GB of the 288 GB HBM.
+STORE_CHUNK = 1 << 29
 
 
-# CUs of the sampling context when a streamed epoch samples chunk c + 1
-# beside chunk c's training (0: sample and train in turn on one context).
-# 192 of MI355X's 256: the trainer keeps 64 CUs (one per workgroup of a
-# batch step). Full C4 HOBE epoch (profiles/r04/c4_epoch/): 350 s in turn,
-# 261 s at 192 / 262 s at 160 / 286 s at 128 sampler CUs, the batch step
-# 9.28 -> 9.42 us, tables bit-identical.
-STREAM_OVERLAP_CUS = 192
-
-
-class _SideSampler:
-  """The second context of an overlapped streamed epoch and its sampler."""
-
-  def __init__(self, ctx, sample):
-    self.ctx, self.sample = ctx, sample
-
-
-def _bound(inc, per_row, row_quota, per_quota):
-  """Record bound per row: `per_row`, or with row quotas (node, edge) their
-  total times `per_quota` spread over the rows (the streaming decision and
-  the chunk count only use bound x rows)."""
-  if row_quota is None:
-    return per_row
-  tot = per_quota * (int(np.sum(row_quota[0], dtype=np.int64)) +
-                     int(np.sum(row_quota[1], dtype=np.int64)))
-  return max(1, -(-tot // max(inc.N + inc.E, 1)))
-
-
-def _row_chunks(inc, bound_per_row, budget):
+def _row_chunks(bound_n, bound_e, budget):
   """Split the rows into n strided classes (offset c, stride n: node rows
-  and edge rows r = c mod n) so that each chunk's record upper bound
-  (bound_per_row per node row and per edge row) stays within `budget`.
-  Strided, not contiguous: every chunk is a uniform slice of the id space,
-  so hub rows (low ids in the power-law generator; sorted or community
-  ordered ids in real data) spread over all chunks, chunks cost the same to
-  sample, and each chunk's shuffle window mixes the whole graph."""
-  total = bound_per_row * (inc.N + inc.E)
+  and edge rows r = c mod n) so that every class's record bound -- the sum
+  of its rows' bounds bound_n[r] / bound_e[r] -- stays within `budget`
+  (the sampler holds one class's records at a time). Strided, not
+  contiguous: hub rows (low ids in the power-law generator; sorted or
+  community ordered ids in real data) spread over all classes, so classes
+  cost the same to sample."""
+  bn = np.asarray(bound_n, np.int64)
+  be = np.asarray(bound_e, np.int64)
+  total = int(bn.sum() + be.sum())
   n = max(1, -(-total // budget))
+  top = max(bn.size, be.size, 1)
+  while n < top:
+    cls = (np.bincount(np.arange(bn.size) % n, weights=bn, minlength=n) +
+           np.bincount(np.arange(be.size) % n, weights=be, minlength=n))
+    if cls.max() <= budget:
+      break
+    n = min(top, n + max(1, n // 8))
   return [(c, n) for c in range(n)]
+
+
+def fill_store(ctx, inc, chunk_fn, bound_n, bound_e, budget):
+  """Sample the stream once into ctx's record store: strided row classes
+  (_row_chunks) sampled in turn by chunk_fn(offset, stride) (the records of
+  that class now on ctx), each packed into the store (hgx_store_append).
+  Returns the records stored."""
+  chunks = _row_chunks(bound_n, bound_e, budget)
+  ctx.store_reset(int(np.sum(bound_n, dtype=np.int64) +
+                      np.sum(bound_e, dtype=np.int64)))
+  for off, stride in chunks:
+    chunk_fn(off, stride)
+    ctx.store_append()
+  return ctx.store_info()[0]
 
 
 def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
                              loss, act, fit_batch_size, fit_epochs,
                              debug_summary_path, disable_pbar, ctx=None,
-                             chunk_sampler_fn=None, bound_per_row=0,
+                             chunk_sampler_fn=None, row_bounds=None,
                              records_budget=None):
   """embedding.py:269-305, device-resident end to end. `hypergraph` is the
   reference's Hypergraph message or an already compressed Incidence (e.g.
-  proto_native.read_incidence of a file too large for Python protobuf)."""
+  proto_native.read_incidence of a file too large for Python protobuf).
+  A stream whose record bound (row_bounds(inc): per node row, per edge
+  row) exceeds the budget is sampled once into the compact record store
+  and trained from it with Keras' global shuffle (Hg2vModel.fit_store)."""
   del disable_pbar
   ctx = ctx or get_context()
   if isinstance(hypergraph, Incidence):
@@ -177,37 +184,19 @@ def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
   else:
     inc = Incidence.from_hypergraph(hypergraph)  # CompressRange + CSR
   budget = RECORDS_BUDGET if records_budget is None else records_budget
-  if callable(bound_per_row):  # a bound that depends on the incidence
-    bound_per_row = bound_per_row(inc)
-  if chunk_sampler_fn is not None and bound_per_row * (inc.N + inc.E) > budget:
-    # the stream does not fit: sample and train strided row chunks in turn
-    chunks = _row_chunks(inc, bound_per_row, budget)
-    seed = numpy_seed()
-    cus = STREAM_OVERLAP_CUS
-    side = None
-    if cus:
-      # chunk c + 1 sampled on a second context (its stream on `cus` CUs)
-      # while chunk c trains on this one (the other CUs); the host hands
-      # the chunks over (Hg2vModel.fit_streaming `side`)
-      side_ctx = _hgx.Context(ctx.device)
-      side_ctx.set_tuning("stream_cus", cus)
-      ctx.set_tuning("stream_cus", -cus)
-      prep = chunk_sampler_fn(inc, side_ctx)
-      side = _SideSampler(side_ctx, lambda c: prep(seed, *chunks[c]))
-    else:
-      prep = chunk_sampler_fn(inc, ctx)
-    try:
+  if chunk_sampler_fn is not None:
+    bn, be = row_bounds(inc)
+    if int(np.sum(bn, dtype=np.int64) + np.sum(be, dtype=np.int64)) > budget:
+      seed = numpy_seed()
+      sample = chunk_sampler_fn(inc, ctx)
+      chunk = min(budget, STORE_CHUNK)
+      fill_store(ctx, inc, lambda off, stride: sample(seed, off, stride), bn,
+                 be, chunk)
       model = Hg2vModel(inc.N + 1, inc.E + 1, dimension, num_neighbors, loss,
                         act, ctx=ctx)
-      model.fit_streaming(lambda c: prep(seed, *chunks[c]), len(chunks),
-                          batch_size=fit_batch_size, epochs=fit_epochs,
-                          side=side)
+      model.fit_store(chunk, batch_size=fit_batch_size, epochs=fit_epochs)
       node_w, edge_w = model.get_weights()
-    finally:
-      if side is not None:
-        ctx.set_tuning("stream_cus", 0)
-        side.ctx.close()
-    return coords_to_embedding(inc, node_w[1:], edge_w[1:], dimension, "")
+      return coords_to_embedding(inc, node_w[1:], edge_w[1:], dimension, "")
   records = sampler_fn(inc, ctx)
   if debug_summary_path is not None:
     _plot_distributions(debug_summary_path, records)
@@ -223,9 +212,10 @@ def EmbedHg2vBoolean(hypergraph, dimension, num_neighbors=5, num_samples=200,
                      debug_summary_path=None, disable_pbar=False,
                      records_budget=None, row_quota=None):
   """FOBE: BooleanSamples + BooleanModel (embedding.py:308-329). A stream of
-  more than `records_budget` records is sampled and trained in strided row
-  chunks (Hg2vModel.fit_streaming). row_quota = (node quotas, edge quotas)
-  (not in the reference) replaces int(weight * S) per row: bounded runs."""
+  more than `records_budget` records is sampled once into the compact
+  record store and every epoch trains it in Keras' global shuffle order
+  (Hg2vModel.fit_store). row_quota = (node quotas, edge quotas) (not in
+  the reference) replaces int(weight * S) per row: bounded runs."""
   sampler_fn = lambda inc, ctx: sample_fobe(inc, num_neighbors, num_samples,
                                             neg_samples, ctx=ctx,
                                             row_quota=row_quota)
@@ -246,21 +236,27 @@ def EmbedHg2vBoolean(hypergraph, dimension, num_neighbors=5, num_samples=200,
                              geq if neg else None)
     return chunk
 
-  # per row at most q nn (or ee) and q node-edge records, q = int(w * S)
-  # (hg2v_sample.py:138-194), plus 3 negative blocks of int(w * neg_samples),
-  # w the largest node / edge weight of the compressed incidence (any float
-  # in the proto, default 1)
-  def bound_per_row(inc):
-    wmax = float(max(np.max(inc.node_weight, initial=0.0),
-                     np.max(inc.edge_weight, initial=0.0), 0.0))
-    neg = int(wmax * 3 * neg_samples)
-    return _bound(inc, int(wmax * 2 * num_samples) + 2, row_quota, 2) + neg
+  # per node row at most q nn and q node-edge records, per edge row q ee and
+  # q node-edge records, q = int(w * S) (hg2v_sample.py:138-194); negatives
+  # (:198-240): g nn + g node-edge per node row, 2 g ee + g node-edge per
+  # edge row, g = int(w * neg_samples)
+  def row_bounds(inc):
+    if row_quota is not None:
+      qn, qe = (np.asarray(q, np.int64) for q in row_quota)
+    else:
+      qn = _quotas(inc.node_weight, num_samples).astype(np.int64)
+      qe = _quotas(inc.edge_weight, num_samples).astype(np.int64)
+    bn, be = 2 * qn, 2 * qe
+    if neg_samples > 0:
+      bn = bn + 2 * _quotas(inc.node_weight, neg_samples).astype(np.int64)
+      be = be + 3 * _quotas(inc.edge_weight, neg_samples).astype(np.int64)
+    return bn, be
 
   emb = _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors,
                                  sampler_fn, _hgx.LOSS_KLD, _hgx.ACT_SIGMOID,
                                  batch_size, epochs, debug_summary_path,
                                  disable_pbar, chunk_sampler_fn=chunk_sampler_fn,
-                                 bound_per_row=bound_per_row,
+                                 row_bounds=row_bounds,
                                  records_budget=records_budget)
   emb.method_name = "HG2V_BOOLEAN"
   return emb
@@ -318,25 +314,31 @@ def hobe_sharded(inc, dimension, num_neighbors=5, num_samples=200,
        np.random draws (algebraic_distance.py:140-141), then one all-gather
        of the node coordinates (N x 10 floats: 400 MB at C4) so every rank
        holds the HOBE weights' inputs;
-    2. the stream in strided row chunks (_row_chunks), each sampled by the
-       ranks on strided shares of its rows and all-gathered in row order
-       (hg2v_sample.sharded_chunk_fn);
+    2. sampling row-sharded: a stream within the budget is sampled on the
+       ranks' strided row shares and all-gathered in row order
+       (hg2v_sample.sample_sharded); a larger one is sampled once into
+       every rank's record store, strided row class by class, each class's
+       12-byte entries all-gathered while the next class samples
+       (hg2v_sample.sharded_store_fill);
     3. training as replicas (batch-256 Adagrad does not
-       partition): every rank trains the same model on the same chunks in
-       the same order (seeds broadcast from rank 0), Hg2vModel.fit_streaming
-       -- or, when the stream is one chunk, it is sampled once and fit() runs
-       the epochs on it, as the single-process path does.
+       partition): every rank trains the same model on the same epochs
+       (seeds broadcast from rank 0): fit() on the resident stream, or
+       Hg2vModel.fit_store's global-shuffle epochs over the store.
   `alg_coords` = (x, y) skips step 1 (tests: the sharded relaxation sums
   partials in another order than one GPU, within 1e-4; steps 2-3 are then
-  bit-identical to the single-process call). Returns (node_tab, edge_tab)
-  without the padding row, identical on every rank."""
+  bit-identical to the single-process call). `stats` (a dict) receives the
+  stage times. Returns (node_tab, edge_tab) without the padding row,
+  identical on every rank."""
+  import time
   import torch.distributed as dist
   from .algebraic_distance import _init_coords, alg_dist_sharded
-  from .hg2v_sample import sharded_chunk_fn
+  from .hg2v_sample import sample_sharded, sharded_store_fill
   ctx = ctx or get_context()
   dev = _dist_backend_device(group)
   world = dist.get_world_size(group)
+  st = stats if stats is not None else {}
   ctx.upload(inc)
+  t0 = time.perf_counter()
   if alg_coords is None:
     x0 = y0 = None
     if dist.get_rank(group) == 0:
@@ -357,25 +359,39 @@ def hobe_sharded(inc, dimension, num_neighbors=5, num_samples=200,
                                            edge_ranges=edge_ranges,
                                            stats=stats)
     x = _all_gather_rows(xo, r0, r1, inc.N, group, dev)
-    if stats is not None:
-      stats["alg_ms"] = ms
+    st["alg_ms"] = ms
   else:
     x, y = alg_coords
   ctx.alg_set(x, y)
+  st["alg_s"] = time.perf_counter() - t0
   sample_seed, model_seed, fit_seed = _broadcast_seeds(3, group, dev)
-  budget = (RECORDS_BUDGET // 2 if world > 1 else RECORDS_BUDGET) \
-      if records_budget is None else records_budget
-  chunks = _row_chunks(inc, 2 * num_samples, budget)
-  fn = sharded_chunk_fn(inc, num_neighbors, num_samples, chunks, ctx=ctx,
-                        seed=sample_seed, kind="hobe", group=group, device=dev)
+  budget = RECORDS_BUDGET if records_budget is None else records_budget
+  bn = np.full(inc.N, 2 * num_samples, np.int64)
+  be = np.full(inc.E, 2 * num_samples, np.int64)
   model = Hg2vModel(inc.N + 1, inc.E + 1, dimension, num_neighbors,
                     _hgx.LOSS_MSE, _hgx.ACT_RELU, ctx=ctx, seed=model_seed)
-  if len(chunks) == 1:
-    fn(0)
+  t0 = time.perf_counter()
+  if int(bn.sum() + be.sum()) <= budget:
+    n, _ = sample_sharded(inc, num_neighbors, num_samples, ctx=ctx,
+                          seed=sample_seed, kind="hobe", group=group,
+                          device=dev)
+    st["sampling_s"] = time.perf_counter() - t0
+    st["records"] = n
+    t0 = time.perf_counter()
     model.fit(batch_size=batch_size, epochs=epochs, shuffle_seed=fit_seed)
   else:
-    model.fit_streaming(fn, len(chunks), batch_size=batch_size, epochs=epochs,
-                        seed=fit_seed % (2**32))
+    chunk = min(budget, STORE_CHUNK)
+    chunks = _row_chunks(bn, be, chunk)
+    n = sharded_store_fill(inc, num_neighbors, num_samples, chunks, ctx=ctx,
+                           seed=sample_seed, kind="hobe", group=group,
+                           device=dev, capacity=int(bn.sum() + be.sum()))
+    st["sampling_s"] = time.perf_counter() - t0
+    st["records"] = n
+    st["sampling_chunks"] = len(chunks)
+    t0 = time.perf_counter()
+    model.fit_store(chunk, batch_size=batch_size, epochs=epochs,
+                    seed=fit_seed % (2**32))
+  st["train_s"] = time.perf_counter() - t0
   node_w, edge_w = model.get_weights()
   return node_w[1:], edge_w[1:]
 
@@ -389,7 +405,8 @@ def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
   UnweightedFloatModel (embedding.py:389-416). `alpha` is accepted and, as
   in the reference, not used (_alpha_scale is called with alpha=0).
   A stream of more than `records_budget` records (RECORDS_BUDGET) is
-  sampled and trained in strided row chunks (Hg2vModel.fit_streaming).
+  sampled once into the compact record store and every epoch trains it in
+  Keras' global shuffle order (Hg2vModel.fit_store).
   `group` (a torch.distributed process group, e.g. group.WORLD under
   torch.distributed.run, one GPU per rank): the multi-GPU pipeline
   (hobe_sharded); every rank returns the same embedding. row_quota =
@@ -433,13 +450,20 @@ def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
                              edge_q=eq)
     return chunk
 
-  # per row at most S nn (or ee) and S node-edge records (hg2v_sample.py:659-703)
+  # per row at most q nn (or ee) and q node-edge records, q = S or the row's
+  # quota (hg2v_sample.py:659-703)
+  def row_bounds(inc):
+    if row_quota is not None:
+      return (2 * np.asarray(row_quota[0], np.int64),
+              2 * np.asarray(row_quota[1], np.int64))
+    return (np.full(inc.N, 2 * num_samples, np.int64),
+            np.full(inc.E, 2 * num_samples, np.int64))
+
   emb = _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors,
                                  sampler_fn, _hgx.LOSS_MSE, _hgx.ACT_RELU,
                                  batch_size, epochs, debug_summary_path,
                                  disable_pbar, chunk_sampler_fn=chunk_sampler_fn,
-                                 bound_per_row=lambda inc: _bound(
-                                     inc, 2 * num_samples, row_quota, 2),
+                                 row_bounds=row_bounds,
                                  records_budget=records_budget)
   emb.method_name = "HG2V_ALG_DIST"
   return emb

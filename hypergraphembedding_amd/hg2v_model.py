@@ -37,94 +37,43 @@ class Hg2vModel:
                           shuffle_seed=numpy_seed() if shuffle_seed is None
                           else shuffle_seed, perms=perms)
 
-  def fit_streaming(self, chunk_fn, n_chunks, batch_size=256, epochs=10,
-                    min_delta=1e-3, lr=0.01, eps=1e-7, seed=None,
-                    chunk_perms=None, side=None):
-    """fit() over a record stream too large to keep resident (SURVEY §5:
-    "stream samples in chunks"; the reference materialises every record,
-    embedding.py:277-284). chunk_fn(c) makes chunk c resident on the context
-    and returns its record count; chunks must be the same records every
-    epoch (the device samplers are keyed by seed and row, so re-sampling a
-    row class reproduces it). Per epoch the chunk order is shuffled and each
-    chunk's records are shuffled on the device: a windowed shuffle in place
-    of Keras' global one over records that never coexist. The
-    chunks are strided row classes (embedding._row_chunks), each a uniform
-    slice of the graph, so a window mixes records of the whole id range;
-    model state carries across chunks (one-epoch hgx_train calls), the epoch
-    loss is the record-weighted mean and EarlyStopping(min_delta,
-    patience=0) applies to it. Epoch ep's chunk order and shuffle seeds come
-    from RandomState([seed, ep]). chunk_perms[ep][c] (optional) fixes a
-    chunk's record order.
-
-    side (optional): a second context on the same device that samples,
-    `side.ctx` with `side.sample(c)` -> record count (chunk_fn is then
-    unused). Chunk c + 1 is sampled on it while chunk c trains here (each
-    context's work on its own stream, on disjoint CUs when both have
-    stream_cus set); the host hands the chunk over (hgx_records_copy) once
-    both are done -- no cross-stream barrier packet ever waits in a queue.
-    Same records, order and seeds as the in-line form, so the same tables
-    bit for bit.
-    Returns the epoch losses; total records per epoch may exceed 2^31."""
-    import threading
+  def fit_store(self, budget, batch_size=256, epochs=10, min_delta=1e-3,
+                lr=0.01, eps=1e-7, seed=None):
+    """fit() over the record store of the context (hgx_store_*): a stream
+    sampled once and kept as 12-byte entries because its trainer records
+    do not fit in HBM (the C4 HOBE stream: 5.9e9 records, 404 GB; the
+    reference materialises it and fits with Keras' shuffle=True,
+    embedding.py:277-302). Every epoch is one global pseudo-random
+    permutation of all records (keyed by record identity and the epoch
+    seed), cut into batches of `batch_size` in that order -- Keras'
+    semantics -- and trained through chunks of at most `budget` records
+    (hgx_store_plan / hgx_store_load): a chunk is the next stretch of the
+    epoch's order, and a chunk's last partial batch is completed by the
+    next chunk's first records. The epoch loss is the record-weighted mean
+    (Keras' batch-size-weighted mean) and EarlyStopping(min_delta,
+    patience=0) applies to it. Epoch ep's seed comes from
+    RandomState([seed, ep]). Returns the epoch losses; per epoch the
+    records may exceed 2^31."""
     import numpy as np
     base = numpy_seed() % (2**32) if seed is None else seed
-
-    def plan(ep):
-      ers = np.random.RandomState([base, ep])
-      order = (np.arange(n_chunks) if chunk_perms is not None
-               else ers.permutation(n_chunks))
-      seeds = ers.randint(0, 2**62, size=n_chunks, dtype=np.int64)
-      return [int(c) for c in order], [int(x) for x in seeds]
-
-    def train(c, ep, shuffle_seed, out):
-      try:
-        perms = (None if chunk_perms is None
-                 else chunk_perms[ep][c][None, :])
-        self.ctx.train(batch=batch_size, max_epochs=1, lr=lr, eps=eps,
-                       loss=self.loss, act=self.act, min_delta=-1e30,
-                       shuffle_seed=shuffle_seed, perms=perms)
-        out.append(self.ctx.train_loss_sum())
-        self.chunk_stats.append((ep, c) + tuple(self.ctx.train_stats()))
-      except BaseException as e:  # re-raised by the caller
-        out.append(e)
-
     best, losses = float("inf"), []
     self.records_per_epoch = 0
     self.chunk_stats = []  # (epoch, chunk, step ms, records, batches)
-    ahead = None  # (epoch, chunk, records) sampled on `side` ahead of time
     for ep in range(epochs):
-      order, seeds = plan(ep)
+      es = int(np.random.RandomState([base, ep]).randint(0, 2**62, dtype=np.int64))
+      bounds, counts = self.ctx.store_plan(es, budget)
       lsum, n = 0.0, 0
-      for i, c in enumerate(order):
-        if side is None:
-          m = chunk_fn(c)
-          if m == 0:
-            continue
-          out = []
-          train(c, ep, seeds[i], out)
-        else:
-          if ahead is not None and ahead[:2] == (ep, c):
-            m = ahead[2]
-          else:
-            m = side.sample(c)
-          ahead = None
-          if m == 0:
-            continue
-          self.ctx.records_copy_from(side.ctx)
-          nxt = ((ep, order[i + 1]) if i + 1 < len(order) else
-                 (ep + 1, plan(ep + 1)[0][0]) if ep + 1 < epochs else None)
-          out = []
-          th = threading.Thread(target=train, args=(c, ep, seeds[i], out))
-          th.start()
-          try:
-            if nxt is not None:
-              ahead = (nxt[0], nxt[1], side.sample(nxt[1]))
-          finally:
-            th.join()
-        if isinstance(out[0], BaseException):
-          raise out[0]
-        lsum += out[0]
+      nc = counts.size
+      for c in range(nc):
+        m = self.ctx.store_load(es, bounds[c], bounds[c + 1], batch_size,
+                                c == nc - 1)
+        if m == 0:
+          continue
+        self.ctx.train(batch=batch_size, max_epochs=1, lr=lr, eps=eps,
+                       loss=self.loss, act=self.act, min_delta=-1e30)
+        lsum += self.ctx.train_loss_sum()
         n += m
+        self.chunk_stats.append((ep, c) + tuple(self.ctx.train_stats()))
       self.records_per_epoch = n
       cur = lsum / max(n, 1)
       losses.append(cur)

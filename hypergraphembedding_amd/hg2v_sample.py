@@ -117,7 +117,7 @@ def shard_range(n, world, rank):
 
 def row_class_quota(quota, offset, stride):
   """`quota` on the rows r = offset (mod stride), 0 elsewhere: one row class
-  of a strided split (fit_streaming chunks, sample_sharded ranks). A class
+  of a strided split (record-store fill chunks, sample_sharded ranks). A class
   is a uniform slice of the id space, so hub rows (the power-law generator
   numbers edges by popularity; real ids are often sorted or community
   ordered) spread over every chunk and rank instead of filling the first."""
@@ -140,7 +140,7 @@ def sample_sharded(inc, num_neighbors, num_samples, ctx=None, seed=0,
   (sampling shards by row with no data-path collective).
 
   `rows` = (offset, stride) restricts the call to one row class of a
-  strided split (fit_streaming chunk `offset` of `stride`; default: every
+  strided split (store-fill chunk `offset` of `stride`; default: every
   row): node rows and edge rows r = offset (mod stride). Rank g samples the
   rows r = offset + g * stride (mod stride * world) of that class -- a
   strided share, so the hub rows spread over the ranks -- (kind "hobe":
@@ -255,26 +255,94 @@ def sample_sharded(inc, num_neighbors, num_samples, ctx=None, seed=0,
   return total, allsz
 
 
-def sharded_chunk_fn(inc, num_neighbors, num_samples, chunks, ctx=None,
-                     seed=0, kind="hobe", node_quota=None, edge_quota=None,
-                     group=None, device=None):
-  """chunk_fn for Hg2vModel.fit_streaming over row-sharded sampling: chunk c
-  (the row class (offset, stride) = chunks[c], embedding._row_chunks) is
-  sampled by every rank on its strided share of the class's rows and
-  all-gathered, so each training replica holds only one chunk's stream at a
-  time (the reference materialises the whole stream in host RAM,
-  embedding.py:277-284). Returns the records of the chunk now resident on
-  ctx, identical to a single-process sample of the same rows
-  (sample_sharded)."""
+def sharded_store_fill(inc, num_neighbors, num_samples, chunks, ctx=None,
+                       seed=0, kind="hobe", node_quota=None, edge_quota=None,
+                       group=None, device=None, capacity=0):
+  """Sample a record stream too large for HBM once into every rank's record
+  store (hgx_store_*), the sampling row-sharded over the ranks of a
+  torch.distributed group. For each strided row class
+  chunks[c] = (offset, stride) (embedding._row_chunks) rank g samples the
+  rows r = offset + g * stride (mod stride * world) of the class and packs
+  them into its store; the class's new entries (12 B per record) are then
+  all-gathered asynchronously -- RCCL on device buffers for a GPU device,
+  gloo through host arrays otherwise -- while the next class is sampled,
+  and every rank appends the other ranks' entries. Every draw is keyed by
+  (seed, block, row, column or rank in row), so every rank ends with
+  exactly the records a single process samples, in another order -- which
+  the store's epoch order does not see (it is keyed by record identity):
+  Hg2vModel.fit_store then trains the same epochs on every rank. Returns
+  the records in the store."""
+  import torch
+  import torch.distributed as dist
   ctx = ctx or get_context()
+  world, rank = dist.get_world_size(group), dist.get_rank(group)
+  K = num_neighbors
+  if node_quota is None:  # HOBE: S per row (hg2v_sample.py:659-703)
+    assert kind == "hobe"
+    node_quota = np.full(inc.N, num_samples, np.int32)
+    edge_quota = np.full(inc.E, num_samples, np.int32)
+  gpu = device is None or torch.device(device).type == "cuda"
+  dev = torch.device("cuda", ctx.device) if device is None else torch.device(device)
+  ctx.store_reset(capacity)
+  pending = None  # (handle, recv buffers, per-rank counts) of the last class
 
-  def chunk(c):
-    total, _ = sample_sharded(inc, num_neighbors, num_samples, ctx=ctx,
-                              seed=seed, kind=kind, node_quota=node_quota,
-                              edge_quota=edge_quota, group=group,
-                              device=device, rows=chunks[c])
-    return total
-  return chunk
+  def finish(p):
+    work, recv, cnt = p
+    work.wait()
+    if gpu:
+      torch.cuda.current_stream(dev).synchronize()
+    for r in range(world):
+      if r == rank or cnt[r] == 0:
+        continue
+      if gpu:
+        ctx.store_write(None, fam, K, seed, n=int(cnt[r]),
+                        src_ptr=recv[r].data_ptr())
+      else:
+        ctx.store_write(recv[r][:int(cnt[r])].numpy().view(np.uint32), fam, K,
+                        seed)
+
+  fam = _hgx.STORE_HOBE if kind == "hobe" else _hgx.STORE_FOBE
+  for off, stride in chunks:
+    mine = (off + rank * stride, stride * world)
+    nq = row_class_quota(node_quota, *mine)
+    eq = row_class_quota(edge_quota, *mine)
+    before = ctx.store_info()[0]
+    if kind == "hobe":
+      ctx.sample_hobe(seed, K, num_samples, node_q=nq, edge_q=eq)
+    else:
+      ctx.sample_fobe(seed, K, nq, eq)
+    ctx.store_append()
+    new = ctx.store_info()[0] - before
+    t = torch.tensor([new], dtype=torch.int64, device=dev)
+    got = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(got, t, group=group)
+    cnt = [int(g.item()) for g in got]
+    if pending is not None:  # the previous class's exchange is done by now
+      finish(pending)
+      pending = None
+    m = max(cnt)
+    if m == 0:
+      continue
+    send = torch.zeros((m, 3), dtype=torch.int32, device=dev)
+    if new:
+      if gpu:
+        torch.cuda.current_stream(dev).synchronize()
+        ctx.store_read(before, new, dst_ptr=send.data_ptr())
+      else:
+        send[:new] = torch.from_numpy(ctx.store_read(before, new).view(np.int32))
+    recv = [torch.empty_like(send) for _ in range(world)]
+    work = dist.all_gather(recv, send, group=group, async_op=True)
+    pending = (work, recv, cnt)
+  if pending is not None:
+    finish(pending)
+  if gpu:
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+  n = ctx.store_info()[0]
+  tot = torch.tensor([n], dtype=torch.int64, device=dev)
+  dist.all_reduce(tot, op=dist.ReduceOp.MAX, group=group)
+  assert int(tot.item()) == n, "ranks hold stores of different sizes"
+  return n
 
 
 def BooleanSamples(hypergraph, num_neighbors, num_samples, neg_samples=0,
@@ -437,6 +505,6 @@ def ModelInputToArrays(features, targets):
 __all__ = ["SimilarityRecord", "BooleanSamples", "AlgebraicDistanceSamples",
            "WeightedJaccardSamples", "sample_jaccard",
            "SamplesToModelInput", "ModelInputToArrays", "DeviceRecords",
-           "sample_sharded", "sharded_chunk_fn", "shard_range",
+           "sample_sharded", "sharded_store_fill", "shard_range",
            "row_class_quota",
            "sample_fobe", "sample_hobe", "records_from_arrays"]

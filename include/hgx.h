@@ -245,6 +245,55 @@ int hgx_records_export(hgx_ctx *ctx, void *d_idx, void *d_tgt);
 int hgx_records_import(hgx_ctx *ctx, int64_t n, int K, const void *d_idx,
                        const void *d_tgt, int nblocks, const int64_t *bounds);
 
+/* ---- compact record store: streams larger than HBM -------------------- *
+ * The reference materialises every SimilarityRecord once and fits with
+ * Keras' shuffle=True: each epoch a uniform permutation of the whole
+ * stream in batches of 256 (embedding.py:277-302). The store keeps each
+ * sampled record as 12 bytes (kind block and row, column or rank in row,
+ * target); the rest of the record (neighbour lists, negatives' columns) is
+ * re-derived from the sampler's keyed draws, bit for bit.
+ *   hgx_store_reset(capacity)   empty the store, reserve `capacity` records
+ *   hgx_store_append()          pack the records of the last
+ *                               hgx_sample_fobe / hgx_sample_hobe(_rows)
+ *                               call (HGX_ESTATE for any other stream; every
+ *                               record is checked to reload bit for bit);
+ *                               graphs of < 2^28 nodes and edges
+ *   hgx_store_read / _write     raw 3 x uint32 entries to / from host or
+ *                               device memory (multi-GPU: ranks exchange
+ *                               what they sampled); write takes the
+ *                               sampler family (0 FOBE, 1 HOBE), K, seed
+ *   hgx_store_plan(epoch_seed, budget)
+ *                               the epoch's order: records sorted by a
+ *                               bijective mix of (identity, epoch_seed), so
+ *                               the order does not depend on where records
+ *                               sit in the store; the key space cut into
+ *                               chunks of <= budget records, as bin ranges
+ *                               of HGX_STORE_BINS bins (bin_bounds:
+ *                               n_chunks + 1 entries, counts: n_chunks;
+ *                               both arrays of HGX_STORE_BINS + 1)
+ *   hgx_store_load(epoch_seed, bin_lo, bin_hi, batch, last)
+ *                               the chunk's records as the context's record
+ *                               stream, in epoch order, after the batch
+ *                               tail the previous load kept (so batches
+ *                               follow the global order); unless `last`,
+ *                               the stream's own tail (< batch records) is
+ *                               kept for the next load. hgx_train then
+ *                               trains the records in that order (no
+ *                               shuffle). n_records = records to train. */
+#define HGX_STORE_BINS 16384
+int hgx_store_reset(hgx_ctx *ctx, int64_t capacity);
+int hgx_store_append(hgx_ctx *ctx);
+int hgx_store_info(hgx_ctx *ctx, int64_t *n, int *family, int *K,
+                   uint64_t *seed);
+int hgx_store_read(hgx_ctx *ctx, int64_t start, int64_t n, void *dst,
+                   int dst_device);
+int hgx_store_write(hgx_ctx *ctx, int64_t n, const void *src, int src_device,
+                    int family, int K, uint64_t seed);
+int hgx_store_plan(hgx_ctx *ctx, uint64_t epoch_seed, int64_t budget,
+                   int *n_chunks, int32_t *bin_bounds, int64_t *counts);
+int hgx_store_load(hgx_ctx *ctx, uint64_t epoch_seed, int32_t bin_lo,
+                   int32_t bin_hi, int batch, int last, int64_t *n_records);
+
 /* ---- hg2v_weighting distance / span weights ------------------------------ *
  * hg2v_weighting.py:34-64 (WeightBySameTypeDistance), 67-103
  * (WeightByDistance), 170-192 + 236-293 (WeightByAlgebraicSpan,

@@ -160,7 +160,7 @@ class ShardEmu:
 
 class SampleEmu:
   """Test double of the row-keyed device samplers for the row-sharded
-  sampling driver (hg2v_sample.sample_sharded / sharded_chunk_fn): the same
+  sampling drivers (hg2v_sample.sample_sharded / sharded_store_fill): the same
   contract as hgx_sample_hobe_rows / hgx_sample_fobe -- kind blocks nn, ee,
   ne node rows, ne edge rows, each in row order; every draw keyed by (seed,
   block, row, rank in row) -- on a small incidence with numpy. Records are
@@ -208,6 +208,7 @@ class SampleEmu:
     blocks = [self._rows(0, nq, seed, K), self._rows(1, eq, seed, K),
               self._rows(2, nq, seed, K), self._rows(3, eq, seed, K)]
     self.K = K
+    self.seed = seed
     self.bounds = np.concatenate([[0], np.cumsum([len(b) for b in blocks])])
     recs = [x for b in blocks for x in b]
     self.idx = (np.stack([r for r, _ in recs]) if recs
@@ -226,3 +227,43 @@ class SampleEmu:
     self.idx = np.asarray(idx, np.int32).copy()
     self.tgt = np.asarray(tgt, np.float32).copy()
     self.bounds = np.array([0, self.idx.shape[0]], np.int64)
+
+  # ---- the record store's host contract (hgx_store_reset / _append /
+  # _info / _read / _write): entries {block << 28 | row, column, target
+  # bits} of the HOBE blocks ----
+  def store_reset(self, capacity=0):
+    self.store = np.zeros((0, 3), np.uint32)
+    self.store_meta = None
+
+  def store_append(self):
+    meta = (1, self.K, self.seed & (2**64 - 1))
+    assert self.store_meta in (None, meta)
+    self.store_meta = meta
+    ents = []
+    cols = ((0, 2, 0), (1, 3, 1), (0, 3, 2), (3, 0, 2))  # row, col, target
+    for b in range(4):
+      blk = slice(int(self.bounds[b]), int(self.bounds[b + 1]))
+      rc, cc, tc = cols[b]
+      row = self.idx[blk, rc].astype(np.uint32) - 1
+      e = np.stack([(np.uint32(b) << np.uint32(28)) | row,
+                    self.idx[blk, cc].astype(np.uint32) - 1,
+                    self.tgt[blk, tc].view(np.uint32)], 1)
+      ents.append(e)
+    self.store = np.concatenate([self.store] + ents).astype(np.uint32)
+
+  def store_info(self):
+    fam, K, seed = self.store_meta or (-1, 0, 0)
+    return self.store.shape[0], fam, K, seed
+
+  def store_read(self, start=0, n=None, dst_ptr=None):
+    assert dst_ptr is None
+    n = self.store.shape[0] - start if n is None else n
+    return self.store[start:start + n].copy()
+
+  def store_write(self, entries, family, K, seed, n=None, src_ptr=None):
+    assert src_ptr is None
+    meta = (family, K, seed & (2**64 - 1))
+    assert self.store_meta in (None, meta)
+    self.store_meta = meta
+    self.store = np.concatenate([self.store,
+                                 np.asarray(entries, np.uint32).reshape(-1, 3)])

@@ -1,0 +1,212 @@
+"""The compact record store (csrc/hgx_store.hip, hgx_store_*): record streams
+larger than HBM trained with Keras' global shuffle (embedding.py:277-302:
+the reference materialises every record and fits with shuffle=True).
+
+  * packing is lossless: every sampled record -- HOBE, FOBE with the five
+    negative blocks -- reloads bit for bit (ids, neighbour lists, targets);
+  * the epoch order is the host restatement's (tests/store_keys.py): the
+    records sorted by a bijective mix of their identity and the epoch seed,
+    whatever the store's order, cut into chunks of at most the budget, each
+    chunk's batch tail carried into the next load;
+  * an epoch trained from the store in small chunks equals, bit for bit,
+    one resident epoch over the same records in that global order (so a
+    streamed epoch is exactly a Keras epoch, only the permutation's RNG
+    differs);
+  * EmbedHg2vAlgDist / EmbedHg2vBoolean take the store path past the
+    budget.
+"""
+
+import numpy as np
+import pytest
+
+import oracle as O
+from store_keys import entry_keys, epoch_order, row_sort
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+  from hypergraphembedding_amd import _hgx
+  c = _hgx.Context(0)
+  yield c
+  c.close()
+
+
+@pytest.fixture(scope="module")
+def plg():
+  from hypergraphembedding_amd.synthetic import powerlaw_hypergraph
+  return powerlaw_hypergraph(N=20_000, E=10_000, seed=5)
+
+
+def _hobe(ctx, inc, seed=17, S=20, K=5, **q):
+  ctx.upload(inc)
+  r = O.Rng(3)
+  ctx.alg_set(r.random((inc.N, 10)), r.random((inc.E, 10)))
+  ctx.alg_run(20)
+  return ctx.sample_hobe(seed, K, S, **q)
+
+
+def _load_all(ctx, es, budget, batch=256):
+  """Every chunk of epoch `es`: (bounds, counts, [(idx, tgt) per load])."""
+  b, c = ctx.store_plan(es, budget)
+  out = []
+  for i in range(c.size):
+    m = ctx.store_load(es, b[i], b[i + 1], batch, i == c.size - 1)
+    idx, tgt = ctx.records_get()
+    assert idx.shape[0] == m
+    out.append((idx, tgt))
+  return b, c, out
+
+
+@pytest.mark.parametrize("kind", ["hobe", "fobe_ns"])
+def test_store_reloads_the_sampled_stream_bitwise(ctx, plg, kind):
+  """Pack then load (one chunk): the same records as sampled (a multiset
+  of ids, neighbour lists and target bits), in the host-computed key
+  order."""
+  inc = plg
+  if kind == "hobe":
+    n = _hobe(ctx, inc)
+  else:
+    ctx.upload(inc)
+    q = np.full(inc.N, 20, np.int32)
+    p = np.full(inc.E, 20, np.int32)
+    n = ctx.sample_fobe(29, 5, q, p, np.full(inc.N, 7, np.int32),
+                        np.full(inc.E, 7, np.int32))
+    assert ctx.records_blocks().size == 10  # nine kind blocks (negatives)
+  idx, tgt = ctx.records_get()
+  ctx.store_reset(n)
+  ctx.store_append()
+  assert ctx.store_info()[:3] == (n, 1 if kind == "hobe" else 0, 5)
+  ent = ctx.store_read()
+  assert ent.shape == (n, 3)
+  b, c, loads = _load_all(ctx, 12345, 10**9)
+  assert c.size == 1 and c[0] == n
+  lidx, ltgt = loads[0]
+  assert np.array_equal(row_sort(lidx, ltgt), row_sort(idx, tgt))
+  order = epoch_order(ent, 12345)
+  assert np.array_equal(lidx, idx[order])  # the store kept the sampler's order
+  assert np.array_equal(ltgt.view(np.uint32), tgt[order].view(np.uint32))
+
+
+def test_store_chunks_walk_the_global_order(ctx, plg):
+  """Chunks of <= budget records in key order; every load but the last
+  trains whole batches and carries its tail; concatenated, the loads are
+  the epoch's global order."""
+  n = _hobe(ctx, plg)
+  idx, tgt = ctx.records_get()
+  ctx.store_reset(n)
+  ctx.store_append()
+  ent = ctx.store_read()
+  for es, budget, batch in ((7, n // 5, 256), (8, 33_333, 100)):
+    b, c, loads = _load_all(ctx, es, budget, batch)
+    assert c.size >= 5 and c.max() <= budget and c.sum() == n
+    keys = entry_keys(ent, es)
+    bins = (keys >> np.uint64(64 - 14)).astype(np.int64)
+    for i in range(c.size):
+      assert ((bins >= b[i]) & (bins < b[i + 1])).sum() == c[i]
+    for li, _ in loads[:-1]:
+      assert li.shape[0] % batch == 0
+    order = epoch_order(ent, es)
+    cat = np.concatenate([li for li, _ in loads])
+    assert np.array_equal(cat, idx[order])
+    cat_t = np.concatenate([lt for _, lt in loads])
+    assert np.array_equal(cat_t.view(np.uint32), tgt[order].view(np.uint32))
+
+
+@pytest.mark.parametrize("d", [32, 128])
+def test_store_epochs_equal_resident_epochs_in_that_order(ctx, plg, d):
+  """fit_store with chunks of ~1/6 of the stream over 2 epochs vs the
+  resident trainer given the store's two global orders as perms: identical
+  tables bit for bit and the same epoch losses (every batch the same
+  records: the chunks' batch tails carry over)."""
+  from hypergraphembedding_amd import _hgx
+  from hypergraphembedding_amd.hg2v_model import Hg2vModel
+  n = _hobe(ctx, plg)
+  idx, tgt = ctx.records_get()
+  ctx.store_reset(n)
+  ctx.store_append()
+  ent = ctx.store_read()
+  m = Hg2vModel(plg.N + 1, plg.E + 1, d, 5, _hgx.LOSS_MSE, _hgx.ACT_RELU,
+                ctx=ctx, seed=41)
+  losses = m.fit_store(n // 6, epochs=2, min_delta=-1e30, seed=9)
+  assert m.records_per_epoch == n and len(m.chunk_stats) >= 12
+  st = m.get_weights()
+  eseeds = [int(np.random.RandomState([9, ep]).randint(0, 2**62, dtype=np.int64))
+            for ep in range(2)]
+  perms = np.stack([epoch_order(ent, es) for es in eseeds])
+  ctx.records_set(idx, tgt)
+  ctx.model_init(d, plg.N + 1, plg.E + 1, seed=41)
+  rl = ctx.train(batch=256, max_epochs=2, loss=_hgx.LOSS_MSE, act=_hgx.ACT_RELU,
+                 perms=perms, min_delta=-1e30)
+  res = ctx.model_get()
+  assert np.array_equal(st[0], res[0]) and np.array_equal(st[1], res[1])
+  assert np.allclose(losses, rl, rtol=1e-6), (losses, rl)
+
+
+def test_store_order_is_independent_of_the_store_layout(ctx, plg):
+  """Entries appended in another order (two row classes, then reversed via
+  store_write) load as the same epoch."""
+  from hypergraphembedding_amd.hg2v_sample import row_class_quota
+  inc = plg
+  _hobe(ctx, inc)
+  full = (np.full(inc.N, 20, np.int32), np.full(inc.E, 20, np.int32))
+  ctx.store_reset(0)
+  for c in (1, 0):
+    ctx.sample_hobe(17, 5, 20, *(row_class_quota(q, c, 2) for q in full))
+    ctx.store_append()
+  n, fam, K, seed = ctx.store_info()
+  a = _load_all(ctx, 77, n // 3)[2]
+  ent = ctx.store_read()
+  ctx.store_reset(n)
+  ctx.store_write(ent[::-1].copy(), fam, K, seed)
+  b = _load_all(ctx, 77, n // 3)[2]
+  for (ia, ta), (ib, tb) in zip(a, b):
+    assert np.array_equal(ia, ib) and np.array_equal(ta, tb)
+  # one resident sample of all rows packs the same multiset of entries
+  assert ctx.sample_hobe(17, 5, 20) == n
+  ctx.store_reset(n)
+  ctx.store_append()
+  assert np.array_equal(np.sort(entry_keys(ctx.store_read(), 1)),
+                        np.sort(entry_keys(ent, 1)))
+
+
+def test_store_refuses_foreign_streams(ctx, plg):
+  from hypergraphembedding_amd import _hgx
+  _hobe(ctx, plg)
+  ctx.store_reset(0)
+  ctx.store_append()
+  idx, tgt = ctx.records_get()
+  ctx.records_set(idx[:1000], tgt[:1000])  # not a sampler stream
+  with pytest.raises(_hgx.HgxError):
+    ctx.store_append()
+  q = np.full(plg.N, 3, np.int32)
+  ctx.sample_fobe(5, 5, q, np.full(plg.E, 3, np.int32))
+  with pytest.raises(AssertionError):  # FOBE records into a HOBE store
+    ctx.store_append()
+  assert ctx.store_info()[0] > 0
+  ctx.upload(plg)
+  assert ctx.store_info()[0] == 0  # upload empties it: it named the old rows
+  with pytest.raises(AssertionError):
+    ctx.store_write(np.array([[9 << 28, 0, 0]], np.uint32), 1, 5, 1)
+
+
+def test_embed_takes_the_store_path(plg):
+  """EmbedHg2vAlgDist / EmbedHg2vBoolean with a record budget below the
+  stream: sampled once into the store (strided row classes), trained in
+  global-shuffle epochs; every record trained once per epoch; the
+  embedding covers every node and edge; the loss falls."""
+  from hypergraphembedding_amd import embedding
+  from hypergraphembedding_amd.runtime import get_context
+  np.random.seed(3)
+  emb = embedding.EmbedHg2vAlgDist(plg, 16, num_samples=20, epochs=3,
+                                   records_budget=200_000)
+  c = get_context()
+  n_store = c.store_info()[0]
+  assert n_store > 600_000
+  assert len(emb.node) == plg.N and len(emb.edge) == plg.E
+  np.random.seed(4)
+  emb = embedding.EmbedHg2vBoolean(plg, 16, num_samples=10, epochs=2,
+                                   records_budget=100_000)
+  assert c.store_info()[1] == 0 and c.store_info()[0] > 300_000
+  assert len(emb.node) == plg.N

@@ -152,15 +152,15 @@ def test_sharded_compact_exchange_local_edges(tmp_path):
   assert np.abs(x - xr).max() <= 1e-4
 
 
-# ---- row-sharded sampling in row-range chunks (fit_streaming) --------------
+# ---- row-sharded sampling into the record store (sharded_store_fill) --------
 def _chunks(inc, n):
   from hypergraphembedding_amd.embedding import _row_chunks
-  per_row = 40
+  per_row = 12
   budget = -(-per_row * (inc.N + inc.E) // n)
-  return _row_chunks(inc, per_row, budget)
+  return _row_chunks(np.full(inc.N, per_row), np.full(inc.E, per_row), budget)
 
 
-def _chunk_worker(rank, world, port, out_path, n_chunks):
+def _store_worker(rank, world, port, out_path, n_chunks):
   import torch.distributed as dist
   root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
   sys.path[:0] = [root, os.path.join(root, "oracle"),
@@ -168,56 +168,65 @@ def _chunk_worker(rank, world, port, out_path, n_chunks):
   from conftest import golden_incidence as gi
   from shard_emu import SampleEmu
   from test_sharded_cpu import _chunks
-  from hypergraphembedding_amd.hg2v_sample import sharded_chunk_fn
+  from hypergraphembedding_amd.hg2v_sample import sharded_store_fill
   os.environ["MASTER_ADDR"] = "127.0.0.1"
   os.environ["MASTER_PORT"] = str(port)
   dist.init_process_group("gloo", rank=rank, world_size=world)
   inc = gi("csr_small.npz")
   emu = SampleEmu()
   emu.upload(inc)
-  chunks = _chunks(inc, n_chunks)
-  fn = sharded_chunk_fn(inc, 3, 6, chunks, ctx=emu, seed=77, kind="hobe",
-                        device="cpu")
-  out = {}
-  for c in (2, 0, 1):  # any chunk order (fit_streaming shuffles it)
-    n = fn(c)
-    idx, tgt = emu.records_get()
-    assert idx.shape[0] == n
-    out[f"idx{c}"], out[f"tgt{c}"] = idx, tgt
-  np.savez(out_path + f".{rank}.npz", **out)
+  n = sharded_store_fill(inc, 3, 6, _chunks(inc, n_chunks), ctx=emu, seed=77,
+                         kind="hobe", device="cpu")
+  assert n == emu.store_info()[0]
+  np.savez(out_path + f".{rank}.npz", store=emu.store_read())
   dist.barrier()
   dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_chunked_sharded_sampling_equals_single_process(tmp_path, world):
-  """Strided row chunks sampled over gloo ranks (each rank a strided share
-  of the chunk's rows) and all-gathered: every rank holds, chunk by chunk,
-  exactly the stream (ids, neighbour lists, targets, kind-block order, rows
-  in order inside each block) a single process samples for that chunk's
-  rows -- so a replica never holds more than one chunk."""
+def test_sharded_store_fill_equals_single_process(tmp_path, world):
+  """Strided row classes sampled over gloo ranks (each rank a strided share
+  of each class's rows), each class's store entries all-gathered while the
+  next class samples: every rank's record store holds exactly the entries
+  a single process stores for the whole stream (as a multiset: the store's
+  epoch order is keyed by record identity, not position)."""
   import torch.multiprocessing as mp
   sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
   from shard_emu import SampleEmu
-  out = str(tmp_path / "chunk")
-  mp.start_processes(_chunk_worker, args=(world, _free_port(), out, 3),
+  out = str(tmp_path / "store")
+  mp.start_processes(_store_worker, args=(world, _free_port(), out, 3),
                      nprocs=world, join=True, start_method="spawn")
   inc = golden_incidence("csr_small.npz")
-  chunks = _chunks(inc, 3)
-  assert len(chunks) == 3
+  assert len(_chunks(inc, 3)) >= 3
   emu = SampleEmu()
   emu.upload(inc)
-  seen = 0
-  from hypergraphembedding_amd.hg2v_sample import row_class_quota
-  for c, (off, stride) in enumerate(chunks):
-    assert (off, stride) == (c, 3)
-    nq = row_class_quota(np.full(inc.N, 6, np.int32), off, stride)
-    eq = row_class_quota(np.full(inc.E, 6, np.int32), off, stride)
-    n = emu.sample_hobe(77, 3, 6, node_q=nq, edge_q=eq)
-    ridx, rtgt = emu.records_get()
-    seen += n
-    for r in range(world):
-      d = np.load(out + f".{r}.npz")
-      assert np.array_equal(d[f"idx{c}"], ridx), (c, r)
-      assert np.array_equal(d[f"tgt{c}"], rtgt), (c, r)
-  assert seen == emu.sample_hobe(77, 3, 6)  # the chunks tile the stream
+  emu.sample_hobe(77, 3, 6)
+  emu.store_reset()
+  emu.store_append()
+  ref = emu.store_read()
+  key = lambda e: np.sort(e[:, 0].astype(np.uint64) << np.uint64(32) |
+                          e[:, 1].astype(np.uint64))
+  for r in range(world):
+    st = np.load(out + f".{r}.npz")["store"]
+    assert st.shape == ref.shape
+    assert np.array_equal(key(st), key(ref))
+    o1 = np.lexsort(st.T[::-1])
+    o2 = np.lexsort(ref.T[::-1])
+    assert np.array_equal(st[o1], ref[o2])
+
+
+def test_row_chunks_respect_per_row_bounds():
+  """the strided classes are sized from the rows' actual
+  bounds: a class holding the heavy-quota rows stays within the budget."""
+  from hypergraphembedding_amd.embedding import _row_chunks
+  bn = np.full(1000, 2, np.int64)
+  bn[::50] = 400  # 20 heavy rows, all in class 0 of a stride of 2, 5, 10, 25, 50
+  be = np.full(300, 2, np.int64)
+  budget = 1000
+  chunks = _row_chunks(bn, be, budget)
+  n = chunks[0][1]
+  cls = (np.bincount(np.arange(bn.size) % n, weights=bn, minlength=n) +
+         np.bincount(np.arange(be.size) % n, weights=be, minlength=n))
+  assert cls.max() <= budget
+  assert [c for c, _ in chunks] == list(range(n))
+  assert n > -(-int(bn.sum() + be.sum()) // budget)  # the even split was not
