@@ -93,6 +93,7 @@ void block_table(const hgx_ctx *ctx, int family, BlockTab &t) {
 
 struct Csr4 {
   const int *rp_n, *col_n, *rp_e, *col_e;
+  int N, E;
 };
 
 // (row, column) of record ri of kind `kind`, from its +1 shifted ids
@@ -106,13 +107,20 @@ __device__ __forceinline__ void row_col(const int *ri, int kind, int &row, int &
 }
 
 // The trainer record of stored entry (w0, w1, w2): ids (+1 shifted, 0 =
-// absent) into ri[0, 4 + 2K), targets into tg[0, 3). Returns false if a
-// node-edge endpoint has no neighbours (the sampler refuses those).
+// absent) at id positions [0, 4 + 2K), targets [0, 3). CHECK = false:
+// written to ri / tg; CHECK = true: compared with the record at ri / tg
+// (hgx_store_append's lossless check), `same` cleared on a difference.
+// Returns false for an entry naming rows outside the graph or a node-edge
+// endpoint without neighbours (the sampler refuses those): nothing is then
+// read from the incidence.
+template <bool CHECK>
 __device__ __forceinline__ bool expand_one(uint32_t w0, uint32_t w1, uint32_t w2,
                                            const BlockTab &t, int K, uint64_t seed,
-                                           const Csr4 &g, int *ri, float *tg) {
+                                           const Csr4 &g, int *ri, float *tg,
+                                           bool &same) {
   const int b = (int)(w0 >> kRowBits);
   const int row = (int)(w0 & kRowMask);
+  if (b >= t.nb) return false;
   const int kind = t.kind[b];
   int col;
   if (t.neg[b]) {  // emit_negatives' column: keyed by (row, rank in row)
@@ -122,44 +130,73 @@ __device__ __forceinline__ bool expand_one(uint32_t w0, uint32_t w1, uint32_t w2
   } else {
     col = (int)w1;
   }
-  for (int s = 0; s < 4 + 2 * K; s++) ri[s] = 0;
-  tg[0] = tg[1] = tg[2] = 0.f;
+  const bool node_row = kind == REC_NN || kind == REC_NE_NODE;
+  const bool node_col = kind == REC_NN || kind == REC_NE_EDGE;
+  if (row >= (node_row ? g.N : g.E) || col < 0 || col >= (node_col ? g.N : g.E))
+    return false;
+  const int R = 4 + 2 * K;
+  int id[4] = {0, 0, 0, 0};
+  float tv[3] = {0.f, 0.f, 0.f};
   const float p = __uint_as_float(w2);
+  int v = 0, e = 0;
   if (kind == REC_NN) {
-    ri[0] = row + 1;
-    ri[2] = col + 1;
-    tg[0] = p;
+    id[0] = row + 1;
+    id[2] = col + 1;
+    tv[0] = p;
+  } else if (kind == REC_EE) {
+    id[1] = row + 1;
+    id[3] = col + 1;
+    tv[1] = p;
+  } else {
+    v = kind == REC_NE_NODE ? row : col;
+    e = kind == REC_NE_NODE ? col : row;
+    id[0] = v + 1;
+    id[3] = e + 1;
+    tv[2] = p;
+  }
+  if (CHECK) {
+    for (int s = 0; s < 4; s++) same = same && ri[s] == id[s];
+    for (int s = 0; s < 3; s++)
+      same = same && __float_as_uint(tg[s]) == __float_as_uint(tv[s]);
+  } else {
+    for (int s = 0; s < 4; s++) ri[s] = id[s];
+    for (int s = 0; s < 3; s++) tg[s] = tv[s];
+  }
+  if (kind == REC_NN || kind == REC_EE) {
+    for (int s = 4; s < R; s++) {
+      if (CHECK) same = same && ri[s] == 0;
+      else ri[s] = 0;
+    }
     return true;
   }
-  if (kind == REC_EE) {
-    ri[1] = row + 1;
-    ri[3] = col + 1;
-    tg[1] = p;
-    return true;
-  }
-  const int v = kind == REC_NE_NODE ? row : col;
-  const int e = kind == REC_NE_NODE ? col : row;
-  ri[0] = v + 1;
-  ri[3] = e + 1;
-  tg[2] = p;
   const int nb = g.rp_e[e], nl = g.rp_e[e + 1] - nb;
   const int eb = g.rp_n[v], el = g.rp_n[v + 1] - eb;
-  if (nl == 0 || el == 0) return false;
-  hgx::draw_record_neighbors(seed, t.nbr_stream[b], row,
-                             t.neg[b] ? (uint64_t)w1 : (uint64_t)col, K, nb, nl,
-                             eb, el, g.col_e, g.col_n, ri + 4);
+  if (nl <= 0 || el <= 0) return false;
+  // hgx::draw_record_neighbors, one neighbour at a time
+  const uint64_t rk = hgx::rand64_key(seed, ((uint64_t)t.nbr_stream[b] << 32) | (uint32_t)row);
+  const uint64_t key = t.neg[b] ? (uint64_t)w1 : (uint64_t)col;
+  for (int k = 0; k < K; k++) {
+    const uint64_t h = hgx::mix64(rk + key * 64 + k);
+    const uint64_t h2 = hgx::mix64(rk + key * 64 + 32 + k);
+    const int a = g.col_e[nb + hgx::bounded(h, (uint32_t)nl)] + 1;
+    const int c = g.col_n[eb + hgx::bounded(h2, (uint32_t)el)] + 1;
+    if (CHECK) {
+      same = same && ri[4 + k] == a && ri[4 + K + k] == c;
+    } else {
+      ri[4 + k] = a;
+      ri[4 + K + k] = c;
+    }
+  }
   return true;
 }
 
 // Pack records [0, n) of the sampler's stream (kind blocks t.bound) into
-// out[3 * (base + i)], checking that each reloads bit for bit. err bits:
-// 1 a record does not reload as sampled, 2 a row id past 2^28.
+// out[3 * i], checking that each reloads bit for bit. err bits: 1 a record
+// does not reload as sampled, 2 a row id past 2^28.
 __global__ void store_pack(const int *idx, const float *tgt, int64_t n, int K,
                            BlockTab t, Csr4 g, uint64_t seed, uint32_t *out,
                            int *err) {
   const int R = 4 + 2 * K;
-  int ri2[36];
-  float tg2[3];
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     int b = 0;
@@ -198,12 +235,10 @@ __global__ void store_pack(const int *idx, const float *tgt, int64_t n, int K,
     const uint32_t w0 = ((uint32_t)b << kRowBits) | ((uint32_t)row & kRowMask);
     const uint32_t w2 = __float_as_uint(p);
     if (!bad) {
-      const bool ok = expand_one(w0, w1, w2, t, K, seed, g, ri2, tg2);
-      bool same = ok;
-      for (int s = 0; s < R; s++) same = same && ri2[s] == ri[s];
-      for (int s = 0; s < 3; s++)
-        same = same && __float_as_uint(tg2[s]) == __float_as_uint(tgt[i * 3 + s]);
-      if (!same) bad = 1;
+      bool same = true;
+      const bool ok = expand_one<true>(w0, w1, w2, t, K, seed, g, const_cast<int *>(ri),
+                                       const_cast<float *>(tgt + i * 3), same);
+      if (!ok || !same) bad = 1;
     }
     uint32_t *o = out + 3 * i;
     o[0] = w0;
@@ -283,8 +318,9 @@ __global__ void store_expand(const uint32_t *sel, const int *order, int64_t m,
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m;
        i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t *c = sel + 3 * (int64_t)order[i];
-    if (!expand_one(c[0], c[1], c[2], t, K, seed, g, idx + (off + i) * R,
-                    tgt + (off + i) * 3))
+    bool same = true;
+    if (!expand_one<false>(c[0], c[1], c[2], t, K, seed, g, idx + (off + i) * R,
+                           tgt + (off + i) * 3, same))
       atomicOr(err, 1);
   }
 }
@@ -296,7 +332,7 @@ int grid_for(int64_t work, int per_block, int cap = 8192) {
 
 Csr4 csr_of(const hgx_ctx *ctx) {
   return Csr4{ctx->rp_n.as<int>(), ctx->col_n.as<int>(), ctx->rp_e.as<int>(),
-              ctx->col_e.as<int>()};
+              ctx->col_e.as<int>(), ctx->N, ctx->E};
 }
 
 // the store's capacity grown to `cap` records, keeping its contents
@@ -605,7 +641,8 @@ extern "C" int hgx_store_load(hgx_ctx *ctx, uint64_t epoch_seed, int32_t bin_lo,
   HGX_CHECK(ctx, (int64_t)(got[0]) == m || m == 0, HGX_EHIP,
             "store selection found %llu of %lld records", got[0], (long long)m);
   HGX_CHECK(ctx, (got[1] & 0xffffffffull) == 0, HGX_EVALUE,
-            "a stored node-edge record has an endpoint without neighbours");
+            "a stored record names rows outside the graph or a node-edge "
+            "endpoint without neighbours");
   // 4. whole batches now; the tail waits for the next load unless last
   const int64_t keep = last ? 0 : total % batch;
   ctx->n_rec = total - keep;

@@ -18,6 +18,9 @@ def per_kernel(path, counter):
     for key in ("train_fwd_bwd", "train_update", "train_step", "train_flush"):
       if key in name:
         vals.setdefault(key, []).append(float(r["Counter_Value"]))
+        if key == "train_step":  # the light / MULTI pending-slot forms
+          form = "train_step[MULTI]" if "true>" in name else "train_step[plain]"
+          vals.setdefault(form, []).append(float(r["Counter_Value"]))
   return {k: float(np.mean(v)) for k, v in vals.items()}, \
       {k: len(v) for k, v in vals.items()}
 
@@ -28,7 +31,7 @@ w, nw = per_kernel(write_csv, "WRITE_SIZE")
 # once per epoch (and before a restart), so it is averaged over batches
 steps = max(nf.get("train_step", 0) + nf.get("train_fwd_bwd", 0), 1)
 def per_step(vals, counts):
-  return sum(vals[k] * counts[k] for k in vals) / steps
+  return sum(vals[k] * counts[k] for k in vals if "[" not in k) / steps
 hbm = 1024 * (2 * per_step(f, nf) + per_step(w, nw))
 alg = 256 * (224 * d + 68)
 res = {
@@ -37,7 +40,7 @@ res = {
                 "--pmc WRITE_SIZE (pass 2) --output-format csv -- python3 "
                 + (sys.argv[6] if len(sys.argv) > 6 else
                    "bench.py --steps 1 --warmup 0 --no-cpu --no-c4 --no-extra")),
-    "note": ("Per batch of 256 records at d=%d on 100k/50k-row tables, summed over "
+    "note": ("Per batch of 256 records at d=%d, summed over "
              "the per-batch kernels (train_step, or train_fwd_bwd + train_update, and the "
              "deferred-row flush once per epoch), per batch step. FETCH_SIZE / "
              "WRITE_SIZE are KB; gfx950 correction: FETCH doubled (wide 16-B-per-"
@@ -49,5 +52,9 @@ res = {
     "hbm_bytes_per_batch": int(round(hbm)),
     "algorithmic_bytes_per_batch": alg,
 }
+forms = {k: int(round(1024 * (2 * f[k] + w.get(k, 0.0))))
+         for k in f if k.startswith("train_step[")}
+if forms:
+  res["hbm_bytes_per_batch_by_form"] = forms
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
