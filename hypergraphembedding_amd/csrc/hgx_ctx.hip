@@ -261,6 +261,7 @@ extern "C" int hgx_upload_incidence(hgx_ctx *ctx, int32_t N, int32_t E,
   ctx->smp_family = -1;
   ctx->rec_in_order = false;
   ctx->n_store = 0;  // stored records name rows of the previous incidence
+  ctx->st_hist_ok = false;
   ctx->store_family = -1;
   ctx->features_ok = ctx->centroids_ok = false;
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "hgx.h"
 
@@ -172,6 +173,11 @@ struct hgx_ctx {
   // records of the last hgx_store_load past ctx->n_rec: the batch tail the
   // next load puts first
   int64_t store_carry = 0;
+  // the last hgx_store_plan's key histogram (host copy) and its epoch seed:
+  // hgx_store_load of that epoch reads its chunk sizes from it
+  std::vector<unsigned> st_hist_host;
+  uint64_t st_hist_seed = 0;
+  bool st_hist_ok = false;
   DevBuf st_sel, st_keys, st_vals, st_tmp, st_hist;  // hgx_store_load scratch
 
   // ---- model ----

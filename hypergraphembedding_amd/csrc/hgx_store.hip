@@ -53,6 +53,10 @@ static_assert(kBins == HGX_STORE_BINS, "bin count");
 struct BlockTab {
   int nb;
   int kind[kMaxBlocks];
+  // id columns of the row and of the column, the target column, whether
+  // row / column index nodes (all from `kind`, precomputed on the host)
+  int rpos[kMaxBlocks], cpos[kMaxBlocks], tpos[kMaxBlocks];
+  int rnode[kMaxBlocks], cnode[kMaxBlocks];
   int neg[kMaxBlocks];
   int ncols[kMaxBlocks];            // negatives: columns of the draw
   uint32_t col_stream[kMaxBlocks];  // negatives: emit_negatives stream
@@ -65,7 +69,14 @@ struct BlockTab {
 void block_table(const hgx_ctx *ctx, int family, BlockTab &t) {
   memset(&t, 0, sizeof(t));
   auto set = [&](int b, int kind, int neg, int ncols, uint32_t cs, uint32_t ns) {
+    static const int rp[4] = {0, 1, 0, 3}, cp[4] = {2, 3, 3, 0}, tp[4] = {0, 1, 2, 2};
+    static const int rn[4] = {1, 0, 1, 0}, cn[4] = {1, 0, 0, 1};
     t.kind[b] = kind;
+    t.rpos[b] = rp[kind];
+    t.cpos[b] = cp[kind];
+    t.tpos[b] = tp[kind];
+    t.rnode[b] = rn[kind];
+    t.cnode[b] = cn[kind];
     t.neg[b] = neg;
     t.ncols[b] = ncols;
     t.col_stream[b] = cs;
@@ -96,92 +107,75 @@ struct Csr4 {
   int N, E;
 };
 
-// (row, column) of record ri of kind `kind`, from its +1 shifted ids
-__device__ __forceinline__ void row_col(const int *ri, int kind, int &row, int &col) {
-  switch (kind) {
-    case REC_NN: row = ri[0] - 1; col = ri[2] - 1; break;
-    case REC_EE: row = ri[1] - 1; col = ri[3] - 1; break;
-    case REC_NE_NODE: row = ri[0] - 1; col = ri[3] - 1; break;
-    default: row = ri[3] - 1; col = ri[0] - 1; break;
-  }
-}
-
 // The trainer record of stored entry (w0, w1, w2): ids (+1 shifted, 0 =
 // absent) at id positions [0, 4 + 2K), targets [0, 3). CHECK = false:
 // written to ri / tg; CHECK = true: compared with the record at ri / tg
-// (hgx_store_append's lossless check), `same` cleared on a difference.
-// Returns false for an entry naming rows outside the graph or a node-edge
-// endpoint without neighbours (the sampler refuses those): nothing is then
-// read from the incidence.
+// (hgx_store_append's lossless check): diff gets 4 (ids), 8 (targets), 16
+// (neighbours) for a difference. Returns false for an entry naming rows
+// outside the graph or a node-edge endpoint without neighbours (the
+// sampler refuses those): nothing is then read from the incidence.
 template <bool CHECK>
 __device__ __forceinline__ bool expand_one(uint32_t w0, uint32_t w1, uint32_t w2,
                                            const BlockTab &t, int K, uint64_t seed,
                                            const Csr4 &g, int *ri, float *tg,
-                                           bool &same) {
+                                           int &diff) {
   const int b = (int)(w0 >> kRowBits);
-  const int row = (int)(w0 & kRowMask);
   if (b >= t.nb) return false;
-  const int kind = t.kind[b];
-  int col;
-  if (t.neg[b]) {  // emit_negatives' column: keyed by (row, rank in row)
-    col = (int)hgx::bounded(
-        hgx::rand64(seed, t.col_stream[b], ((uint64_t)row << 32) | w1),
-        (uint32_t)t.ncols[b]);
-  } else {
-    col = (int)w1;
-  }
-  const bool node_row = kind == REC_NN || kind == REC_NE_NODE;
-  const bool node_col = kind == REC_NN || kind == REC_NE_EDGE;
-  if (row >= (node_row ? g.N : g.E) || col < 0 || col >= (node_col ? g.N : g.E))
+  const int row = (int)(w0 & kRowMask);
+  const int neg = t.neg[b], rpos = t.rpos[b], cpos = t.cpos[b], tpos = t.tpos[b];
+  const int rnode = t.rnode[b], cnode = t.cnode[b];
+  const int col = neg ? (int)hgx::bounded(  // emit_negatives' keyed column
+                            hgx::rand64(seed, t.col_stream[b],
+                                        ((uint64_t)row << 32) | w1),
+                            (uint32_t)t.ncols[b])
+                      : (int)w1;
+  if (row >= (rnode ? g.N : g.E) || col < 0 || col >= (cnode ? g.N : g.E))
     return false;
   const int R = 4 + 2 * K;
-  int id[4] = {0, 0, 0, 0};
-  float tv[3] = {0.f, 0.f, 0.f};
+  const bool ne = t.kind[b] >= REC_NE_NODE;
+  for (int s = 0; s < 4; s++) {
+    const int want = s == rpos ? row + 1 : s == cpos ? col + 1 : 0;
+    if (CHECK) {
+      if (ri[s] != want) diff |= 4;
+    } else {
+      ri[s] = want;
+    }
+  }
   const float p = __uint_as_float(w2);
-  int v = 0, e = 0;
-  if (kind == REC_NN) {
-    id[0] = row + 1;
-    id[2] = col + 1;
-    tv[0] = p;
-  } else if (kind == REC_EE) {
-    id[1] = row + 1;
-    id[3] = col + 1;
-    tv[1] = p;
-  } else {
-    v = kind == REC_NE_NODE ? row : col;
-    e = kind == REC_NE_NODE ? col : row;
-    id[0] = v + 1;
-    id[3] = e + 1;
-    tv[2] = p;
+  for (int s = 0; s < 3; s++) {
+    const float want = s == tpos ? p : 0.f;
+    if (CHECK) {
+      if (__float_as_uint(tg[s]) != __float_as_uint(want)) diff |= 8;
+    } else {
+      tg[s] = want;
+    }
   }
-  if (CHECK) {
-    for (int s = 0; s < 4; s++) same = same && ri[s] == id[s];
-    for (int s = 0; s < 3; s++)
-      same = same && __float_as_uint(tg[s]) == __float_as_uint(tv[s]);
-  } else {
-    for (int s = 0; s < 4; s++) ri[s] = id[s];
-    for (int s = 0; s < 3; s++) tg[s] = tv[s];
-  }
-  if (kind == REC_NN || kind == REC_EE) {
+  if (!ne) {
     for (int s = 4; s < R; s++) {
-      if (CHECK) same = same && ri[s] == 0;
-      else ri[s] = 0;
+      if (CHECK) {
+        if (ri[s] != 0) diff |= 16;
+      } else {
+        ri[s] = 0;
+      }
     }
     return true;
   }
+  const int v = rnode ? row : col;
+  const int e = rnode ? col : row;
   const int nb = g.rp_e[e], nl = g.rp_e[e + 1] - nb;
   const int eb = g.rp_n[v], el = g.rp_n[v + 1] - eb;
   if (nl <= 0 || el <= 0) return false;
   // hgx::draw_record_neighbors, one neighbour at a time
-  const uint64_t rk = hgx::rand64_key(seed, ((uint64_t)t.nbr_stream[b] << 32) | (uint32_t)row);
-  const uint64_t key = t.neg[b] ? (uint64_t)w1 : (uint64_t)col;
+  const uint64_t rk =
+      hgx::rand64_key(seed, ((uint64_t)t.nbr_stream[b] << 32) | (uint32_t)row);
+  const uint64_t key = neg ? (uint64_t)w1 : (uint64_t)col;
   for (int k = 0; k < K; k++) {
     const uint64_t h = hgx::mix64(rk + key * 64 + k);
     const uint64_t h2 = hgx::mix64(rk + key * 64 + 32 + k);
     const int a = g.col_e[nb + hgx::bounded(h, (uint32_t)nl)] + 1;
     const int c = g.col_n[eb + hgx::bounded(h2, (uint32_t)el)] + 1;
     if (CHECK) {
-      same = same && ri[4 + k] == a && ri[4 + K + k] == c;
+      if (ri[4 + k] != a || ri[4 + K + k] != c) diff |= 16;
     } else {
       ri[4 + k] = a;
       ri[4 + K + k] = c;
@@ -192,7 +186,9 @@ __device__ __forceinline__ bool expand_one(uint32_t w0, uint32_t w1, uint32_t w2
 
 // Pack records [0, n) of the sampler's stream (kind blocks t.bound) into
 // out[3 * i], checking that each reloads bit for bit. err bits: 1 a record
-// does not reload as sampled, 2 a row id past 2^28.
+// does not reload as sampled (4 ids, 8 targets, 16 neighbours differ, 32
+// rows outside the graph; 64 << block: the blocks concerned), 2 a row id
+// past 2^28.
 __global__ void store_pack(const int *idx, const float *tgt, int64_t n, int K,
                            BlockTab t, Csr4 g, uint64_t seed, uint32_t *out,
                            int *err) {
@@ -200,12 +196,11 @@ __global__ void store_pack(const int *idx, const float *tgt, int64_t n, int K,
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     int b = 0;
-    while (b + 1 < t.nb && i >= t.bound[b + 1]) b++;
+    for (int q = 1; q < t.nb; q++) b += i >= t.bound[q] ? 1 : 0;
     const int *ri = idx + i * R;
-    const int kind = t.kind[b];
-    int row, col;
-    row_col(ri, kind, row, col);
-    const float p = tgt[i * 3 + (kind == REC_NN ? 0 : kind == REC_EE ? 1 : 2)];
+    const int rpos = t.rpos[b], cpos = t.cpos[b];
+    const int row = ri[rpos] - 1, col = ri[cpos] - 1;
+    const float p = tgt[i * 3 + t.tpos[b]];
     int bad = row < 0 || (uint32_t)row > kRowMask ? 2 : 0;
     uint32_t w1 = (uint32_t)col;
     if (t.neg[b] && !bad) {
@@ -214,9 +209,7 @@ __global__ void store_pack(const int *idx, const float *tgt, int64_t n, int K,
       const int64_t b0 = t.bound[b];
       int64_t good = i, step = 1, lo = b0 - 1;
       while (good - step >= b0) {
-        int r2, c2;
-        row_col(idx + (good - step) * R, kind, r2, c2);
-        if (r2 != row) {
+        if (idx[(good - step) * R + rpos] - 1 != row) {
           lo = good - step;
           break;
         }
@@ -225,9 +218,7 @@ __global__ void store_pack(const int *idx, const float *tgt, int64_t n, int K,
       }
       while (good - lo > 1) {
         const int64_t mid = lo + (good - lo) / 2;
-        int r2, c2;
-        row_col(idx + mid * R, kind, r2, c2);
-        if (r2 == row) good = mid;
+        if (idx[mid * R + rpos] - 1 == row) good = mid;
         else lo = mid;
       }
       w1 = (uint32_t)(i - good);
@@ -235,10 +226,20 @@ __global__ void store_pack(const int *idx, const float *tgt, int64_t n, int K,
     const uint32_t w0 = ((uint32_t)b << kRowBits) | ((uint32_t)row & kRowMask);
     const uint32_t w2 = __float_as_uint(p);
     if (!bad) {
-      bool same = true;
+      int diff = 0;
       const bool ok = expand_one<true>(w0, w1, w2, t, K, seed, g, const_cast<int *>(ri),
-                                       const_cast<float *>(tgt + i * 3), same);
-      if (!ok || !same) bad = 1;
+                                       const_cast<float *>(tgt + i * 3), diff);
+      if (!ok) diff |= 32;
+      if (diff) {
+        bad = 1 | diff | (64 << b);
+        // the first mismatching record, for the error message
+        if (atomicCAS(err + 1, 0, 1) == 0) {
+          err[2] = (int)i;
+          err[3] = b;
+          err[4] = row;
+          err[5] = col;
+        }
+      }
     }
     uint32_t *o = out + 3 * i;
     o[0] = w0;
@@ -318,9 +319,9 @@ __global__ void store_expand(const uint32_t *sel, const int *order, int64_t m,
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m;
        i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t *c = sel + 3 * (int64_t)order[i];
-    bool same = true;
+    int diff = 0;
     if (!expand_one<false>(c[0], c[1], c[2], t, K, seed, g, idx + (off + i) * R,
-                           tgt + (off + i) * 3, same))
+                           tgt + (off + i) * 3, diff))
       atomicOr(err, 1);
   }
 }
@@ -366,6 +367,7 @@ extern "C" int hgx_store_reset(hgx_ctx *ctx, int64_t capacity) {
   ctx->store_K = 0;
   ctx->store_seed = 0;
   ctx->store_carry = 0;
+  ctx->st_hist_ok = false;
   if (capacity > ctx->cap_store) {
     hgx_release(ctx->store);  // nothing to keep
     ctx->cap_store = 0;
@@ -417,21 +419,25 @@ extern "C" int hgx_store_append(hgx_ctx *ctx) {
   HGX_HIP(ctx, hipSetDevice(ctx->device));
   if (ctx->n_store + n > ctx->cap_store)
     HGX_TRY(store_grow(ctx, std::max(ctx->n_store + n, ctx->cap_store + ctx->cap_store / 4)));
-  HGX_TRY(hgx_ensure(ctx, ctx->s0, 16));
-  HGX_HIP(ctx, hipMemsetAsync(ctx->s0.p, 0, sizeof(int), ctx->stream));
+  HGX_TRY(hgx_ensure(ctx, ctx->s0, 32));
+  HGX_HIP(ctx, hipMemsetAsync(ctx->s0.p, 0, 32, ctx->stream));
   hipLaunchKernelGGL(store_pack, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream,
                      ctx->rec_idx.as<int>(), ctx->rec_tgt.as<float>(), n, K, t,
                      csr_of(ctx), ctx->store_seed,
                      ctx->store.as<uint32_t>() + 3 * ctx->n_store, ctx->s0.as<int>());
   HGX_LAUNCH_CHECK(ctx);
-  int err = 0;
-  HGX_HIP(ctx, hipMemcpyAsync(&err, ctx->s0.p, sizeof(int), hipMemcpyDeviceToHost,
-                              ctx->stream));
+  int ev[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  HGX_HIP(ctx, hipMemcpyAsync(ev, ctx->s0.p, 32, hipMemcpyDeviceToHost, ctx->stream));
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  const int err = ev[0];
   HGX_CHECK(ctx, !(err & 2), HGX_EUNSUP, "a record row id exceeds 2^28");
   HGX_CHECK(ctx, err == 0, HGX_ESTATE,
-            "a sampled record does not reload bit for bit from its stored form");
+            "a sampled record does not reload bit for bit from its stored form "
+            "(mismatch bits 0x%x: 4 ids, 8 targets, 16 neighbours, 32 rows; "
+            "64 << kind block; first: record %d, block %d, row %d, column %d)",
+            err, ev[2], ev[3], ev[4], ev[5]);
   ctx->n_store += n;
+  ctx->st_hist_ok = false;
   return HGX_OK;
 }
 
@@ -500,6 +506,7 @@ extern "C" int hgx_store_write(hgx_ctx *ctx, int64_t n, const void *src,
                               ctx->stream));
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->n_store += n;
+  ctx->st_hist_ok = false;
   return HGX_OK;
 }
 
@@ -518,10 +525,13 @@ extern "C" int hgx_store_plan(hgx_ctx *ctx, uint64_t epoch_seed, int64_t budget,
                      0, ctx->stream, ctx->store.as<uint32_t>(), ctx->n_store, k1, k2,
                      ctx->st_hist.as<unsigned>());
   HGX_LAUNCH_CHECK(ctx);
-  std::vector<unsigned> h(kBins);
+  std::vector<unsigned> &h = ctx->st_hist_host;
+  h.assign(kBins, 0u);
   HGX_HIP(ctx, hipMemcpyAsync(h.data(), ctx->st_hist.p, sizeof(unsigned) * kBins,
                               hipMemcpyDeviceToHost, ctx->stream));
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->st_hist_seed = epoch_seed;
+  ctx->st_hist_ok = true;
   // greedy: consecutive bins while the chunk stays within budget (a bin
   // larger than the budget is a chunk of its own)
   int nc = 0;
@@ -563,18 +573,24 @@ extern "C" int hgx_store_load(hgx_ctx *ctx, uint64_t epoch_seed, int32_t bin_lo,
   // 1. the chunk's entries and their keys
   HGX_TRY(hgx_ensure(ctx, ctx->s0, 16));
   HGX_HIP(ctx, hipMemsetAsync(ctx->s0.p, 0, 16, ctx->stream));
-  // selection capacity: at most the store (sized from a first count pass
-  // would cost a second read of the store; the histogram gives it)
-  HGX_TRY(hgx_ensure(ctx, ctx->st_hist, sizeof(unsigned) * kBins));
-  HGX_HIP(ctx, hipMemsetAsync(ctx->st_hist.p, 0, sizeof(unsigned) * kBins, ctx->stream));
-  hipLaunchKernelGGL(store_hist, dim3(grid_for(ctx->n_store, 1024, 1024)), dim3(1024),
-                     0, ctx->stream, ctx->store.as<uint32_t>(), ctx->n_store, k1, k2,
-                     ctx->st_hist.as<unsigned>());
-  HGX_LAUNCH_CHECK(ctx);
-  std::vector<unsigned> h(kBins);
-  HGX_HIP(ctx, hipMemcpyAsync(h.data(), ctx->st_hist.p, sizeof(unsigned) * kBins,
-                              hipMemcpyDeviceToHost, ctx->stream));
-  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // the chunk's size from the epoch's key histogram (hgx_store_plan's, or
+  // computed here for a load without a plan of this epoch)
+  if (!ctx->st_hist_ok || ctx->st_hist_seed != epoch_seed) {
+    HGX_TRY(hgx_ensure(ctx, ctx->st_hist, sizeof(unsigned) * kBins));
+    HGX_HIP(ctx, hipMemsetAsync(ctx->st_hist.p, 0, sizeof(unsigned) * kBins, ctx->stream));
+    hipLaunchKernelGGL(store_hist, dim3(grid_for(ctx->n_store, 1024, 1024)), dim3(1024),
+                       0, ctx->stream, ctx->store.as<uint32_t>(), ctx->n_store, k1, k2,
+                       ctx->st_hist.as<unsigned>());
+    HGX_LAUNCH_CHECK(ctx);
+    ctx->st_hist_host.assign(kBins, 0u);
+    HGX_HIP(ctx, hipMemcpyAsync(ctx->st_hist_host.data(), ctx->st_hist.p,
+                                sizeof(unsigned) * kBins, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->st_hist_seed = epoch_seed;
+    ctx->st_hist_ok = true;
+  }
+  const std::vector<unsigned> &h = ctx->st_hist_host;
   int64_t m = 0;
   for (int b = bin_lo; b < bin_hi; b++) m += h[b];
   const int64_t carry = ctx->store_carry;
