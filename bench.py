@@ -53,6 +53,8 @@ MFMA_F32_PEAK_TFLOPS = 157.3  # f32-in MFMA = the FP32 vector peak (same guide)
 METRIC = ("training samples/sec + alg-dist SpMV GB/s, HOBE dim=128 at "
           "1/2/4/8 MI355X")
 PMC_TRAIN = os.path.join(ROOT, "profiles", "r04", "final", "pmc_train.json")
+# FETCH/WRITE passes of the C4 d = 256 step (tools/train_d256_pmc_prog.py)
+PMC_TRAIN_D256 = os.path.join(ROOT, "profiles", "r05", "pmc_train_d256.json")
 
 
 def parse():
@@ -604,6 +606,26 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
            "batch_steps": {"train_step": fz4, "train_fwd_bwd+train_update": sp4},
            "multi_pending_batches": ctx.train_multi_pending(),
            "loss": "MSE", "act": "relu"}
+  # roofline of the north-star config's step (d = 256, the power-law
+  # stream: train_step<64,4,5,2,256,{false,true}>, the plain and the MULTI
+  # pending-slot form)
+  b_rec4 = 224.0 * d4 + 68.0
+  pb_us = ms4t * 1e3 / max(bat4, 1)
+  ach4 = b_rec4 * (n4 / max(bat4, 1)) / (pb_us * 1e-6) / 1e9
+  rf4 = {"bound": "hbm", "achieved": round(ach4, 1), "peak": HBM_PEAK_GBPS,
+         "unit": "GB/s", "frac": round(ach4 / HBM_PEAK_GBPS, 4),
+         "per_launch_us": round(pb_us, 2),
+         "algorithmic_bytes_per_launch": round(b_rec4 * n4 / max(bat4, 1)),
+         "traffic": None}
+  if os.path.exists(PMC_TRAIN_D256):
+    with open(PMC_TRAIN_D256) as f:
+      pm4 = json.load(f)
+    rf4["traffic"] = pm4.get("hbm_bytes_per_batch")
+    rf4["traffic_by_form"] = pm4.get("hbm_bytes_per_batch_by_form")
+    rf4["traffic_source"] = os.path.relpath(PMC_TRAIN_D256, ROOT)
+    if "per_form_us" in pm4:
+      rf4["per_form_us"] = pm4["per_form_us"]
+  hobe4["roofline"] = rf4
   # the whole pipeline of this slice on N GPUs: relaxation (20 iterations,
   # node-row sharded at N > 1, plus the node-coordinate all-gather),
   # sampling, one epoch; records/s of ONE embedding (the replicas train the

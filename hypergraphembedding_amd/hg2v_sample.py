@@ -287,7 +287,7 @@ def sharded_store_fill(inc, num_neighbors, num_samples, chunks, ctx=None,
   pending = None  # (handle, recv buffers, per-rank counts) of the last class
 
   def finish(p):
-    work, recv, cnt = p
+    work, recv, cnt, _send = p
     work.wait()
     if gpu:
       torch.cuda.current_stream(dev).synchronize()
@@ -332,7 +332,7 @@ def sharded_store_fill(inc, num_neighbors, num_samples, chunks, ctx=None,
         send[:new] = torch.from_numpy(ctx.store_read(before, new).view(np.int32))
     recv = [torch.empty_like(send) for _ in range(world)]
     work = dist.all_gather(recv, send, group=group, async_op=True)
-    pending = (work, recv, cnt)
+    pending = (work, recv, cnt, send)  # buffers live until the gather ends
   if pending is not None:
     finish(pending)
   if gpu:
