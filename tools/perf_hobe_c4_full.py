@@ -100,6 +100,15 @@ def main():
     t_chunk[0] = now
     return r
   ctx.train = train
+  orig_load = ctx.store_load
+  load_s = []
+
+  def load(*a, **kw):
+    t = time.perf_counter()
+    r = orig_load(*a, **kw)
+    load_s.append(time.perf_counter() - t)
+    return r
+  ctx.store_load = load
   t3 = time.perf_counter()
   losses = model.fit_store(a.chunk, epochs=a.epochs, min_delta=-1e30, seed=3)
   ctx.synchronize()
@@ -115,6 +124,8 @@ def main():
       per_batch_us=round(batch_ms * 1e3 / max(batches, 1), 2),
       batch_kernel_s=round(batch_ms / 1e3, 2),
       load_overhead_s=round(wall - batch_ms / 1e3, 2),
+      store_load_s=round(sum(load_s), 2),
+      store_load_s_per_chunk=[round(x, 3) for x in load_s],
       chunks_per_epoch=len(cs) // max(len(losses), 1),
       end_to_end_s=round(out["upload_alg_s"] + fill_s + wall, 2))
   free, total = _mem()
