@@ -9,7 +9,9 @@ acc = {}
 for r in csv.DictReader(open(path)):
   if r["Counter_Name"] != counter:
     continue
-  k = r["Kernel_Name"].split("(")[0]
+  k = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+  k = k[5:] if k.startswith("void ") else k
+  k = k.split("(")[0]
   s, n = acc.get(k, (0.0, 0))
   acc[k] = (s + float(r["Counter_Value"]), n + 1)
 res = {k: {"mean": s / n, "launches": n} for k, (s, n) in acc.items()}
