@@ -588,6 +588,21 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
     bat4 = sum(x[4] for x in cs)
     fz4, sp4 = bat4, 0  # train_path_stats of the last chunk only
     t4 = max_over_ranks(t4)
+  else:
+    sync()
+    t = time.perf_counter()
+    n4 = ctx.sample_hobe(4000, K4, S4, node_q=nq4, edge_q=eq4)
+    sync()
+    hobe_sample_s = time.perf_counter() - t
+    rej_rows, fb_rows = ctx.sample_stats()
+    sync()
+    t = time.perf_counter()
+    ctx.train(batch=args.batch, max_epochs=1, loss=_hgx.LOSS_MSE,
+              act=_hgx.ACT_RELU, min_delta=-1e30, shuffle_seed=2)
+    sync()
+    t4 = time.perf_counter() - t
+    ms4t, rec4, bat4 = ctx.train_stats()
+    fz4, sp4 = ctx.train_path_stats()
   hobe4 = {"workload": "HG2V_ALG_DIST (HOBE) dim=256 on the 10M/5M power-law "
                        f"graph, rows sampled: a seeded {args.c4_frac:.0%} of "
                        "node rows and edge rows (quota S=200, K=5), 1 epoch",
