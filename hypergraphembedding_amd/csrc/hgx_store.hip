@@ -272,42 +272,71 @@ __global__ void store_hist(const uint32_t *st, int64_t n, uint64_t k1, uint64_t 
 }
 
 // Records whose key lies in bins [lo, hi): copied to sel (their keys to
-// keys, their positions in sel to vals); one atomic per wave.
-__global__ void store_select(const uint32_t *st, int64_t n, uint64_t k1, uint64_t k2,
-                             uint32_t lo, uint32_t hi, uint32_t *sel,
-                             unsigned long long *keys, int *vals,
-                             unsigned long long *count) {
-  const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t n_up = (n + 63) / 64 * 64;  // every lane of a wave iterates alike
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_up;
-       i += stride) {
-    uint32_t w0 = 0, w1 = 0, w2 = 0;
-    uint64_t key = 0;
-    bool take = false;
-    if (i < n) {
-      w0 = st[3 * i];
-      w1 = st[3 * i + 1];
-      w2 = st[3 * i + 2];
-      key = epoch_key(w0, w1, k1, k2);
-      const uint32_t bin = (uint32_t)(key >> (64 - kBinBits));
-      take = bin >= lo && bin < hi;
+// keys, their positions in sel to vals). Tiles of 256 x kSelItems entries
+// (item j of thread t at tile + j * 256 + t, coalesced), one atomic per
+// tile for the tile's base: a per-wave atomic on the one counter serialised
+// the selection (223 ms for 2^28 of 1.2e9 entries vs 2.6 ms for the
+// histogram pass over the same store). Where a record lands in sel depends
+// on the tiles' atomic order; the load's order does not: the keys are
+// distinct and sorted.
+constexpr int kSelItems = 8;
+__global__ __launch_bounds__(256) void store_select(
+    const uint32_t *st, int64_t n, uint64_t k1, uint64_t k2, uint32_t lo, uint32_t hi,
+    uint32_t *sel, unsigned long long *keys, int *vals, unsigned long long *count) {
+  __shared__ unsigned wave_off[4];
+  __shared__ unsigned long long tile_base;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const unsigned long long below = (1ull << lane) - 1;
+  const int64_t tile = 256 * kSelItems;
+  for (int64_t t0 = blockIdx.x * tile; t0 < n; t0 += (int64_t)gridDim.x * tile) {
+    uint32_t w0[kSelItems], w1[kSelItems], w2[kSelItems];
+    uint64_t key[kSelItems];
+    unsigned long long mask[kSelItems];
+    unsigned wtot = 0;
+#pragma unroll
+    for (int j = 0; j < kSelItems; j++) {
+      const int64_t i = t0 + j * 256 + threadIdx.x;
+      bool take = false;
+      w0[j] = w1[j] = w2[j] = 0;
+      key[j] = 0;
+      if (i < n) {
+        w0[j] = st[3 * i];
+        w1[j] = st[3 * i + 1];
+        w2[j] = st[3 * i + 2];
+        key[j] = epoch_key(w0[j], w1[j], k1, k2);
+        const uint32_t bin = (uint32_t)(key[j] >> (64 - kBinBits));
+        take = bin >= lo && bin < hi;
+      }
+      mask[j] = __ballot(take);
+      wtot += (unsigned)__popcll(mask[j]);
     }
-    const unsigned long long mask = __ballot(take);
-    if (!mask) continue;
-    unsigned long long base = 0;
-    const int leader = __ffsll((long long)mask) - 1;
-    if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(mask));
-    base = __shfl(base, leader);
-    if (take) {
-      const int64_t pos = (int64_t)base + __popcll(mask & ((1ull << lane) - 1));
-      uint32_t *o = sel + 3 * pos;
-      o[0] = w0;
-      o[1] = w1;
-      o[2] = w2;
-      keys[pos] = key;
-      vals[pos] = (int)pos;
+    if (lane == 0) wave_off[wave] = wtot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned run = 0;
+      for (int w = 0; w < 4; w++) {
+        const unsigned c = wave_off[w];
+        wave_off[w] = run;
+        run += c;
+      }
+      tile_base = run ? atomicAdd(count, (unsigned long long)run) : 0ull;
     }
+    __syncthreads();
+    int64_t base = (int64_t)tile_base + wave_off[wave];
+#pragma unroll
+    for (int j = 0; j < kSelItems; j++) {
+      if ((mask[j] >> lane) & 1ull) {
+        const int64_t pos = base + __popcll(mask[j] & below);
+        uint32_t *o = sel + 3 * pos;
+        o[0] = w0[j];
+        o[1] = w1[j];
+        o[2] = w2[j];
+        keys[pos] = key[j];
+        vals[pos] = (int)pos;
+      }
+      base += __popcll(mask[j]);
+    }
+    __syncthreads();  // wave_off / tile_base reused by the next tile
   }
 }
 
@@ -611,7 +640,8 @@ extern "C" int hgx_store_load(hgx_ctx *ctx, uint64_t epoch_seed, int32_t bin_lo,
   vin = ctx->st_vals.as<int>();
   vout = vin + (m + 1);
   if (m > 0) {
-    hipLaunchKernelGGL(store_select, dim3(grid_for(ctx->n_store, 256)), dim3(256), 0,
+    hipLaunchKernelGGL(store_select, dim3(grid_for(ctx->n_store, 256 * kSelItems, 4096)),
+                       dim3(256), 0,
                        ctx->stream, ctx->store.as<uint32_t>(), ctx->n_store, k1, k2,
                        (uint32_t)bin_lo, (uint32_t)bin_hi, ctx->st_sel.as<uint32_t>(),
                        kin, vin, ctx->s0.as<unsigned long long>());
