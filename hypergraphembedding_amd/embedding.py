@@ -157,11 +157,16 @@ def fill_store(ctx, inc, chunk_fn, bound_n, bound_e, budget):
   (_row_chunks) sampled in turn by chunk_fn(offset, stride) (the records of
   that class now on ctx), each packed into the store (hgx_store_append).
   Returns the records stored."""
-  chunks = _row_chunks(bound_n, bound_e, budget)
-  ctx.store_reset(int(np.sum(bound_n, dtype=np.int64) +
-                      np.sum(bound_e, dtype=np.int64)))
+  bn = np.asarray(bound_n, np.int64)
+  be = np.asarray(bound_e, np.int64)
+  chunks = _row_chunks(bn, be, budget)
+  ctx.store_reset(int(bn.sum() + be.sum()))
   for off, stride in chunks:
-    chunk_fn(off, stride)
+    m = chunk_fn(off, stride)
+    cap = int(bn[off::stride].sum() + be[off::stride].sum())
+    assert m is None or m <= cap, (
+        "row class %d/%d sampled %d records, above its bound %d" %
+        (off, stride, m, cap))
     ctx.store_append()
   return ctx.store_info()[0]
 
