@@ -1025,9 +1025,11 @@ int resident_grid(F fn) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+            hipSuccess ||
+        cus <= 0)
+      cus = 256;  // the grid size only: MI355X's CU count
   }
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, 0) !=
@@ -1333,8 +1335,11 @@ int build_tpos(hgx_ctx *ctx) {
     hipcub::DoubleBuffer<int> keys(ctx->tpos.as<int>(), k2.as<int>());
     hipcub::DoubleBuffer<int> vals(v1.as<int>(), v2.as<int>());
     size_t tb = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, vals, (int)n, 0, bits,
-                                       ctx->stream);
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, vals, (int)n, 0, bits,
+                                           ctx->stream) != hipSuccess) {
+      rc = hgx_fail(ctx, HGX_EHIP, "tpos radix sort sizing failed");
+      break;
+    }
     if ((rc = hgx_ensure(ctx, tmp, tb + 256)) != HGX_OK) break;
     if (hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, keys, vals, (int)n, 0, bits,
                                            ctx->stream) != hipSuccess) {

@@ -192,7 +192,10 @@ __device__ __forceinline__ int esize(const HobeW &H, int e) {
   return H.rp_e[e + 1] - H.rp_e[e];
 }
 
-// One full wave: max(p, ee(e, f)), wave-uniform in and out.
+// One full wave: max(p, ee(e, f)), wave-uniform in and out. Each lane
+// probes kEeWays members of the smaller edge at once (their binary searches
+// in lockstep: independent load chains), kEeWays * 64 members per step.
+constexpr int kEeWays = 4;
 __device__ float wave_ee(const HobeW &H, int e, int f, float p, int lane) {
   if (e == f) return fmaxf(p, H.self[e]);
   const float bound = fminf(H.self[e], H.self[f]);
@@ -204,25 +207,66 @@ __device__ float wave_ee(const HobeW &H, int e, int f, float p, int lane) {
   }
   const int se = H.rp_e[s + 1];
   float lp = p;
-  for (int t0 = H.rp_e[s]; t0 < se; t0 += 64) {
-    const int t = t0 + lane;
-    if (t < se) {
-      const float ws = H.we[t];
-      if (ws > lp) {
-        const int u = H.col_e[t];
-        const int j = find_sorted(H.col_n, H.rp_n[u], H.rp_n[u + 1], b);
-        if (j >= 0) lp = fmaxf(lp, fminf(ws, H.wn[j]));
+  for (int t0 = H.rp_e[s]; t0 < se; t0 += 64 * kEeWays) {
+    float ws[kEeWays];
+    int lo[kEeWays], hi[kEeWays], end[kEeWays];
+#pragma unroll
+    for (int k = 0; k < kEeWays; k++) {
+      const int t = t0 + k * 64 + lane;
+      ws[k] = t < se ? H.we[t] : 0.f;
+      const int u = t < se && ws[k] > lp ? H.col_e[t] : -1;
+      lo[k] = u >= 0 ? H.rp_n[u] : 0;
+      end[k] = u >= 0 ? H.rp_n[u + 1] : 0;
+      hi[k] = end[k];
+    }
+    while (true) {  // lower bound of b in each member's edge list
+      bool live = false;
+      int v[kEeWays];
+#pragma unroll
+      for (int k = 0; k < kEeWays; k++) {
+        v[k] = lo[k] < hi[k] ? H.col_n[(lo[k] + hi[k]) >> 1] : 0;
+        live |= lo[k] < hi[k];
+      }
+      if (!live) break;
+#pragma unroll
+      for (int k = 0; k < kEeWays; k++) {
+        if (lo[k] < hi[k]) {
+          const int mid = (lo[k] + hi[k]) >> 1;
+          if (v[k] < b) lo[k] = mid + 1;
+          else hi[k] = mid;
+        }
       }
     }
+#pragma unroll
+    for (int k = 0; k < kEeWays; k++)
+      if (lo[k] < end[k] && H.col_n[lo[k]] == b) lp = fmaxf(lp, fminf(ws[k], H.wn[lo[k]]));
     lp = hgx::wave_max(lp);
     if (lp >= bound) break;
   }
   return lp;
 }
 
-// One full wave: ne(v, e) = max over e' in E(v) of ee(e, e').
-__device__ float wave_ne(const HobeW &H, int v, int e, int lane) {
+// A wave's LDS hash of E(v) (wave_ne's member walk)
+constexpr int kNeBits = 9;
+constexpr int kNeHash = 1 << kNeBits;
+constexpr int kNeCap = kNeHash / 2;
+constexpr int kNeRead = 8;
+__device__ __forceinline__ unsigned ne_slot(int e) {
+  return ((unsigned)e * 2654435761u) >> (32 - kNeBits);
+}
+
+#ifdef HGX_DEBUG_KNOBS
+// wave_ne branch census (debug builds, hgx_hobe_diag): [branch] pairs,
+// [4 + branch] s_memrealtime ticks; branch 0 bound 0, 1 LDS member walk,
+// 2 merged member walk, 3 per-edge ee
+__device__ unsigned long long g_ne_diag[8];
+#endif
+
+// One full wave: ne(v, e) = max over e' in E(v) of ee(e, e'). `ev`: the
+// wave's kNeHash ints of LDS.
+__device__ float wave_ne(const HobeW &H, int v, int e, int lane, int *ev, int &br) {
   const float bound = H.self[e];
+  br = 0;
   if (bound <= 0.f) return 0.f;
   const int vb = H.rp_n[v], ve = H.rp_n[v + 1];
   const int eb = H.rp_e[e], eend = H.rp_e[e + 1], esz = eend - eb;
@@ -232,8 +276,63 @@ __device__ float wave_ne(const HobeW &H, int v, int e, int lane) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) cost_b += __shfl_xor(cost_b, off);
   float p = 0.f;
+  if ((long long)esz * 4 <= cost_b && ve - vb <= kNeCap) {
+    br = 1;
+    // (a) members u of e: max over e' in E(u) ∩ E(v) of min(w(e,u), w(u,e')),
+    // E(v) in the wave's LDS hash, each member's edge list read straight
+    // through (independent loads) instead of merged with E(v)
+    for (int k = lane; k < kNeHash; k += 64) ev[k] = -1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int t = vb + lane; t < ve; t += 64) {
+      const int f = H.col_n[t];
+      unsigned sl = ne_slot(f);
+      while (true) {
+        const int old = atomicCAS(&ev[sl], -1, f);
+        if (old == -1 || old == f) break;
+        sl = (sl + 1) & (kNeHash - 1);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int t0 = eb; t0 < eend; t0 += 64) {
+      const int t = t0 + lane;
+      if (t < eend) {
+        const float weu = H.we[t];
+        if (weu > p) {
+          const int u = H.col_e[t];
+          const int ae = H.rp_n[u + 1];
+          // kNeRead edge ids per step, all loads issued before any probe
+          for (int a0 = H.rp_n[u]; a0 < ae; a0 += kNeRead) {
+            int f[kNeRead];
+#pragma unroll
+            for (int j = 0; j < kNeRead; j++) f[j] = a0 + j < ae ? H.col_n[a0 + j] : -1;
+#pragma unroll
+            for (int j = 0; j < kNeRead; j++) {
+              if (f[j] < 0) continue;
+              unsigned sl = ne_slot(f[j]);
+              int k;
+              while ((k = ev[sl]) >= 0 && k != f[j]) sl = (sl + 1) & (kNeHash - 1);
+              if (k == f[j]) p = fmaxf(p, fminf(weu, H.wn[a0 + j]));
+            }
+          }
+        }
+      }
+      p = hgx::wave_max(p);
+      if (p >= bound) break;
+    }
+    // the next pair of this wave rewrites ev: every lane is done reading
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return p;
+  }
+  br = 3;
   if ((long long)esz * 4 <= cost_b) {
-    // (a) members u of e: max over e' in E(u) ∩ E(v) of min(w(e,u), w(u,e'))
+    br = 2;
+    // (a) with a long E(v): each member's edge list merged with E(v)
     for (int t0 = eb; t0 < eend; t0 += 64) {
       const int t = t0 + lane;
       if (t < eend) {
@@ -318,13 +417,25 @@ __global__ void hobe_nn_kernel(HobeW H, PairSrc P, int64_t n) {
 // edge-edge (kind 1) / node-edge (kind 2): one wave per pair
 __global__ __launch_bounds__(256) void hobe_wave_kernel(HobeW H, PairSrc P,
                                                         int kind, int64_t n) {
+  __shared__ int s_ev[4][kNeHash];  // per wave: wave_ne's E(v) hash
   const int lane = threadIdx.x & 63;
+  int *ev = s_ev[threadIdx.x >> 6];
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
   for (int64_t q = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
        q < n; q += nw) {
     int a, b;
     get_pair(P, kind, q, a, b);
-    const float p = kind == 1 ? wave_ee(H, a, b, 0.f, lane) : wave_ne(H, a, b, lane);
+#ifdef HGX_DEBUG_KNOBS
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    int br = 0;
+    const float p = kind == 1 ? wave_ee(H, a, b, 0.f, lane) : wave_ne(H, a, b, lane, ev, br);
+#ifdef HGX_DEBUG_KNOBS
+    if (kind == 2 && lane == 0) {
+      atomicAdd(&g_ne_diag[br], 1ull);
+      atomicAdd(&g_ne_diag[4 + br], __builtin_amdgcn_s_memrealtime() - t0);
+    }
+#endif
     if (lane == 0) put_prob(P, kind, q, p);
   }
 }
@@ -348,12 +459,21 @@ int launch_probs(hgx_ctx *ctx, int kind, const PairSrc &P, int64_t n) {
                        0, ctx->stream, H, P, n);
   } else {
     int dev = 0, ncu = 256;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    HGX_HIP(ctx, hipGetDevice(&dev));
+    HGX_HIP(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     hipLaunchKernelGGL(hobe_wave_kernel, dim3(grid_for(n, 4, 8 * ncu)), dim3(256),
                        0, ctx->stream, H, P, kind, n);
   }
   HGX_LAUNCH_CHECK(ctx);
+#ifdef HGX_DEBUG_KNOBS
+  if (kind == 2 && hgx_debug_env("HGX_NE_DIAG", 0)) {
+    unsigned long long d[8];
+    HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    HGX_HIP(ctx, hipMemcpyFromSymbol(d, HIP_SYMBOL(g_ne_diag), sizeof(d)));
+    fprintf(stderr, "ne_diag pairs %llu %llu %llu %llu wave_ms %.1f %.1f %.1f %.1f\n",
+            d[0], d[1], d[2], d[3], d[4] / 1e5, d[5] / 1e5, d[6] / 1e5, d[7] / 1e5);
+  }
+#endif
   return HGX_OK;
 }
 

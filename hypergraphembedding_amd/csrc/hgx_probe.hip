@@ -61,8 +61,8 @@ extern "C" int hgx_probe_gather(hgx_ctx *ctx, int64_t table_bytes,
   HGX_TRY(hgx_ensure(ctx, ctx->s7, (size_t)table_bytes + 64));
   HGX_HIP(ctx, hipMemsetAsync(ctx->s7.p, 0, (size_t)table_bytes + 64, ctx->stream));
   int dev = 0, ncu = 256;
-  hipGetDevice(&dev);
-  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  HGX_HIP(ctx, hipGetDevice(&dev));
+  HGX_HIP(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   const int blocks = ncu * 8, threads = 256;
   const uint64_t groups = (uint64_t)blocks * threads / 4;
   const uint64_t iters = ((1ull << 28) / groups + in_flight - 1) / in_flight * in_flight;

@@ -191,7 +191,15 @@ __device__ int first_common(const int *a, int na, const int *b, int nb) {
 // ---- 3-hop membership (A: node -> edges, AT: edge -> nodes) --------------
 // Smallest node in members(x) ∩ members(y) (INT_MAX if none): the smaller
 // edge's members in ascending order, each probed for the other edge in its
-// own sorted edge list; the first hit is the minimum.
+// own sorted edge list; the first hit is the minimum. Eight members are
+// probed at once (their binary searches interleaved step by step): a lone
+// thread's probe is a chain of ~6 dependent loads, and the walk over two
+// disjoint mid-size power-law edges (thousands of members) was that chain
+// thousands of times. C4 2% slice (tools/sample_c4_probe.py): sampling
+// 2.39 s one at a time, 1.66 s four, 1.53 s eight, 2.84 s sixteen (register
+// pressure). A merge of the two sorted member lists measured slower (one
+// dependent load per step over both lists): 3.0 s.
+constexpr int kProbeWays = 8;
 __device__ int edges_min_common(const Csr &A, const Csr &AT, int x, int y) {
   if (x == y) return AT.rp[x + 1] > AT.rp[x] ? AT.col[AT.rp[x]] : INT_MAX;
   if (AT.rp[x + 1] - AT.rp[x] > AT.rp[y + 1] - AT.rp[y]) {
@@ -199,9 +207,42 @@ __device__ int edges_min_common(const Csr &A, const Csr &AT, int x, int y) {
     x = y;
     y = t;
   }
-  for (int t = AT.rp[x]; t < AT.rp[x + 1]; t++) {
-    const int u = AT.col[t];
-    if (find_sorted(A.col, A.rp[u], A.rp[u + 1], y) >= 0) return u;
+  const int xe = AT.rp[x + 1];
+  for (int t = AT.rp[x]; t < xe; t += kProbeWays) {
+    int u[kProbeWays], lo[kProbeWays], hi[kProbeWays], end[kProbeWays];
+#pragma unroll
+    for (int k = 0; k < kProbeWays; k++) u[k] = t + k < xe ? AT.col[t + k] : -1;
+#pragma unroll
+    for (int k = 0; k < kProbeWays; k++) {
+      lo[k] = u[k] >= 0 ? A.rp[u[k]] : 0;
+      end[k] = u[k] >= 0 ? A.rp[u[k] + 1] : 0;
+      hi[k] = end[k];
+    }
+    // lower bound of y in each member's edge list, in lockstep
+    while (true) {
+      bool live = false;
+      int v[kProbeWays];
+#pragma unroll
+      for (int k = 0; k < kProbeWays; k++) {
+        v[k] = lo[k] < hi[k] ? A.col[(lo[k] + hi[k]) >> 1] : 0;
+        live |= lo[k] < hi[k];
+      }
+      if (!live) break;
+#pragma unroll
+      for (int k = 0; k < kProbeWays; k++) {
+        if (lo[k] < hi[k]) {
+          const int mid = (lo[k] + hi[k]) >> 1;
+          if (v[k] < y) lo[k] = mid + 1;
+          else hi[k] = mid;
+        }
+      }
+    }
+    int hit[kProbeWays];
+#pragma unroll
+    for (int k = 0; k < kProbeWays; k++) hit[k] = lo[k] < end[k] ? A.col[lo[k]] : -1;
+#pragma unroll
+    for (int k = 0; k < kProbeWays; k++)
+      if (hit[k] == y) return u[k];
   }
   return INT_MAX;
 }
@@ -466,11 +507,20 @@ struct RejectArgs {
                              // |l3 row of the incidence's column| (nnz + 1)
   int mode3;                 // 0 auto, 1 paths, 2 uniform columns
   int *stats;                // [0] rejection rows, [1] stalled, [3] uniform-mode rows
+  long long *diag;           // debug builds: per-row {pattern, row, mode, n1, q, W,
+  int *diag_n;               // rounds, s_memrealtime ticks} (HGX_REJ_DIAG_OUT)
+  int diag_cap;
 };
+
+constexpr int kEvBits = 9;  // LDS hash of a node row's edges (<= kSB of them)
+constexpr int kEvHash = 1 << kEvBits;
 
 struct RejShared {
   int sel[kSelCap];
   int hash[kHash];
+  int ev[kEvHash];  // PAT_NNE uniform columns: the row's edges E(v)
+  int evsz[kSB];    // and their sizes
+  int nev;          // |E(v)| when staged, else -1
   unsigned long long key[kSB];
   int flag[kSB];
   int a_id[kSB];
@@ -503,6 +553,38 @@ __device__ void hash_put(int *h, int c) {
   }
 }
 
+__device__ __forceinline__ unsigned evslot(int e) {
+  return ((unsigned)e * 2654435761u) >> (32 - kEvBits);
+}
+__device__ bool ev_has(const int *h, int e) {
+  unsigned s = evslot(e);
+  while (true) {
+    const int k = h[s];
+    if (k == e) return true;
+    if (k < 0) return false;
+    s = (s + 1) & (kEvHash - 1);
+  }
+}
+
+// (v, c) in A A^T A with E(v) staged in LDS (S.ev): some member u of edge c
+// has an edge in E(v). Each member costs its (contiguous) edge list probed
+// in LDS; ne3_member instead intersects every e1 of E(v) with c from the
+// smaller side (a binary search per probed node), which is the cheaper walk
+// when c is far larger than the row's edges. The same set either way.
+__device__ bool nne_member_lds(const RejectArgs &A, const RejShared &S, int v, int c) {
+  const int cb = A.AT.rp[c], nc = A.AT.rp[c + 1] - cb;
+  long long probes = 0;
+  for (int j = 0; j < S.nev; j++) probes += min(S.evsz[j], nc);
+  if (2ll * nc > 5ll * probes) return ne3_member(A.A, A.AT, v, c);
+  for (int t = cb; t < cb + nc; t++) {
+    const int u = A.AT.col[t];
+    const int ue = A.A.rp[u + 1];
+    for (int j = A.A.rp[u]; j < ue; j++)
+      if (ev_has(S.ev, A.A.col[j])) return true;
+  }
+  return false;
+}
+
 // path count of level-1 entity m of row r
 __device__ __forceinline__ long long level1_weight(const RejectArgs &A, int m) {
   if (A.levels == 2) return A.l2.rp[m + 1] - A.l2.rp[m];
@@ -524,7 +606,8 @@ __device__ int draw_candidate(const RejectArgs &A, int r, int mode, bool small,
   if (mode == 2) {
     const int c = (int)hgx::bounded(h, (uint32_t)A.ncols);
     if (hash_has(S.hash, c)) return INT_MAX;
-    const bool in = A.pattern == PAT_NNE ? ne3_member(A.A, A.AT, r, c)
+    const bool in = A.pattern == PAT_NNE ? (S.nev >= 0 ? nne_member_lds(A, S, r, c)
+                                                       : ne3_member(A.A, A.AT, r, c))
                                          : ne3_member(A.A, A.AT, c, r);
     return in ? c : INT_MAX;
   }
@@ -654,10 +737,33 @@ __global__ __launch_bounds__(kSB) void reject_rows(RejectArgs A) {
     }
     for (int k = tid; k < kHash; k += kSB) S.hash[k] = -1;
     if (tid == 0) S.nsel = 0;
+    // uniform columns of a node row: its edges into LDS for the membership
+    // test (nne_member_lds)
+    const bool stage_ev = mode == 2 && A.pattern == PAT_NNE && n1 <= kSB;
+    for (int k = tid; k < kEvHash; k += kSB) S.ev[k] = -1;
+    if (tid == 0) S.nev = stage_ev ? n1 : -1;
+    __syncthreads();
+    if (stage_ev && tid < n1) {
+      const int e1 = A.l1.col[b1 + tid];
+      S.evsz[tid] = A.AT.rp[e1 + 1] - A.AT.rp[e1];
+      unsigned sl = evslot(e1);
+      while (true) {
+        const int old = atomicCAS(&S.ev[sl], -1, e1);
+        if (old == -1 || old == e1) break;
+        sl = (sl + 1) & (kEvHash - 1);
+      }
+    }
     __syncthreads();
     int stall = 0;
     bool done = false;
+#ifdef HGX_DEBUG_KNOBS
+    const unsigned long long t_row = __builtin_amdgcn_s_memrealtime();
+    int rounds_used = 0;
+#endif
     for (int round = 0; round < 4096; round++) {
+#ifdef HGX_DEBUG_KNOBS
+      rounds_used = round + 1;
+#endif
       const uint64_t base = ((uint64_t)(uint32_t)r << 32) ^ ((uint64_t)round << 12);
       const uint64_t h = hgx::rand64(A.seed, 0x300 + A.pattern, base + tid);
       const int cand = draw_candidate(A, r, mode, small, n1, W, wmax, S, h);
@@ -704,6 +810,22 @@ __global__ __launch_bounds__(kSB) void reject_rows(RejectArgs A) {
       stall = got ? 0 : stall + 1;
       if (stall >= 32) break;
     }
+#ifdef HGX_DEBUG_KNOBS
+    if (A.diag && tid == 0) {
+      const int k = atomicAdd(A.diag_n, 1);
+      if (k < A.diag_cap) {
+        long long *o = A.diag + 8ll * k;
+        o[0] = A.pattern;
+        o[1] = r;
+        o[2] = done ? mode : -1 - mode;
+        o[3] = n1;
+        o[4] = q;
+        o[5] = W;
+        o[6] = rounds_used;
+        o[7] = (long long)(__builtin_amdgcn_s_memrealtime() - t_row);
+      }
+    }
+#endif
     if (!done) {  // the union looks smaller than q: expand it (pass 2)
       if (tid == 0) {
         A.defer_big[atomicAdd(&A.ndefer[1], 1)] = r;
@@ -848,7 +970,7 @@ int excl_scan_i32_to_i64(hgx_ctx *ctx, const int *in, int64_t *out, int n,
   // out has n+1 entries; out[n] = total; accumulate in int64
   hipcub::TransformInputIterator<int64_t, ToI64, const int *> it(in, ToI64());
   size_t tmp = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, out, n + 1, ctx->stream);
+  HGX_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, out, n + 1, ctx->stream));
   HGX_TRY(hgx_ensure(ctx, ctx->s7, tmp + 256));
   HGX_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(ctx->s7.p, tmp, it, out, n + 1,
                                                 ctx->stream));
@@ -912,11 +1034,14 @@ int expand_pass(hgx_ctx *ctx, const ExpandArgs &base, const int *rows, int n,
   a.list_cap = list_cap;
   a.lds_bitmap = lds;
   int rc = HGX_OK;
-  hipMemsetAsync(a.row_ctr, 0, sizeof(int), ctx->stream);
-  hipLaunchKernelGGL(expand_rows, dim3(nwg), dim3(kSB), lds ? (size_t)nwords * 4 : 0,
-                     ctx->stream, a);
-  if (hipGetLastError() != hipSuccess)
-    rc = hgx_fail(ctx, HGX_EHIP, "expand_rows launch failed");
+  if (hipMemsetAsync(a.row_ctr, 0, sizeof(int), ctx->stream) != hipSuccess)
+    rc = hgx_fail(ctx, HGX_EHIP, "expand_rows queue reset failed");
+  if (rc == HGX_OK) {
+    hipLaunchKernelGGL(expand_rows, dim3(nwg), dim3(kSB), lds ? (size_t)nwords * 4 : 0,
+                       ctx->stream, a);
+    if (hipGetLastError() != hipSuccess)
+      rc = hgx_fail(ctx, HGX_EHIP, "expand_rows launch failed");
+  }
   if (hipStreamSynchronize(ctx->stream) != hipSuccess && rc == HGX_OK)
     rc = hgx_fail(ctx, HGX_EHIP, "expand_rows failed");
   hgx_release(list);
@@ -998,8 +1123,8 @@ int run_pattern(hgx_ctx *ctx, int pattern, const int32_t *host_quota,
           it(ci, f);
       size_t tmp = 0;
       // the value at t == nnz is never used: scan nnz values, then the total
-      hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, ps.as<int64_t>(), nnz,
-                                       ctx->stream);
+      HGX_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, ps.as<int64_t>(),
+                                                    nnz, ctx->stream));
       HGX_TRY(hgx_ensure(ctx, ctx->s7, tmp + 256));
       HGX_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(ctx->s7.p, tmp, it,
                                                     ps.as<int64_t>(), nnz,
@@ -1034,14 +1159,41 @@ int run_pattern(hgx_ctx *ctx, int pattern, const int32_t *host_quota,
     r.ps = ps.as<int64_t>();
     r.mode3 = ctx->tune.sample_mode3;
     r.stats = ctr + 5;
+    DevBuf diag;
+#ifdef HGX_DEBUG_KNOBS
+    const char *diag_out = hgx_debug_env_str("HGX_REJ_DIAG_OUT");
+    if (diag_out && nlist > 0) {
+      HGX_TRY(hgx_ensure(ctx, diag, sizeof(long long) * 8 * (size_t)nlist + 64));
+      HGX_HIP(ctx, hipMemsetAsync(diag.p, 0, 64, ctx->stream));
+      r.diag_n = diag.as<int>();
+      r.diag = reinterpret_cast<long long *>(diag.as<char>() + 64);
+      r.diag_cap = nlist;
+    }
+#endif
     if (nlist > 0) {
       int dev = 0, ncu = 256;
-      hipGetDevice(&dev);
-      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      HGX_HIP(ctx, hipGetDevice(&dev));
+      HGX_HIP(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
       const int nwg = std::min(nlist, 4 * ncu);
       hipLaunchKernelGGL(reject_rows, dim3(nwg), dim3(kSB), 0, ctx->stream, r);
       HGX_LAUNCH_CHECK(ctx);
     }
+#ifdef HGX_DEBUG_KNOBS
+    if (r.diag) {
+      int nd = 0;
+      HGX_HIP(ctx, hipMemcpyAsync(&nd, diag.p, sizeof(int), hipMemcpyDeviceToHost,
+                                  ctx->stream));
+      HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      nd = std::min(nd, nlist);
+      std::vector<long long> h(8 * (size_t)nd);
+      HGX_HIP(ctx, hipMemcpy(h.data(), r.diag, sizeof(long long) * h.size(),
+                             hipMemcpyDeviceToHost));
+      if (FILE *f = fopen(diag_out, "ab")) {
+        fwrite(h.data(), sizeof(long long), h.size(), f);
+        fclose(f);
+      }
+    }
+#endif
     int nd[2] = {0, 0};
     HGX_HIP(ctx, hipMemcpyAsync(nd, ctr + 2, sizeof(nd), hipMemcpyDeviceToHost,
                                 ctx->stream));
@@ -1049,6 +1201,7 @@ int run_pattern(hgx_ctx *ctx, int pattern, const int32_t *host_quota,
                                 ctx->stream));
     HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
     hgx_release(ps);
+    hgx_release(diag);
     // deferred rows: small ones have at most reject_w distinct columns
     HGX_TRY(expand_pass(ctx, a, dsmall.as<int>(), nd[0],
                         std::min<int64_t>(a.ncols, std::max<int64_t>(2 * reject_w, 65536))));

@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "hgx_internal.h"
@@ -114,10 +115,11 @@ struct Csr4 {
 // (neighbours) for a difference. Returns false for an entry naming rows
 // outside the graph or a node-edge endpoint without neighbours (the
 // sampler refuses those): nothing is then read from the incidence.
-template <bool CHECK>
+template <bool CHECK, typename IdPtr = std::conditional_t<CHECK, const int *, int *>,
+          typename TgPtr = std::conditional_t<CHECK, const float *, float *>>
 __device__ __forceinline__ bool expand_one(uint32_t w0, uint32_t w1, uint32_t w2,
                                            const BlockTab &t, int K, uint64_t seed,
-                                           const Csr4 &g, int *ri, float *tg,
+                                           const Csr4 &g, IdPtr ri, TgPtr tg,
                                            int &diff) {
   const int b = (int)(w0 >> kRowBits);
   if (b >= t.nb) return false;
@@ -135,7 +137,7 @@ __device__ __forceinline__ bool expand_one(uint32_t w0, uint32_t w1, uint32_t w2
   const bool ne = t.kind[b] >= REC_NE_NODE;
   for (int s = 0; s < 4; s++) {
     const int want = s == rpos ? row + 1 : s == cpos ? col + 1 : 0;
-    if (CHECK) {
+    if constexpr (CHECK) {
       if (ri[s] != want) diff |= 4;
     } else {
       ri[s] = want;
@@ -144,7 +146,7 @@ __device__ __forceinline__ bool expand_one(uint32_t w0, uint32_t w1, uint32_t w2
   const float p = __uint_as_float(w2);
   for (int s = 0; s < 3; s++) {
     const float want = s == tpos ? p : 0.f;
-    if (CHECK) {
+    if constexpr (CHECK) {
       if (__float_as_uint(tg[s]) != __float_as_uint(want)) diff |= 8;
     } else {
       tg[s] = want;
@@ -152,7 +154,7 @@ __device__ __forceinline__ bool expand_one(uint32_t w0, uint32_t w1, uint32_t w2
   }
   if (!ne) {
     for (int s = 4; s < R; s++) {
-      if (CHECK) {
+      if constexpr (CHECK) {
         if (ri[s] != 0) diff |= 16;
       } else {
         ri[s] = 0;
@@ -174,7 +176,7 @@ __device__ __forceinline__ bool expand_one(uint32_t w0, uint32_t w1, uint32_t w2
     const uint64_t h2 = hgx::mix64(rk + key * 64 + 32 + k);
     const int a = g.col_e[nb + hgx::bounded(h, (uint32_t)nl)] + 1;
     const int c = g.col_n[eb + hgx::bounded(h2, (uint32_t)el)] + 1;
-    if (CHECK) {
+    if constexpr (CHECK) {
       if (ri[4 + k] != a || ri[4 + K + k] != c) diff |= 16;
     } else {
       ri[4 + k] = a;
@@ -227,8 +229,7 @@ __global__ void store_pack(const int *idx, const float *tgt, int64_t n, int K,
     const uint32_t w2 = __float_as_uint(p);
     if (!bad) {
       int diff = 0;
-      const bool ok = expand_one<true>(w0, w1, w2, t, K, seed, g, const_cast<int *>(ri),
-                                       const_cast<float *>(tgt + i * 3), diff);
+      const bool ok = expand_one<true>(w0, w1, w2, t, K, seed, g, ri, tgt + i * 3, diff);
       if (!ok) diff |= 32;
       if (diff) {
         bad = 1 | diff | (64 << b);
