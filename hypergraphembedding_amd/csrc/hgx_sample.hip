@@ -518,8 +518,9 @@ constexpr int kEvHash = 1 << kEvBits;
 struct RejShared {
   int sel[kSelCap];
   int hash[kHash];
-  int ev[kEvHash];  // PAT_NNE uniform columns: the row's edges E(v)
-  int evsz[kSB];    // and their sizes
+  int ev[kEvHash];  // PAT_NNE rejection rows: the row's edges E(v)
+  int evid[kSB];    // and in E(v)'s (ascending) order
+  int evsz[kSB];    // with their sizes
   int nev;          // |E(v)| when staged, else -1
   unsigned long long key[kSB];
   int flag[kSB];
@@ -566,22 +567,50 @@ __device__ bool ev_has(const int *h, int e) {
   }
 }
 
-// (v, c) in A A^T A with E(v) staged in LDS (S.ev): some member u of edge c
-// has an edge in E(v). Each member costs its (contiguous) edge list probed
-// in LDS; ne3_member instead intersects every e1 of E(v) with c from the
-// smaller side (a binary search per probed node), which is the cheaper walk
-// when c is far larger than the row's edges. The same set either way.
-__device__ bool nne_member_lds(const RejectArgs &A, const RejShared &S, int v, int c) {
-  const int cb = A.AT.rp[c], nc = A.AT.rp[c + 1] - cb;
-  long long probes = 0;
-  for (int j = 0; j < S.nev; j++) probes += min(S.evsz[j], nc);
-  if (2ll * nc > 5ll * probes) return ne3_member(A.A, A.AT, v, c);
-  for (int t = cb; t < cb + nc; t++) {
-    const int u = A.AT.col[t];
-    const int ue = A.A.rp[u + 1];
-    for (int j = A.A.rp[u]; j < ue; j++)
-      if (ev_has(S.ev, A.A.col[j])) return true;
+// With E(v) staged in LDS (S.ev, ids S.evid, sizes S.evsz; ascending):
+// does some member u of edge c have an edge f of E(v) with f < lim? Each
+// member costs its contiguous edge list (read kEvRead ids at a time, all
+// loads before the LDS probes), members kEvWays at a time. The other walk
+// -- every such f intersected with c from the smaller side, a binary search
+// per probed node -- is cheaper when c is far larger than the row's edges:
+// nne_meets picks by the probe counts. The same answer either way.
+constexpr int kEvWays = 4;
+constexpr int kEvRead = 8;
+__device__ bool members_meet_ev(const RejectArgs &A, const RejShared &S, int c, int lim) {
+  const int cb = A.AT.rp[c], ce = A.AT.rp[c + 1];
+  for (int t = cb; t < ce; t += kEvWays) {
+    int ub[kEvWays], ue[kEvWays];
+#pragma unroll
+    for (int k = 0; k < kEvWays; k++) {
+      const int u = t + k < ce ? A.AT.col[t + k] : -1;
+      ub[k] = u >= 0 ? A.A.rp[u] : 0;
+      ue[k] = u >= 0 ? A.A.rp[u + 1] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kEvWays; k++) {
+      for (int a0 = ub[k]; a0 < ue[k]; a0 += kEvRead) {
+        int f[kEvRead];
+#pragma unroll
+        for (int j = 0; j < kEvRead; j++) f[j] = a0 + j < ue[k] ? A.A.col[a0 + j] : INT_MAX;
+#pragma unroll
+        for (int j = 0; j < kEvRead; j++)
+          if (f[j] < lim && ev_has(S.ev, f[j])) return true;
+      }
+    }
   }
+  return false;
+}
+
+// some e1 of E(v) with e1 < lim meets edge c (lim = INT_MAX: (v, c) in
+// A A^T A); E(v) staged in LDS
+__device__ bool nne_meets(const RejectArgs &A, const RejShared &S, int v, int c, int lim) {
+  const int nc = A.AT.rp[c + 1] - A.AT.rp[c];
+  long long probes = 0;
+  for (int j = 0; j < S.nev && S.evid[j] < lim; j++) probes += min(S.evsz[j], nc);
+  if (probes == 0) return false;
+  if (2ll * nc <= 5ll * probes) return members_meet_ev(A, S, c, lim);
+  for (int j = 0; j < S.nev && S.evid[j] < lim; j++)
+    if (edges_min_common(A.A, A.AT, S.evid[j], c) != INT_MAX) return true;
   return false;
 }
 
@@ -606,7 +635,7 @@ __device__ int draw_candidate(const RejectArgs &A, int r, int mode, bool small,
   if (mode == 2) {
     const int c = (int)hgx::bounded(h, (uint32_t)A.ncols);
     if (hash_has(S.hash, c)) return INT_MAX;
-    const bool in = A.pattern == PAT_NNE ? (S.nev >= 0 ? nne_member_lds(A, S, r, c)
+    const bool in = A.pattern == PAT_NNE ? (S.nev >= 0 ? nne_meets(A, S, r, c, INT_MAX)
                                                        : ne3_member(A.A, A.AT, r, c))
                                          : ne3_member(A.A, A.AT, c, r);
     return in ? c : INT_MAX;
@@ -647,7 +676,10 @@ __device__ int draw_candidate(const RejectArgs &A, int r, int mode, bool small,
   // canonical (first) path to c, lexicographic in (m1, m2)
   if (A.pattern == PAT_NNE) {
     // r = v, m1 = e1 in E(v), m2 = u in e1, c = e: the first e1 of E(v)
-    // meeting e, then the smallest common member
+    // meeting e, then the smallest common member (a walk over e's members
+    // against E(v) in LDS measured slower here: an accepted path must rule
+    // out every earlier e1, so it reads all of e's members, where this loop
+    // stops at the first e1 meeting e -- usually an early, large one)
     for (int t = b1; t < A.l1.rp[r + 1]; t++) {
       const int e1 = A.l1.col[t];
       if (e1 > m1) break;
@@ -738,13 +770,14 @@ __global__ __launch_bounds__(kSB) void reject_rows(RejectArgs A) {
     for (int k = tid; k < kHash; k += kSB) S.hash[k] = -1;
     if (tid == 0) S.nsel = 0;
     // uniform columns of a node row: its edges into LDS for the membership
-    // test (nne_member_lds)
+    // test (nne_meets)
     const bool stage_ev = mode == 2 && A.pattern == PAT_NNE && n1 <= kSB;
     for (int k = tid; k < kEvHash; k += kSB) S.ev[k] = -1;
     if (tid == 0) S.nev = stage_ev ? n1 : -1;
     __syncthreads();
     if (stage_ev && tid < n1) {
       const int e1 = A.l1.col[b1 + tid];
+      S.evid[tid] = e1;
       S.evsz[tid] = A.AT.rp[e1 + 1] - A.AT.rp[e1];
       unsigned sl = evslot(e1);
       while (true) {
