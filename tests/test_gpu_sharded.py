@@ -234,8 +234,10 @@ def test_row_sharded_sampling_equals_single_process(tmp_path, kind, world,
       assert np.isin(idx[i, 9:14] - 1, inc.col_n[inc.rp_n[v]:inc.rp_n[v + 1]]).all()
 
 
-def _pipeline_worker(rank, world, port, out_path, budget, with_coords):
-  """embedding.hobe_sharded on `world` gloo ranks sharing cuda:0."""
+def _pipeline_worker(rank, world, port, out_path, budget, with_coords,
+                     backend="gloo"):
+  """embedding.hobe_sharded on `world` ranks sharing cuda:0 (gloo; nccl
+  only at world 1)."""
   import torch
   import torch.distributed as dist
   import sys
@@ -246,8 +248,12 @@ def _pipeline_worker(rank, world, port, out_path, budget, with_coords):
   from hypergraphembedding_amd.embedding import hobe_sharded
   os.environ["MASTER_ADDR"] = "127.0.0.1"
   os.environ["MASTER_PORT"] = str(port)
-  dist.init_process_group("gloo", rank=rank, world_size=world)
   torch.cuda.set_device(0)
+  if backend == "nccl":
+    dist.init_process_group("nccl", rank=rank, world_size=world,
+                            device_id=torch.device("cuda", 0))
+  else:
+    dist.init_process_group("gloo", rank=rank, world_size=world)
   inc = _graph("powerlaw")
   coords = None
   if with_coords:
@@ -287,6 +293,25 @@ def test_hobe_pipeline_sharded_equals_single_process(tmp_path, budget):
   for d in out[2]:
     assert np.array_equal(d["nt"], ref["nt"])
     assert np.array_equal(d["et"], ref["et"])
+
+
+def test_hobe_pipeline_rccl_single_rank_store_path(tmp_path):
+  """The store path of the multi-GPU pipeline over RCCL (device buffers:
+  class entries read from the store into a device tensor, all-gathered
+  asynchronously, appended from device memory) with one rank -- the only
+  RCCL configuration a 1-GPU box runs -- gives the gloo rank's tables bit
+  for bit."""
+  import torch.multiprocessing as mp
+  out = {}
+  for backend in ("gloo", "nccl"):
+    path = str(tmp_path / backend)
+    mp.start_processes(_pipeline_worker,
+                       args=(1, _free_port(), path, 300_000, True, backend),
+                       nprocs=1, join=True, start_method="spawn")
+    out[backend] = np.load(path + ".0.npz")
+  assert np.isfinite(out["nccl"]["nt"]).all()
+  for k in ("nt", "et"):
+    assert np.array_equal(out["nccl"][k], out["gloo"][k]), k
 
 
 def test_hobe_pipeline_sharded_full_path(tmp_path):
