@@ -382,7 +382,7 @@ int hgx_train_multi_pending(hgx_ctx *ctx, int64_t *batches);
  * accumulators persist; the padding row is written back at the end of each
  * call), so a stream too large to keep resident trains as a sequence of
  * one-epoch calls over resident chunks, the caller adding up these sums
- * (hg2v_model.Hg2vModel.fit_streaming). */
+ * (hg2v_model.Hg2vModel.fit_store over hgx_store_load's chunks). */
 int hgx_train_last_loss(hgx_ctx *ctx, double *loss_sum);
 
 /* ---- dense MLP engine (combiners + link-prediction classifier) --------- *
