@@ -230,3 +230,44 @@ def test_row_chunks_respect_per_row_bounds():
   assert cls.max() <= budget
   assert [c for c, _ in chunks] == list(range(n))
   assert n > -(-int(bn.sum() + be.sum()) // budget)  # the even split was not
+
+
+def test_fill_store_checks_each_class_against_its_bound():
+  """fill_store samples every strided class once, appends it, and refuses a
+  class whose sampled count exceeds the class's record bound (the sampler
+  holds one class at a time; the trainer's loads are sized from it)."""
+  from hypergraphembedding_amd.embedding import fill_store
+
+  class FakeStore:
+    def __init__(self):
+      self.n, self.appends, self.cap = 0, 0, None
+
+    def store_reset(self, cap):
+      self.n, self.cap = 0, cap
+
+    def store_append(self):
+      self.appends += 1
+
+    def store_info(self):
+      return (self.n, 1, 5, 0)
+
+  bn = np.full(100, 4, np.int64)
+  be = np.full(40, 4, np.int64)
+  ctx = FakeStore()
+  seen = []
+
+  def ok(off, stride):
+    seen.append((off, stride))
+    m = int(bn[off::stride].sum() + be[off::stride].sum())
+    ctx.n += m
+    return m
+
+  assert fill_store(ctx, None, ok, bn, be, 100) == int(bn.sum() + be.sum())
+  assert ctx.cap == int(bn.sum() + be.sum())
+  assert ctx.appends == len(seen) and sorted(o for o, _ in seen) == list(range(seen[0][1]))
+
+  def too_many(off, stride):
+    return int(bn[off::stride].sum() + be[off::stride].sum()) + 1
+
+  with pytest.raises(AssertionError):
+    fill_store(FakeStore(), None, too_many, bn, be, 100)
