@@ -81,7 +81,7 @@ extern "C" int hgx_destroy(hgx_ctx *ctx) {
                     &ctx->s3, &ctx->s4, &ctx->s5, &ctx->s6, &ctx->s7,
                     &ctx->feat_n, &ctx->feat_e, &ctx->cn_p, &ctx->cn_j,
                     &ctx->cn_v, &ctx->ce_p, &ctx->ce_j, &ctx->ce_v,
-                    &ctx->hw_n, &ctx->hw_e, &ctx->hw_self, &ctx->store,
+                    &ctx->hw_n, &ctx->hw_e, &ctx->hw_self, &ctx->bloom_off, &ctx->bloom_bits, &ctx->store,
                     &ctx->st_sel, &ctx->st_keys, &ctx->st_vals, &ctx->st_tmp,
                     &ctx->st_hist};
   for (DevBuf *b : bufs) hgx_release(*b);
@@ -260,6 +260,7 @@ extern "C" int hgx_upload_incidence(hgx_ctx *ctx, int32_t N, int32_t E,
   ctx->n_rec = 0;
   ctx->smp_family = -1;
   ctx->rec_in_order = false;
+  ctx->bloom_ok = false;  // member filters of the previous incidence
   ctx->n_store = 0;  // stored records name rows of the previous incidence
   ctx->st_hist_ok = false;
   ctx->store_family = -1;

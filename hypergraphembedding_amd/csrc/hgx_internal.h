@@ -142,6 +142,8 @@ struct hgx_ctx {
   // HOBE per-incidence distance weights (node-major, edge-major) and each
   // edge's largest weight, built from the current alg coords
   DevBuf hw_n, hw_e, hw_self;
+  DevBuf bloom_off, bloom_bits;  // per-edge member filters (hgx_sample.hip)
+  bool bloom_ok = false;
 
   // ---- records (SamplesToModelInput layout) ----
   int64_t n_rec = 0;

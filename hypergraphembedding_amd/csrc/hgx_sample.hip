@@ -200,14 +200,76 @@ __device__ int first_common(const int *a, int na, const int *b, int nb) {
 // pressure). A merge of the two sorted member lists measured slower (one
 // dependent load per step over both lists): 3.0 s.
 constexpr int kProbeWays = 8;
-__device__ int edges_min_common(const Csr &A, const Csr &AT, int x, int y) {
+constexpr int kBloomWays = 16;
+
+// Blocked Bloom filters of the edges' member sets (built once per incidence,
+// ensure_bloom): per edge a power of two of 64-byte blocks, >= 16 bits per
+// member; a member sets 3 bits of one block chosen by its hash. A member
+// whose 3 bits are not all set is not in the edge, so its binary search is
+// skipped (~0.5-1 % false positives): a chunk of 8 probes then costs two
+// round trips (ids, filter words) instead of ~7. The answer is the exact
+// one (a positive still takes the search).
+struct Bloom {
+  const long long *off;  // first 32-bit word of edge e's filter, E + 1
+  const unsigned *bits;
+};
+__device__ __forceinline__ uint64_t bloom_hash(int u) {
+  return hgx::mix64((uint64_t)(uint32_t)u ^ 0x426c6f6f6d4d656dull);
+}
+
+__device__ int edges_min_common(const Csr &A, const Csr &AT, int x, int y,
+                                const Bloom &B = Bloom{nullptr, nullptr}) {
   if (x == y) return AT.rp[x + 1] > AT.rp[x] ? AT.col[AT.rp[x]] : INT_MAX;
   if (AT.rp[x + 1] - AT.rp[x] > AT.rp[y + 1] - AT.rp[y]) {
     const int t = x;
     x = y;
     y = t;
   }
+  const unsigned *fy = nullptr;
+  unsigned bmask = 0;
+  if (B.bits) {
+    const long long o = B.off[y];
+    fy = B.bits + o;
+    bmask = (unsigned)((B.off[y + 1] - o) / 16 - 1);  // blocks - 1
+  }
   const int xe = AT.rp[x + 1];
+  if (fy) {
+    // kBloomWays members filtered at once (ids, then their filter words),
+    // the rare positives searched one by one in ascending order
+    for (int t = AT.rp[x]; t < xe; t += kBloomWays) {
+      int u[kBloomWays];
+#pragma unroll
+      for (int k = 0; k < kBloomWays; k++) u[k] = t + k < xe ? AT.col[t + k] : -1;
+      unsigned pass = 0;
+      unsigned w0[kBloomWays], w1[kBloomWays], w2[kBloomWays];
+      unsigned s0[kBloomWays], s1[kBloomWays], s2[kBloomWays];
+#pragma unroll
+      for (int k = 0; k < kBloomWays; k++) {
+        const uint64_t h = bloom_hash(u[k]);
+        const unsigned *blk = fy + 16 * ((unsigned)(h >> 40) & bmask);
+        s0[k] = (unsigned)h & 511;
+        s1[k] = (unsigned)(h >> 9) & 511;
+        s2[k] = (unsigned)(h >> 18) & 511;
+        w0[k] = u[k] >= 0 ? blk[s0[k] >> 5] : 0u;
+        w1[k] = u[k] >= 0 ? blk[s1[k] >> 5] : 0u;
+        w2[k] = u[k] >= 0 ? blk[s2[k] >> 5] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < kBloomWays; k++)
+        pass |= ((w0[k] >> (s0[k] & 31)) & (w1[k] >> (s1[k] & 31)) & (w2[k] >> (s2[k] & 31)) &
+                 1u) << k;
+      while (pass) {
+        const int k = __builtin_ctz(pass);
+        pass &= pass - 1;
+        int uk = 0;
+#pragma unroll
+        for (int j = 0; j < kBloomWays; j++)
+          if (j == k) uk = u[j];
+        if (find_sorted(A.col, A.rp[uk], A.rp[uk + 1], y) >= 0) return uk;
+      }
+    }
+    return INT_MAX;
+  }
   for (int t = AT.rp[x]; t < xe; t += kProbeWays) {
     int u[kProbeWays], lo[kProbeWays], hi[kProbeWays], end[kProbeWays];
 #pragma unroll
@@ -249,9 +311,10 @@ __device__ int edges_min_common(const Csr &A, const Csr &AT, int x, int y) {
 
 // (v, e) in A A^T A (equivalently (e, v) in A^T A A^T): some edge of v
 // shares a node with e. E(v) is walked in ascending id order.
-__device__ bool ne3_member(const Csr &A, const Csr &AT, int v, int e) {
+__device__ bool ne3_member(const Csr &A, const Csr &AT, int v, int e,
+                           const Bloom &B = Bloom{nullptr, nullptr}) {
   for (int t = A.rp[v]; t < A.rp[v + 1]; t++)
-    if (edges_min_common(A, AT, A.col[t], e) != INT_MAX) return true;
+    if (edges_min_common(A, AT, A.col[t], e, B) != INT_MAX) return true;
   return false;
 }
 
@@ -507,6 +570,7 @@ struct RejectArgs {
                              // |l3 row of the incidence's column| (nnz + 1)
   int mode3;                 // 0 auto, 1 paths, 2 uniform columns
   int *stats;                // [0] rejection rows, [1] stalled, [3] uniform-mode rows
+  Bloom bloom;               // member filters of the edges (3-hop patterns)
   long long *diag;           // debug builds: per-row {pattern, row, mode, n1, q, W,
   int *diag_n;               // rounds, s_memrealtime ticks} (HGX_REJ_DIAG_OUT)
   int diag_cap;
@@ -610,7 +674,7 @@ __device__ bool nne_meets(const RejectArgs &A, const RejShared &S, int v, int c,
   if (probes == 0) return false;
   if (2ll * nc <= 5ll * probes) return members_meet_ev(A, S, c, lim);
   for (int j = 0; j < S.nev && S.evid[j] < lim; j++)
-    if (edges_min_common(A.A, A.AT, S.evid[j], c) != INT_MAX) return true;
+    if (edges_min_common(A.A, A.AT, S.evid[j], c, A.bloom) != INT_MAX) return true;
   return false;
 }
 
@@ -636,8 +700,8 @@ __device__ int draw_candidate(const RejectArgs &A, int r, int mode, bool small,
     const int c = (int)hgx::bounded(h, (uint32_t)A.ncols);
     if (hash_has(S.hash, c)) return INT_MAX;
     const bool in = A.pattern == PAT_NNE ? (S.nev >= 0 ? nne_meets(A, S, r, c, INT_MAX)
-                                                       : ne3_member(A.A, A.AT, r, c))
-                                         : ne3_member(A.A, A.AT, c, r);
+                                                       : ne3_member(A.A, A.AT, r, c, A.bloom))
+                                         : ne3_member(A.A, A.AT, c, r, A.bloom);
     return in ? c : INT_MAX;
   }
   // uniform path: level-1 entity m1 and the path offset w1 inside it
@@ -683,7 +747,7 @@ __device__ int draw_candidate(const RejectArgs &A, int r, int mode, bool small,
     for (int t = b1; t < A.l1.rp[r + 1]; t++) {
       const int e1 = A.l1.col[t];
       if (e1 > m1) break;
-      const int u = edges_min_common(A.A, A.AT, e1, c);
+      const int u = edges_min_common(A.A, A.AT, e1, c, A.bloom);
       if (u != INT_MAX) return (e1 == m1 && u == m2) ? c : INT_MAX;
     }
     return INT_MAX;
@@ -1082,6 +1146,71 @@ int expand_pass(hgx_ctx *ctx, const ExpandArgs &base, const int *rows, int n,
   return rc;
 }
 
+// filter words of edge e: 16 per 64-byte block, a power of two of blocks
+// holding >= 16 bits per member
+__global__ void bloom_words(const int *rp_e, int E, long long *words) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x) {
+    const long long want = (16ll * (rp_e[e + 1] - rp_e[e]) + 511) / 512;
+    long long b = 1;
+    while (b < want) b <<= 1;
+    words[e] = 16 * b;
+  }
+}
+
+// the 3 bits of every incidence (edge of incidence t by binary search)
+__global__ void bloom_set(const int *rp_e, const int *col_e, int E, int64_t nnz,
+                          const long long *off, unsigned *bits) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nnz;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    int lo = 0, hi = E - 1;
+    while (lo < hi) {  // last edge e with rp_e[e] <= t
+      const int mid = (lo + hi + 1) >> 1;
+      if (rp_e[mid] <= t) lo = mid;
+      else hi = mid - 1;
+    }
+    const long long o = off[lo];
+    const unsigned bmask = (unsigned)((off[lo + 1] - o) / 16 - 1);
+    const uint64_t h = bloom_hash(col_e[t]);
+    unsigned *blk = bits + o + 16 * ((unsigned)(h >> 40) & bmask);
+    const unsigned s0 = (unsigned)h & 511, s1 = (unsigned)(h >> 9) & 511,
+                   s2 = (unsigned)(h >> 18) & 511;
+    atomicOr(&blk[s0 >> 5], 1u << (s0 & 31));
+    atomicOr(&blk[s1 >> 5], 1u << (s1 & 31));
+    atomicOr(&blk[s2 >> 5], 1u << (s2 & 31));
+  }
+}
+
+int ensure_bloom(hgx_ctx *ctx) {
+  if (ctx->bloom_ok) return HGX_OK;
+  const int E = ctx->E;
+  HGX_TRY(hgx_ensure(ctx, ctx->bloom_off, sizeof(long long) * (E + 1)));
+  long long *off = ctx->bloom_off.as<long long>();
+  hipLaunchKernelGGL(bloom_words, dim3(grid_for(E, 256, 65536)), dim3(256), 0,
+                     ctx->stream, ctx->rp_e.as<int>(), E, off);
+  HGX_LAUNCH_CHECK(ctx);
+  HGX_HIP(ctx, hipMemsetAsync(off + E, 0, sizeof(long long), ctx->stream));
+  size_t tmp = 0;
+  HGX_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, off, off, E + 1, ctx->stream));
+  HGX_TRY(hgx_ensure(ctx, ctx->s7, tmp + 256));
+  HGX_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(ctx->s7.p, tmp, off, off, E + 1, ctx->stream));
+  long long words = 0;
+  HGX_HIP(ctx, hipMemcpyAsync(&words, off + E, sizeof(long long), hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  HGX_TRY(hgx_ensure(ctx, ctx->bloom_bits, sizeof(unsigned) * (size_t)(words + 16)));
+  HGX_HIP(ctx, hipMemsetAsync(ctx->bloom_bits.p, 0, sizeof(unsigned) * (size_t)(words + 16),
+                              ctx->stream));
+  if (ctx->nnz > 0) {
+    hipLaunchKernelGGL(bloom_set, dim3(grid_for(ctx->nnz, 256, 65536)), dim3(256), 0,
+                       ctx->stream, ctx->rp_e.as<int>(), ctx->col_e.as<int>(), E, ctx->nnz,
+                       off, ctx->bloom_bits.as<unsigned>());
+    HGX_LAUNCH_CHECK(ctx);
+  }
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->bloom_ok = true;
+  return HGX_OK;
+}
+
 int run_pattern(hgx_ctx *ctx, int pattern, const int32_t *host_quota,
                 int quota_all, uint64_t seed, PatOut &po) {
   const int N = ctx->N, E = ctx->E;
@@ -1097,6 +1226,8 @@ int run_pattern(hgx_ctx *ctx, int pattern, const int32_t *host_quota,
     case PAT_NNE: a.nrows = N; a.ncols = E; a.l1 = A; a.l2 = AT; a.l3 = A; a.levels = 3; break;
     default: a.nrows = E; a.ncols = N; a.l1 = AT; a.l2 = A; a.l3 = AT; a.levels = 3; break;
   }
+  // (before any work is queued: the build may grow the shared scratch)
+  if (a.levels == 3 && ctx->tune.sample_reject_w > 0) HGX_TRY(ensure_bloom(ctx));
   const int R = a.nrows;
   po.nrows = R;
   HGX_TRY(hgx_ensure(ctx, po.q, sizeof(int) * (R + 1)));
@@ -1192,6 +1323,8 @@ int run_pattern(hgx_ctx *ctx, int pattern, const int32_t *host_quota,
     r.ps = ps.as<int64_t>();
     r.mode3 = ctx->tune.sample_mode3;
     r.stats = ctr + 5;
+    if (a.levels == 3)
+      r.bloom = Bloom{ctx->bloom_off.as<long long>(), ctx->bloom_bits.as<unsigned>()};
     DevBuf diag;
 #ifdef HGX_DEBUG_KNOBS
     const char *diag_out = hgx_debug_env_str("HGX_REJ_DIAG_OUT");
