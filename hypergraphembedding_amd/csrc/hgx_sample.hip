@@ -200,7 +200,7 @@ __device__ int first_common(const int *a, int na, const int *b, int nb) {
 // pressure). A merge of the two sorted member lists measured slower (one
 // dependent load per step over both lists): 3.0 s.
 constexpr int kProbeWays = 8;
-constexpr int kBloomWays = 16;
+constexpr int kBloomWays = 8;
 
 // Blocked Bloom filters of the edges' member sets (built once per incidence,
 // ensure_bloom): per edge a power of two of 64-byte blocks, >= 16 bits per
@@ -235,7 +235,8 @@ __device__ int edges_min_common(const Csr &A, const Csr &AT, int x, int y,
   const int xe = AT.rp[x + 1];
   if (fy) {
     // kBloomWays members filtered at once (ids, then their filter words),
-    // the rare positives searched one by one in ascending order
+    // the rare positives searched one by one in ascending order (C4 2%
+    // slice: 0.94 s at 4, 0.89 s at 8, 0.975 s at 16 -- register pressure)
     for (int t = AT.rp[x]; t < xe; t += kBloomWays) {
       int u[kBloomWays];
 #pragma unroll
