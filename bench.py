@@ -29,7 +29,25 @@ incidence already resident in HBM. Reported beside it, from the same run:
 Multi-GPU: alg-dist is node-row sharded with RCCL all-reduces
 (algebraic_distance.alg_dist_sharded); training runs as independent replicas
 (synchronous batch-256 Adagrad does not partition), so `value`
-is weak-scaled: total records trained by all ranks / max wall time.
+is weak-scaled: total records trained by all ranks / max wall time. Beside
+it, `distinct_records_per_s` (the records of ONE embedding per second) and
+`c4_time_to_embedding_s` (the C4 slice's alg-dist + sampling + epoch) do not
+count replicas.
+
+Rank launch. Under torch.distributed.run (WORLD_SIZE in the environment)
+this process is one rank. A plain `python bench.py --gpus N` with N > 1 and
+no WORLD_SIZE is the launcher: before any GPU call it starts N children of
+this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+MASTER_PORT set, one GPU each), forwards rank 0's JSON line, and exits
+non-zero if any child fails or `--launch-timeout` passes (the others are
+then killed). A `--gpus` that disagrees with WORLD_SIZE is refused. The
+line carries `ranks_seen` (dist.get_world_size()) and `devices_seen`
+(torch.cuda.device_count()).
+
+--c4-full (opt-in, not in the default run; ~5 min on one GPU): the WHOLE
+C4 pipeline timed as `c4_full` -- alg-dist (k=10, 20 iterations; sharded at
+N > 1), HOBE sampling of every row into the record store, one
+global-shuffle d=256 epoch from the store (embedding.py:389-416's path).
 """
 
 import argparse
@@ -59,7 +77,13 @@ PMC_TRAIN_D256 = os.path.join(ROOT, "profiles", "r05", "pmc_train_d256.json")
 
 def parse():
   p = argparse.ArgumentParser()
-  p.add_argument("--gpus", type=int, default=1)
+  p.add_argument("--gpus", type=int, default=None,
+                 help="ranks (default: WORLD_SIZE, else 1); > 1 without "
+                      "WORLD_SIZE starts that many child ranks")
+  p.add_argument("--launch-timeout", type=float, default=3000.0,
+                 help="launcher: seconds before unfinished ranks are killed")
+  p.add_argument("--launch-selftest", choices=("ok", "fail"), default=None,
+                 help=argparse.SUPPRESS)  # launcher test: trivial children
   p.add_argument("--edge-ranges", type=int, default=4,
                  help="C4 sharded alg-dist: edge ranges the exchange is "
                       "pipelined over (1 = one all-reduce per iteration)")
@@ -151,11 +175,149 @@ def timed_runs(fn, reps):
   return out
 
 
+def _free_port():
+  import socket
+  with socket.socket() as s:
+    s.bind(("127.0.0.1", 0))
+    return s.getsockname()[1]
+
+
+def _kill_group(p, sig):
+  import signal
+  try:
+    os.killpg(p.pid, sig)
+  except (ProcessLookupError, PermissionError):
+    pass
+
+
+def launch_ranks(n, timeout):
+  """Start n ranks of this script as child processes and wait for them.
+
+  The launcher itself never initialises a GPU (it imports no torch) and never
+  execs: each rank is a fresh `python bench.py ...` child with RANK /
+  LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, in its own process
+  group. Rank 0's stdout (the JSON line) is forwarded to ours; the other
+  ranks' stdout goes to our stderr. The first child that exits non-zero, or
+  the timeout, ends the run: every remaining child group is killed and the
+  status is returned (124 on timeout, 1 if rank 0 printed no JSON line)."""
+  import signal
+  import subprocess
+  import threading
+  port = os.environ.get("MASTER_PORT") or str(_free_port())
+  argv = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+  procs = []
+  seen = {"json": 0}
+
+  def pump(stream):
+    for line in iter(stream.readline, b""):
+      s = line.decode(errors="replace")
+      if s.lstrip().startswith("{"):
+        seen["json"] += 1
+      sys.stdout.write(s)
+      sys.stdout.flush()
+    stream.close()
+
+  def stop_all(sig):
+    for p in procs:
+      if p.poll() is None:
+        _kill_group(p, sig)
+
+  def on_term(signum, frame):
+    raise SystemExit(128 + signum)
+
+  old = signal.signal(signal.SIGTERM, on_term)
+  pump_t = None
+  rc = 0
+  try:
+    for r in range(n):
+      env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                 LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", ROLE_RANK=str(r),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+      p = subprocess.Popen(argv, env=env, start_new_session=True,
+                           stdout=subprocess.PIPE if r == 0 else sys.stderr)
+      procs.append(p)
+      if r == 0:
+        pump_t = threading.Thread(target=pump, args=(p.stdout,), daemon=True)
+        pump_t.start()
+    print(f"[launcher] {n} ranks started, MASTER_PORT {port}", file=sys.stderr,
+          flush=True)
+    t0 = time.time()
+    while True:
+      codes = [p.poll() for p in procs]
+      bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+      if bad:
+        r, c = bad[0]
+        print(f"[launcher] rank {r} exited with status {c}; stopping the "
+              f"other ranks", file=sys.stderr, flush=True)
+        rc = c if c > 0 else 128 - c
+        break
+      if all(c == 0 for c in codes):
+        break
+      if time.time() - t0 > timeout:
+        print(f"[launcher] ranks still running after {timeout:.0f} s; "
+              f"killing them", file=sys.stderr, flush=True)
+        rc = 124
+        break
+      time.sleep(0.2)
+  finally:
+    stop_all(signal.SIGTERM)
+    deadline = time.time() + 10
+    for p in procs:
+      try:
+        p.wait(timeout=max(0.1, deadline - time.time()))
+      except subprocess.TimeoutExpired:
+        _kill_group(p, signal.SIGKILL)
+        p.wait()
+    if pump_t is not None:
+      pump_t.join(timeout=10)
+    signal.signal(signal.SIGTERM, old)
+  if rc == 0 and seen["json"] == 0:
+    print("[launcher] rank 0 printed no JSON line", file=sys.stderr, flush=True)
+    rc = 1
+  return rc
+
+
+def launch_selftest(mode, world, rank):
+  """--launch-selftest child: a gloo rendezvous on the CPU (no GPU), rank 0
+  prints the ranks it saw; in mode 'fail' the last rank exits 3 and rank 0
+  blocks as a rank waiting on a collective would."""
+  import torch
+  import torch.distributed as dist
+  print(f"[selftest] rank {rank} of {world}", file=sys.stderr, flush=True)
+  if mode == "fail" and world > 1:
+    if rank == world - 1:
+      sys.exit(3)
+    time.sleep(600)
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  got = [None] * world
+  dist.all_gather_object(got, (rank, int(os.environ["LOCAL_RANK"]),
+                               int(os.environ["WORLD_SIZE"])))
+  if rank == 0:
+    print(json.dumps({"selftest": mode, "ranks_seen": dist.get_world_size(),
+                      "ranks": got}), flush=True)
+  dist.destroy_process_group()
+
+
 def main():
   args = parse()
-  world = int(os.environ.get("WORLD_SIZE", "1"))
+  env_world = os.environ.get("WORLD_SIZE")
+  if env_world is None:
+    want = args.gpus or 1
+    if want > 1:
+      # the launcher: no GPU call in this process (see launch_ranks)
+      sys.exit(launch_ranks(want, args.launch_timeout))
+    world = 1
+  else:
+    world = int(env_world)
+    if args.gpus is not None and args.gpus != world:
+      print(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world}",
+            file=sys.stderr, flush=True)
+      sys.exit(2)
   rank = int(os.environ.get("RANK", "0"))
   local = int(os.environ.get("LOCAL_RANK", "0"))
+  if args.launch_selftest:
+    launch_selftest(args.launch_selftest, world, rank)
+    return
   dist = None
   if args.one_device:
     local = 0
@@ -426,6 +588,11 @@ def main():
   if not args.no_c4:
     c4 = bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded)
 
+  ranks_seen = dist.get_world_size() if dist is not None else 1
+  import torch
+  devices_seen = torch.cuda.device_count()
+  hobe4 = (c4 or {}).get("hobe_d256") or {}
+  tte4 = (hobe4.get("time_to_embedding_s") or {}).get("total_s")
   if rank == 0:
     out = {
         "metric": METRIC,
@@ -435,6 +602,13 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+        "ranks_seen": ranks_seen,
+        "devices_seen": devices_seen,
+        # the records of ONE embedding per second (value counts every
+        # replica's identical epoch) and the C4 slice's wall time to an
+        # embedding (alg-dist + sampling + one epoch, sharded at N > 1)
+        "distinct_records_per_s": round(n * args.steps / elapsed, 1),
+        "c4_time_to_embedding_s": tte4,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -91,6 +91,7 @@ SIGNATURES = {
     "hgx_store_write": (_int, [_vp, _i64, _vp, _int, _int, _int, _u64]),
     "hgx_store_plan": (_int, [_vp, _u64, _i64, _pint, _vp, _vp]),
     "hgx_store_load": (_int, [_vp, _u64, _i32, _i32, _int, _int, _pi64]),
+    "hgx_store_release": (_int, [_vp]),
     "hgx_model_init": (_int, [_vp, _int, _i64, _i64, _u64, _vp, _vp]),
     "hgx_model_get": (_int, [_vp, _vp, _vp]),
     "hgx_model_get_rows": (_int, [_vp, _int, _i64, _vp, _vp]),
@@ -479,6 +480,10 @@ class Context:
   # ---- compact record store (streams larger than HBM, hgx_store_*) ----
   def store_reset(self, capacity=0):
     self._chk(lib().hgx_store_reset(self.h, int(capacity)))
+
+  def store_release(self):
+    """Free the store, its load scratch and the loaded records."""
+    self._chk(lib().hgx_store_release(self.h))
 
   def store_append(self):
     """Pack the records of the last sample_fobe / sample_hobe call."""

@@ -260,6 +260,7 @@ extern "C" int hgx_upload_incidence(hgx_ctx *ctx, int32_t N, int32_t E,
   ctx->n_rec = 0;
   ctx->smp_family = -1;
   ctx->rec_in_order = false;
+  ctx->store_carry = 0;
   ctx->bloom_ok = false;  // member filters of the previous incidence
   ctx->n_store = 0;  // stored records name rows of the previous incidence
   ctx->st_hist_ok = false;

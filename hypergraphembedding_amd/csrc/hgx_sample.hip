@@ -1398,6 +1398,7 @@ int alloc_records(hgx_ctx *ctx, int64_t n, int K) {
   ctx->n_rec = n;
   ctx->K = K;
   ctx->rec_in_order = false;
+  ctx->store_carry = 0;  // no store batch tail survives a rewrite
   ctx->smp_family = -1;  // set by the sampler once its records are complete
   return HGX_OK;
 }

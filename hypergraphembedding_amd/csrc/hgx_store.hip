@@ -406,6 +406,33 @@ extern "C" int hgx_store_reset(hgx_ctx *ctx, int64_t capacity) {
   return HGX_OK;
 }
 
+// Frees the store, its load scratch and the record buffers the last load
+// filled (at C4: the ~71 GB store, ~19 GB of st_* scratch and a ~36 GB
+// chunk), so the device's HBM is back for the next embedding or the
+// combiner. The context stays usable: the next reset / append / write grows
+// the store again.
+extern "C" int hgx_store_release(hgx_ctx *ctx) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  for (DevBuf *b : {&ctx->store, &ctx->st_sel, &ctx->st_keys, &ctx->st_vals, &ctx->st_tmp,
+                    &ctx->st_hist, &ctx->rec_idx, &ctx->rec_tgt})
+    hgx_release(*b);
+  ctx->cap_store = 0;
+  ctx->n_store = 0;
+  ctx->store_family = -1;
+  ctx->store_K = 0;
+  ctx->store_seed = 0;
+  ctx->store_carry = 0;
+  ctx->st_hist_ok = false;
+  ctx->n_rec = 0;
+  ctx->smp_family = -1;
+  ctx->rec_in_order = false;
+  ctx->rec_bounds[0] = ctx->rec_bounds[1] = 0;
+  ctx->n_rec_blocks = 1;
+  return HGX_OK;
+}
+
 // the store's sampler family / K / seed: set by the first records, equal
 // for every later one
 static int store_adopt(hgx_ctx *ctx, int family, int K, uint64_t seed) {

@@ -2036,6 +2036,7 @@ extern "C" int hgx_records_set(hgx_ctx *ctx, int64_t n, int K,
   ctx->K = K;
   ctx->smp_family = -1;
   ctx->rec_in_order = false;
+  ctx->store_carry = 0;  // no store batch tail survives a rewrite
   ctx->rec_bounds[0] = 0;
   ctx->rec_bounds[1] = n;
   ctx->n_rec_blocks = 1;
@@ -2098,6 +2099,7 @@ extern "C" int hgx_records_import(hgx_ctx *ctx, int64_t n, int K,
   ctx->K = K;
   ctx->smp_family = -1;
   ctx->rec_in_order = false;
+  ctx->store_carry = 0;  // no store batch tail survives a rewrite
   if (nblocks > 0) {
     for (int i = 0; i <= nblocks; i++) ctx->rec_bounds[i] = bounds[i];
     ctx->n_rec_blocks = nblocks;
@@ -2139,6 +2141,7 @@ extern "C" int hgx_records_copy(hgx_ctx *dst, hgx_ctx *src) {
   dst->smp_family = src->smp_family;
   dst->smp_seed = src->smp_seed;
   dst->rec_in_order = src->rec_in_order;
+  dst->store_carry = 0;  // the tail (if any) stays with src's buffer
   dst->n_rec_blocks = src->n_rec_blocks;
   for (int i = 0; i <= src->n_rec_blocks; i++) dst->rec_bounds[i] = src->rec_bounds[i];
   return HGX_OK;

@@ -163,12 +163,19 @@ def fill_store(ctx, inc, chunk_fn, bound_n, bound_e, budget):
   ctx.store_reset(int(bn.sum() + be.sum()))
   for off, stride in chunks:
     m = chunk_fn(off, stride)
-    cap = int(bn[off::stride].sum() + be[off::stride].sum())
-    assert m is None or m <= cap, (
-        "row class %d/%d sampled %d records, above its bound %d" %
-        (off, stride, m, cap))
+    check_class_bound(m, bn, be, off, stride)
     ctx.store_append()
   return ctx.store_info()[0]
+
+
+def check_class_bound(m, bn, be, off, stride):
+  """A row class must not sample more records than its rows' bounds (the
+  store and the chunk plan are sized by them): a real exception, not an
+  assert, so python -O keeps it."""
+  cap = int(bn[off::stride].sum() + be[off::stride].sum())
+  if m is not None and m > cap:
+    raise RuntimeError("row class %d/%d sampled %d records, above its bound "
+                       "%d" % (off, stride, m, cap))
 
 
 def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
@@ -195,12 +202,17 @@ def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
       seed = numpy_seed()
       sample = chunk_sampler_fn(inc, ctx)
       chunk = min(budget, STORE_CHUNK)
-      fill_store(ctx, inc, lambda off, stride: sample(seed, off, stride), bn,
-                 be, chunk)
-      model = Hg2vModel(inc.N + 1, inc.E + 1, dimension, num_neighbors, loss,
-                        act, ctx=ctx)
-      model.fit_store(chunk, batch_size=fit_batch_size, epochs=fit_epochs)
-      node_w, edge_w = model.get_weights()
+      try:
+        fill_store(ctx, inc, lambda off, stride: sample(seed, off, stride),
+                   bn, be, chunk)
+        model = Hg2vModel(inc.N + 1, inc.E + 1, dimension, num_neighbors,
+                          loss, act, ctx=ctx)
+        model.fit_store(chunk, batch_size=fit_batch_size, epochs=fit_epochs)
+        node_w, edge_w = model.get_weights()
+      finally:
+        # the store (~71 GB at C4), its load scratch and the last chunk's
+        # records go back to the device, also when sampling or fit raises
+        ctx.store_release()
       return coords_to_embedding(inc, node_w[1:], edge_w[1:], dimension, "")
   records = sampler_fn(inc, ctx)
   if debug_summary_path is not None:
@@ -370,7 +382,14 @@ def hobe_sharded(inc, dimension, num_neighbors=5, num_samples=200,
   ctx.alg_set(x, y)
   st["alg_s"] = time.perf_counter() - t0
   sample_seed, model_seed, fit_seed = _broadcast_seeds(3, group, dev)
-  budget = RECORDS_BUDGET if records_budget is None else records_budget
+  # resident at world > 1 only up to half the single-GPU budget: the
+  # row-sharded sampler holds its gather buffers, the gathered stream and
+  # the context's copy at once (~2.5x the stream); larger streams take the
+  # store path, whose per-rank peak is the single-GPU one
+  if records_budget is not None:
+    budget = records_budget
+  else:
+    budget = RECORDS_BUDGET if world == 1 else RECORDS_BUDGET // 2
   bn = np.full(inc.N, 2 * num_samples, np.int64)
   be = np.full(inc.E, 2 * num_samples, np.int64)
   model = Hg2vModel(inc.N + 1, inc.E + 1, dimension, num_neighbors,
@@ -387,15 +406,19 @@ def hobe_sharded(inc, dimension, num_neighbors=5, num_samples=200,
   else:
     chunk = min(budget, STORE_CHUNK)
     chunks = _row_chunks(bn, be, chunk)
-    n = sharded_store_fill(inc, num_neighbors, num_samples, chunks, ctx=ctx,
-                           seed=sample_seed, kind="hobe", group=group,
-                           device=dev, capacity=int(bn.sum() + be.sum()))
-    st["sampling_s"] = time.perf_counter() - t0
-    st["records"] = n
-    st["sampling_chunks"] = len(chunks)
-    t0 = time.perf_counter()
-    model.fit_store(chunk, batch_size=batch_size, epochs=epochs,
-                    seed=fit_seed % (2**32))
+    try:
+      n = sharded_store_fill(inc, num_neighbors, num_samples, chunks, ctx=ctx,
+                             seed=sample_seed, kind="hobe", group=group,
+                             device=dev, capacity=int(bn.sum() + be.sum()),
+                             row_bounds=(bn, be))
+      st["sampling_s"] = time.perf_counter() - t0
+      st["records"] = n
+      st["sampling_chunks"] = len(chunks)
+      t0 = time.perf_counter()
+      model.fit_store(chunk, batch_size=batch_size, epochs=epochs,
+                      seed=fit_seed % (2**32))
+    finally:
+      ctx.store_release()
   st["train_s"] = time.perf_counter() - t0
   node_w, edge_w = model.get_weights()
   return node_w[1:], edge_w[1:]

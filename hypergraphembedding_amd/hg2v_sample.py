@@ -257,7 +257,9 @@ def sample_sharded(inc, num_neighbors, num_samples, ctx=None, seed=0,
 
 def sharded_store_fill(inc, num_neighbors, num_samples, chunks, ctx=None,
                        seed=0, kind="hobe", node_quota=None, edge_quota=None,
-                       group=None, device=None, capacity=0):
+                       group=None, device=None, capacity=0,
+                       neg_node_quota=None, neg_edge_quota=None,
+                       row_bounds=None):
   """Sample a record stream too large for HBM once into every rank's record
   store (hgx_store_*), the sampling row-sharded over the ranks of a
   torch.distributed group. For each strided row class
@@ -271,16 +273,24 @@ def sharded_store_fill(inc, num_neighbors, num_samples, chunks, ctx=None,
   exactly the records a single process samples, in another order -- which
   the store's epoch order does not see (it is keyed by record identity):
   Hg2vModel.fit_store then trains the same epochs on every rank. Returns
-  the records in the store."""
+  the records in the store. FOBE takes its negative quotas
+  (neg_node_quota / neg_edge_quota, both or neither), sharded like the
+  positive ones. row_bounds = (per node row, per edge row) record bounds:
+  each rank's share of a class is checked against them (RuntimeError)."""
   import torch
   import torch.distributed as dist
-  ctx = ctx or get_context()
-  world, rank = dist.get_world_size(group), dist.get_rank(group)
   K = num_neighbors
+  if (neg_node_quota is None) != (neg_edge_quota is None):
+    raise ValueError("give both negative quotas or neither")
+  if neg_node_quota is not None and kind != "fobe":
+    raise ValueError("negative quotas are a FOBE (BooleanSamples) option")
   if node_quota is None:  # HOBE: S per row (hg2v_sample.py:659-703)
-    assert kind == "hobe"
+    if kind != "hobe":
+      raise ValueError("FOBE sharded sampling needs its row quotas")
     node_quota = np.full(inc.N, num_samples, np.int32)
     edge_quota = np.full(inc.E, num_samples, np.int32)
+  ctx = ctx or get_context()
+  world, rank = dist.get_world_size(group), dist.get_rank(group)
   gpu = device is None or torch.device(device).type == "cuda"
   dev = torch.device("cuda", ctx.device) if device is None else torch.device(device)
   ctx.store_reset(capacity)
@@ -308,9 +318,20 @@ def sharded_store_fill(inc, num_neighbors, num_samples, chunks, ctx=None,
     eq = row_class_quota(edge_quota, *mine)
     before = ctx.store_info()[0]
     if kind == "hobe":
-      ctx.sample_hobe(seed, K, num_samples, node_q=nq, edge_q=eq)
+      got_n = ctx.sample_hobe(seed, K, num_samples, node_q=nq, edge_q=eq)
+    elif neg_node_quota is not None:
+      got_n = ctx.sample_fobe(seed, K, nq, eq,
+                              row_class_quota(neg_node_quota, *mine),
+                              row_class_quota(neg_edge_quota, *mine))
     else:
-      ctx.sample_fobe(seed, K, nq, eq)
+      got_n = ctx.sample_fobe(seed, K, nq, eq)
+    if row_bounds is not None:
+      cap = int(np.asarray(row_bounds[0], np.int64)[mine[0]::mine[1]].sum() +
+                np.asarray(row_bounds[1], np.int64)[mine[0]::mine[1]].sum())
+      if got_n > cap:
+        raise RuntimeError("rank %d's share of row class %d/%d sampled %d "
+                           "records, above its bound %d" %
+                           (rank, off, stride, got_n, cap))
     ctx.store_append()
     new = ctx.store_info()[0] - before
     t = torch.tensor([new], dtype=torch.int64, device=dev)

@@ -279,7 +279,10 @@ int hgx_records_import(hgx_ctx *ctx, int64_t n, int K, const void *d_idx,
  *                               the stream's own tail (< batch records) is
  *                               kept for the next load. hgx_train then
  *                               trains the records in that order (no
- *                               shuffle). n_records = records to train. */
+ *                               shuffle). n_records = records to train.
+ *   hgx_store_release()         free the store, its load scratch and the
+ *                               loaded records (the embedders call it when
+ *                               fit_store returns or raises). */
 #define HGX_STORE_BINS 16384
 int hgx_store_reset(hgx_ctx *ctx, int64_t capacity);
 int hgx_store_append(hgx_ctx *ctx);
@@ -293,6 +296,7 @@ int hgx_store_plan(hgx_ctx *ctx, uint64_t epoch_seed, int64_t budget,
                    int *n_chunks, int32_t *bin_bounds, int64_t *counts);
 int hgx_store_load(hgx_ctx *ctx, uint64_t epoch_seed, int32_t bin_lo,
                    int32_t bin_hi, int batch, int last, int64_t *n_records);
+int hgx_store_release(hgx_ctx *ctx);
 
 /* ---- hg2v_weighting distance / span weights ------------------------------ *
  * hg2v_weighting.py:34-64 (WeightBySameTypeDistance), 67-103

@@ -191,22 +191,71 @@ def test_store_refuses_foreign_streams(ctx, plg):
     ctx.store_write(np.array([[9 << 28, 0, 0]], np.uint32), 1, 5, 1)
 
 
-def test_embed_takes_the_store_path(plg):
+def test_embed_takes_the_store_path(plg, monkeypatch):
   """EmbedHg2vAlgDist / EmbedHg2vBoolean with a record budget below the
   stream: sampled once into the store (strided row classes), trained in
-  global-shuffle epochs; every record trained once per epoch; the
-  embedding covers every node and edge; the loss falls."""
+  global-shuffle epochs; the embedding covers every node and edge. The
+  store, its scratch and the loaded records are released when the embed
+  returns (hgx_store_release)."""
   from hypergraphembedding_amd import embedding
   from hypergraphembedding_amd.runtime import get_context
+  filled = []
+  orig = embedding.fill_store
+
+  def spy(ctx, *a, **k):
+    n = orig(ctx, *a, **k)
+    filled.append((n, ctx.store_info()[1]))
+    return n
+  monkeypatch.setattr(embedding, "fill_store", spy)
   np.random.seed(3)
   emb = embedding.EmbedHg2vAlgDist(plg, 16, num_samples=20, epochs=3,
                                    records_budget=200_000)
   c = get_context()
-  n_store = c.store_info()[0]
-  assert n_store > 600_000
+  assert filled[-1][0] > 600_000 and filled[-1][1] == 1
+  assert c.store_info()[0] == 0 and c.records_info()[0] == 0
   assert len(emb.node) == plg.N and len(emb.edge) == plg.E
   np.random.seed(4)
   emb = embedding.EmbedHg2vBoolean(plg, 16, num_samples=10, epochs=2,
                                    records_budget=100_000)
-  assert c.store_info()[1] == 0 and c.store_info()[0] > 300_000
+  assert filled[-1][0] > 300_000 and filled[-1][1] == 0
+  assert c.store_info()[0] == 0
   assert len(emb.node) == plg.N
+
+
+def test_store_release_returns_the_memory(ctx, plg):
+  """hgx_store_release frees the store's HBM (device free memory comes
+  back) and leaves a usable context: the store grows again afterwards."""
+  import torch
+  ctx.upload(plg)
+  ctx.store_release()
+  free0 = torch.cuda.mem_get_info(ctx.device)[0]
+  ctx.store_reset(100_000_000)  # 1.2 GB of 12-byte entries
+  free1 = torch.cuda.mem_get_info(ctx.device)[0]
+  assert free0 - free1 >= 1_100_000_000
+  ctx.store_release()
+  free2 = torch.cuda.mem_get_info(ctx.device)[0]
+  assert free2 - free1 >= 1_100_000_000
+  assert ctx.store_info()[0] == 0
+  _hobe(ctx, plg)
+  ctx.store_reset(0)
+  ctx.store_append()
+  assert ctx.store_info()[0] == ctx.records_info()[0] > 0
+  ctx.store_release()
+  assert ctx.store_info()[0] == 0 and ctx.records_info()[0] == 0
+
+
+def test_record_writers_drop_the_store_tail(ctx, plg):
+  """A load keeps its batch tail for the next load; a record writer other
+  than the store (records_set here) overwrites the buffer the tail lived
+  in, so the next load must not prepend it."""
+  _hobe(ctx, plg)
+  ctx.store_reset(0)
+  ctx.store_append()
+  b, c = ctx.store_plan(5, 50_000)
+  assert c.size >= 2
+  m0 = ctx.store_load(5, b[0], b[1], 256, False)
+  assert m0 == c[0] - c[0] % 256
+  idx, tgt = ctx.records_get()
+  ctx.records_set(idx[:1000], tgt[:1000])
+  m1 = ctx.store_load(5, b[1], b[2], 256, True)
+  assert m1 == c[1]

@@ -269,5 +269,20 @@ def test_fill_store_checks_each_class_against_its_bound():
   def too_many(off, stride):
     return int(bn[off::stride].sum() + be[off::stride].sum()) + 1
 
-  with pytest.raises(AssertionError):
+  with pytest.raises(RuntimeError, match="above its bound"):
     fill_store(FakeStore(), None, too_many, bn, be, 100)
+
+
+def test_sharded_store_fill_argument_checks():
+  """FOBE needs its quotas; negative quotas come in pairs and only for FOBE
+  (checked before any collective)."""
+  from hypergraphembedding_amd.hg2v_sample import sharded_store_fill
+  q = np.ones(4, np.int32)
+  with pytest.raises(ValueError, match="needs its row quotas"):
+    sharded_store_fill(None, 2, 3, [(0, 1)], kind="fobe")
+  with pytest.raises(ValueError, match="both negative quotas"):
+    sharded_store_fill(None, 2, 3, [(0, 1)], kind="fobe", node_quota=q,
+                       edge_quota=q, neg_node_quota=q)
+  with pytest.raises(ValueError, match="FOBE"):
+    sharded_store_fill(None, 2, 3, [(0, 1)], kind="hobe", neg_node_quota=q,
+                       neg_edge_quota=q)
