@@ -589,8 +589,9 @@ def main():
     c4 = bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded)
 
   ranks_seen = dist.get_world_size() if dist is not None else 1
-  import torch
-  devices_seen = torch.cuda.device_count()
+  # HIP devices visible to this rank's libhgx (hipGetDeviceCount; torch's
+  # own HIP runtime is not initialised at N = 1)
+  devices_seen = _hgx.device_count()
   hobe4 = (c4 or {}).get("hobe_d256") or {}
   tte4 = (hobe4.get("time_to_embedding_s") or {}).get("total_s")
   if rank == 0:

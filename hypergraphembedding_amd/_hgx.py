@@ -46,6 +46,8 @@ SIGNATURES = {
     "hgx_version": (_int, []),
     "hgx_set_stream": (_int, [_vp, _vp]),
     "hgx_synchronize": (_int, [_vp]),
+    "hgx_device_count": (_int, [_pint]),
+    "hgx_mem_info": (_int, [_vp, _pi64, _pi64]),
     "hgx_set_tuning": (_int, [_vp, ctypes.c_char_p, _i64]),
     "hgx_upload_incidence": (_int, [_vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]),
     "hgx_alg_dist": (_int, [_vp, _int, _int, _vp, _vp]),
@@ -70,6 +72,9 @@ SIGNATURES = {
     "hgx_sample_fobe": (_int, [_vp, _u64, _int, _vp, _vp, _vp, _vp, _pi64]),
     "hgx_sample_hobe": (_int, [_vp, _u64, _int, _int, _pi64]),
     "hgx_sample_hobe_rows": (_int, [_vp, _u64, _int, _vp, _vp, _int, _pi64]),
+    "hgx_sample_fobe_mt": (_int, [_vp, _vp, _pint, _int, _vp, _vp, _vp, _vp,
+                                  _pi64]),
+    "hgx_sample_hobe_mt": (_int, [_vp, _vp, _pint, _int, _int, _pi64]),
     "hgx_sample_last_stats": (_int, [_vp, _pi64, _pi64]),
     "hgx_sample_uniform_rows": (_int, [_vp, _pi64]),
     "hgx_features_set": (_int, [_vp, _vp, _vp]),
@@ -193,6 +198,13 @@ def _c(a, dtype):
   return None if a is None else np.ascontiguousarray(a, dtype=dtype)
 
 
+def device_count():
+  """HIP devices visible to libhgx (hipGetDeviceCount)."""
+  n = ctypes.c_int()
+  lib().hgx_device_count(ctypes.byref(n))
+  return n.value
+
+
 class Context:
   """One device context (owns device memory and one HIP stream)."""
 
@@ -228,6 +240,12 @@ class Context:
 
   def synchronize(self):
     self._chk(lib().hgx_synchronize(self.h))
+
+  def mem_info(self):
+    """(free, total) bytes of the context's device (hipMemGetInfo)."""
+    f, t = ctypes.c_int64(), ctypes.c_int64()
+    self._chk(lib().hgx_mem_info(self.h, ctypes.byref(f), ctypes.byref(t)))
+    return f.value, t.value
 
   def set_tuning(self, key, value):
     """Pick between exact implementations (hgx_set_tuning): sample_reject_w,
@@ -389,6 +407,35 @@ class Context:
                                            _ptr(nq), _ptr(eq), S,
                                            ctypes.byref(n)))
     return n.value
+
+  def _mt_call(self, fn, *args):
+    """Run a numpy-seeded sampler on numpy's global RandomState: its MT19937
+    state goes in, the state the reference leaves behind comes back."""
+    st = np.random.get_state()
+    if st[0] != "MT19937":
+      raise ValueError("numpy's global RandomState is not MT19937")
+    key = np.array(st[1], dtype=np.uint32, copy=True)
+    pos = ctypes.c_int(int(st[2]))
+    n = ctypes.c_int64()
+    self._chk(fn(self.h, _ptr(key), ctypes.byref(pos), *args, ctypes.byref(n)))
+    np.random.set_state((st[0], key, pos.value, st[3], st[4]))
+    return n.value
+
+  def sample_fobe_mt(self, K, node_q, edge_q, neg_node_q=None, neg_edge_q=None):
+    """BooleanSamples drawing from numpy's global RandomState (the
+    reference's stream bit for bit; hgx_sample_fobe_mt)."""
+    nq, eq = _c(node_q, np.int32), _c(edge_q, np.int32)
+    nnq, neq = _c(neg_node_q, np.int32), _c(neg_edge_q, np.int32)
+    for q, n in ((nq, self.inc.N), (eq, self.inc.E), (nnq, self.inc.N),
+                 (neq, self.inc.E)):
+      assert q is None or q.size == n, "one quota per row"
+    return self._mt_call(lib().hgx_sample_fobe_mt, K, _ptr(nq), _ptr(eq),
+                         _ptr(nnq), _ptr(neq))
+
+  def sample_hobe_mt(self, K, S):
+    """AlgebraicDistanceSamples(run_in_parallel=False) drawing from numpy's
+    global RandomState (hgx_sample_hobe_mt)."""
+    return self._mt_call(lib().hgx_sample_hobe_mt, K, S)
 
   # weighted-Jaccard samplers
   def features_set(self, node_major, edge_major):

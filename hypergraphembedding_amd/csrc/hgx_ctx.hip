@@ -194,6 +194,24 @@ extern "C" int hgx_synchronize(hgx_ctx *ctx) {
   return HGX_OK;
 }
 
+extern "C" int hgx_device_count(int *n) {
+  if (!n) return HGX_EINVAL;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *n = c;
+  return HGX_OK;
+}
+
+extern "C" int hgx_mem_info(hgx_ctx *ctx, int64_t *free_bytes, int64_t *total_bytes) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  size_t f = 0, t = 0;
+  HGX_HIP(ctx, hipMemGetInfo(&f, &t));
+  if (free_bytes) *free_bytes = (int64_t)f;
+  if (total_bytes) *total_bytes = (int64_t)t;
+  return HGX_OK;
+}
+
 static int check_csr(hgx_ctx *ctx, const char *name, int32_t R, int32_t C,
                      int64_t nnz, const int32_t *rp, const int32_t *col) {
   HGX_CHECK(ctx, rp && (nnz == 0 || col), HGX_EINVAL, "%s: null pointer", name);

@@ -28,7 +28,7 @@ from .hg2v_sample import (_quotas, row_class_quota, sample_fobe, sample_hobe,
                           sample_jaccard)
 from .hypergraph_util import Incidence
 from .proto import HypergraphEmbedding
-from .runtime import get_context, numpy_seed
+from .runtime import check_rng, get_context, numpy_seed, numpy_state_seed
 
 log = logging.getLogger()
 
@@ -182,13 +182,18 @@ def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
                              loss, act, fit_batch_size, fit_epochs,
                              debug_summary_path, disable_pbar, ctx=None,
                              chunk_sampler_fn=None, row_bounds=None,
-                             records_budget=None):
+                             records_budget=None, rng=None):
   """embedding.py:269-305, device-resident end to end. `hypergraph` is the
   reference's Hypergraph message or an already compressed Incidence (e.g.
   proto_native.read_incidence of a file too large for Python protobuf).
   A stream whose record bound (row_bounds(inc): per node row, per edge
   row) exceeds the budget is sampled once into the compact record store
-  and trained from it with Keras' global shuffle (Hg2vModel.fit_store)."""
+  and trained from it with Keras' global shuffle (Hg2vModel.fit_store).
+  rng="mt19937" (the stream stays resident): the sampler draws numpy's
+  stream, the tables are initialised from a seed derived from numpy's
+  state without drawing from it (Keras' init comes from TF), and every
+  epoch's order is Keras' np.random.shuffle -- numpy's global stream
+  advances exactly as the reference's does."""
   del disable_pbar
   ctx = ctx or get_context()
   if isinstance(hypergraph, Incidence):
@@ -196,7 +201,7 @@ def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
   else:
     inc = Incidence.from_hypergraph(hypergraph)  # CompressRange + CSR
   budget = RECORDS_BUDGET if records_budget is None else records_budget
-  if chunk_sampler_fn is not None:
+  if chunk_sampler_fn is not None and rng is None:
     bn, be = row_bounds(inc)
     if int(np.sum(bn, dtype=np.int64) + np.sum(be, dtype=np.int64)) > budget:
       seed = numpy_seed()
@@ -218,8 +223,9 @@ def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
   if debug_summary_path is not None:
     _plot_distributions(debug_summary_path, records)
   model = Hg2vModel(inc.N + 1, inc.E + 1, dimension, num_neighbors, loss, act,
-                    ctx=ctx)  # rows = max compressed idx + 2
-  model.fit(batch_size=fit_batch_size, epochs=fit_epochs)
+                    ctx=ctx, seed=numpy_state_seed() if rng else None)
+  # (rows = max compressed idx + 2)
+  model.fit(batch_size=fit_batch_size, epochs=fit_epochs, rng=rng)
   node_w, edge_w = model.get_weights()
   return coords_to_embedding(inc, node_w[1:], edge_w[1:], dimension, "")
 
@@ -227,15 +233,20 @@ def _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors, sampler_fn,
 def EmbedHg2vBoolean(hypergraph, dimension, num_neighbors=5, num_samples=200,
                      batch_size=256, epochs=10, neg_samples=0,
                      debug_summary_path=None, disable_pbar=False,
-                     records_budget=None, row_quota=None):
+                     records_budget=None, row_quota=None, rng=None):
   """FOBE: BooleanSamples + BooleanModel (embedding.py:308-329). A stream of
   more than `records_budget` records is sampled once into the compact
   record store and every epoch trains it in Keras' global shuffle order
   (Hg2vModel.fit_store). row_quota = (node quotas, edge quotas) (not in
-  the reference) replaces int(weight * S) per row: bounded runs."""
+  the reference) replaces int(weight * S) per row: bounded runs.
+  rng="mt19937": after np.random.seed(s) the records and every epoch's
+  order are the reference's bit for bit (_hypergraph2vec_skeleton)."""
+  if check_rng(rng) and row_quota is not None:
+    raise ValueError("row_quota is not a reference option: not with "
+                     "rng='mt19937'")
   sampler_fn = lambda inc, ctx: sample_fobe(inc, num_neighbors, num_samples,
                                             neg_samples, ctx=ctx,
-                                            row_quota=row_quota)
+                                            row_quota=row_quota, rng=rng)
 
   def chunk_sampler_fn(inc, ctx):
     ctx.upload(inc)
@@ -274,7 +285,7 @@ def EmbedHg2vBoolean(hypergraph, dimension, num_neighbors=5, num_samples=200,
                                  batch_size, epochs, debug_summary_path,
                                  disable_pbar, chunk_sampler_fn=chunk_sampler_fn,
                                  row_bounds=row_bounds,
-                                 records_budget=records_budget)
+                                 records_budget=records_budget, rng=rng)
   emb.method_name = "HG2V_BOOLEAN"
   return emb
 
@@ -428,7 +439,7 @@ def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
                      num_samples=200, batch_size=256, epochs=10,
                      debug_summary_path=None, disable_pbar=False,
                      records_budget=None, group=None, edge_ranges=1,
-                     row_quota=None):
+                     row_quota=None, rng=None):
   """HOBE: alg-dist (k=10, 20 iterations) + AlgebraicDistanceSamples +
   UnweightedFloatModel (embedding.py:389-416). `alpha` is accepted and, as
   in the reference, not used (_alpha_scale is called with alpha=0).
@@ -439,8 +450,15 @@ def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
   torch.distributed.run, one GPU per rank): the multi-GPU pipeline
   (hobe_sharded); every rank returns the same embedding. row_quota =
   (node quotas, edge quotas) (not in the reference) replaces S on every
-  row: bounded runs (rows with quota 0 are not sampled)."""
+  row: bounded runs (rows with quota 0 are not sampled). rng="mt19937":
+  after np.random.seed(s) the alg-dist init, the HOBE pairs and
+  (run_in_parallel=False) neighbours and every epoch's order come from
+  numpy's stream as in the reference (the probabilities from this
+  device's alg-dist coordinates, within 1e-4 of the reference's)."""
   del alpha
+  if check_rng(rng) and (group is not None or row_quota is not None):
+    raise ValueError("rng='mt19937' is the single-process reference "
+                     "stream: no group, no row_quota")
   if group is not None:
     assert row_quota is None, "row_quota is a single-process option"
     inc = (hypergraph if isinstance(hypergraph, Incidence)
@@ -463,7 +481,7 @@ def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
   def sampler_fn(inc, ctx):
     alg_dist(inc, ctx)
     return sample_hobe(inc, num_neighbors, num_samples, ctx=ctx,
-                       row_quota=row_quota)
+                       row_quota=row_quota, rng=rng)
 
   def chunk_sampler_fn(inc, ctx):
     alg_dist(inc, ctx)
@@ -492,7 +510,7 @@ def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
                                  batch_size, epochs, debug_summary_path,
                                  disable_pbar, chunk_sampler_fn=chunk_sampler_fn,
                                  row_bounds=row_bounds,
-                                 records_budget=records_budget)
+                                 records_budget=records_budget, rng=rng)
   emb.method_name = "HG2V_ALG_DIST"
   return emb
 

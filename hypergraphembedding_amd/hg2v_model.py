@@ -29,13 +29,37 @@ class Hg2vModel:
                         numpy_seed() if seed is None else seed)
 
   def fit(self, batch_size=256, epochs=10, min_delta=1e-3, lr=0.01, eps=1e-7,
-          shuffle_seed=None, perms=None):
+          shuffle_seed=None, perms=None, rng=None):
     """Keras fit(shuffle=True) + EarlyStopping(monitor='loss', min_delta,
-    patience=0) over the records resident on the context."""
+    patience=0) over the records resident on the context. rng="mt19937":
+    every epoch's order is Keras 2.x's own, np.random.shuffle of
+    arange(records) on numpy's global RandomState (training_arrays.fit_loop),
+    drawn only for the epochs that run."""
+    if rng == "mt19937":
+      return self._fit_numpy_order(batch_size, epochs, min_delta, lr, eps)
     return self.ctx.train(batch=batch_size, max_epochs=epochs, lr=lr, eps=eps,
                           loss=self.loss, act=self.act, min_delta=min_delta,
                           shuffle_seed=numpy_seed() if shuffle_seed is None
                           else shuffle_seed, perms=perms)
+
+  def _fit_numpy_order(self, batch_size, epochs, min_delta, lr, eps):
+    import numpy as np
+    n = self.ctx.records_info()[0]
+    md = float(np.float32(min_delta))  # hgx_train compares in double
+    best, losses = float("inf"), []
+    for _ in range(epochs):
+      order = np.arange(n)
+      np.random.shuffle(order)
+      self.ctx.train(batch=batch_size, max_epochs=1, lr=lr, eps=eps,
+                     loss=self.loss, act=self.act, min_delta=-1e30,
+                     perms=order[None, :])
+      cur = self.ctx.train_loss_sum() / max(n, 1)
+      losses.append(cur)
+      if cur < best - md:
+        best = cur
+      else:
+        break
+    return np.array(losses, np.float32)
 
   def fit_store(self, budget, batch_size=256, epochs=10, min_delta=1e-3,
                 lr=0.01, eps=1e-7, seed=None):

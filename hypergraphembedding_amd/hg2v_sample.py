@@ -12,6 +12,11 @@ columns uniformly (np.random.choice(replace=False), :77-85) and K
 neighbours with replacement (:49-51). The device draws the same
 distribution from a counter-based generator keyed by a seed taken from
 numpy's global RNG, so np.random.seed(s) still makes runs reproducible.
+
+rng="mt19937": the samplers draw from numpy's global RandomState itself
+(hgx_sample_fobe_mt / hgx_sample_hobe_mt): after np.random.seed(s) the
+records are the reference's bit for bit and numpy's state is left where the
+reference leaves it (HOBE: run_in_parallel=False semantics).
 """
 
 from collections import namedtuple
@@ -21,7 +26,7 @@ import scipy.sparse as sp
 
 from . import _hgx
 from .hypergraph_util import Incidence
-from .runtime import get_context, numpy_seed
+from .runtime import check_rng, get_context, numpy_seed
 
 SimilarityRecord = namedtuple(
     "SimilarityRecord",
@@ -69,11 +74,13 @@ def records_from_arrays(idx, tgt, K):
 
 
 def sample_fobe(inc, num_neighbors, num_samples, neg_samples=0, ctx=None,
-                seed=None, row_quota=None):
+                seed=None, row_quota=None, rng=None):
   """BooleanSamples on the device; returns DeviceRecords. row_quota =
   (node quotas, edge quotas) replaces int(weight * S) per row (bounded
-  runs; rows with quota 0 are not sampled)."""
+  runs; rows with quota 0 are not sampled). rng="mt19937": numpy's global
+  stream, the reference's records bit for bit (seed unused)."""
   assert num_neighbors >= 1
+  check_rng(rng)
   ctx = ctx or get_context()
   ctx.upload(inc)
   if row_quota is not None:
@@ -85,22 +92,34 @@ def sample_fobe(inc, num_neighbors, num_samples, neg_samples=0, ctx=None,
   if neg_samples > 0:
     nnq = _quotas(inc.node_weight, neg_samples)
     neq = _quotas(inc.edge_weight, neg_samples)
-  n = ctx.sample_fobe(numpy_seed() if seed is None else seed, num_neighbors,
-                      nq, eq, nnq, neq)
+  if rng == "mt19937":
+    n = ctx.sample_fobe_mt(num_neighbors, nq, eq, nnq, neq)
+  else:
+    n = ctx.sample_fobe(numpy_seed() if seed is None else seed,
+                        num_neighbors, nq, eq, nnq, neq)
   return DeviceRecords(ctx, inc, n, num_neighbors)
 
 
 def sample_hobe(inc, num_neighbors, num_samples, ctx=None, seed=None,
-                alg_coords=None, row_quota=None):
+                alg_coords=None, row_quota=None, rng=None):
   """AlgebraicDistanceSamples on the device (alg coords must be resident on
   ctx, e.g. from algebraic_distance.AlgebraicDistance, or given). row_quota
-  = (node quotas, edge quotas) instead of S on every row (bounded runs)."""
+  = (node quotas, edge quotas) instead of S on every row (bounded runs).
+  rng="mt19937": numpy's global stream, the reference's pairs and
+  (run_in_parallel=False) neighbours bit for bit."""
   assert num_neighbors >= 0
   assert num_samples >= 0
+  check_rng(rng)
   ctx = ctx or get_context()
   if alg_coords is not None:
     ctx.upload(inc)
     ctx.alg_set(*alg_coords)
+  if rng == "mt19937":
+    if row_quota is not None:
+      raise ValueError("row_quota is not a reference option: not with "
+                       "rng='mt19937'")
+    n = ctx.sample_hobe_mt(num_neighbors, num_samples)
+    return DeviceRecords(ctx, inc, n, num_neighbors)
   seed = numpy_seed() if seed is None else seed
   if row_quota is not None:
     n = ctx.sample_hobe(seed, num_neighbors, num_samples,

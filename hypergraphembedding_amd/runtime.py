@@ -46,6 +46,30 @@ def scratch_context(device=None):
     ctx.close()
 
 
+def numpy_state_seed():
+  """A 63-bit device seed derived from numpy's global RandomState WITHOUT
+  drawing from it (a hash of its MT19937 key and position): the seed of the
+  table init in rng="mt19937" runs, where numpy's stream must advance
+  exactly as the reference's does (Keras draws its init from TF, not numpy)."""
+  import hashlib
+  st = np.random.get_state()
+  h = hashlib.blake2b(np.asarray(st[1], np.uint32).tobytes() +
+                      int(st[2]).to_bytes(4, "little"), digest_size=8)
+  return int.from_bytes(h.digest(), "little") >> 1
+
+
+RNG_MODES = (None, "mt19937")
+
+
+def check_rng(rng):
+  """rng=None: the device's counter-based draws keyed by a numpy-drawn seed
+  (distribution parity); rng="mt19937": numpy's global RandomState stream
+  itself, the reference's records and epoch shuffles bit for bit."""
+  if rng not in RNG_MODES:
+    raise ValueError("rng must be None or 'mt19937', not %r" % (rng,))
+  return rng
+
+
 def numpy_seed():
   """A 63-bit device seed drawn from numpy's global RandomState, so that
   np.random.seed(s) makes a whole embedding run reproducible, as it does for

@@ -57,6 +57,10 @@ int hgx_version(void);
  * the context's own stream. */
 int hgx_set_stream(hgx_ctx *ctx, void *hip_stream);
 int hgx_synchronize(hgx_ctx *ctx);
+/* HIP devices visible to this library (no context needed), and the free /
+ * total device memory of a context's device (hipMemGetInfo). */
+int hgx_device_count(int *n);
+int hgx_mem_info(hgx_ctx *ctx, int64_t *free_bytes, int64_t *total_bytes);
 /* Implementation choices of this context (none changes a result's math or
  * distribution; not a reference interface). key:
  *   "sample_reject_w"  2/3-hop sample rows with more expansion paths are
@@ -199,6 +203,25 @@ int hgx_sample_hobe(hgx_ctx *ctx, uint64_t seed, int K, int S,
 int hgx_sample_hobe_rows(hgx_ctx *ctx, uint64_t seed, int K,
                          const int32_t *node_quota, const int32_t *edge_quota,
                          int S, int64_t *n_records);
+/* The reference's record stream bit for bit (rng="mt19937"): the same
+ * samplers drawing from numpy's global legacy RandomState, whose MT19937
+ * state (np.random.get_state(): 624 key words and the position) is passed
+ * in and updated in place to the state the reference leaves behind.
+ * hgx_sample_fobe_mt replaces BooleanSamples (hg2v_sample.py:125-242, the
+ * quotas as for hgx_sample_fobe); hgx_sample_hobe_mt replaces
+ * AlgebraicDistanceSamples(run_in_parallel=False) (:632-717): its
+ * neighbour draws come from the worker's copy of the stream (:604-605), so
+ * the returned state is the parent's after its last pair draw. The host
+ * walks the stream (the bounded draws' accepted values, in order); the
+ * device orders the pattern rows (scipy's SMMP column order), runs every
+ * row's Fisher-Yates and writes the records (csrc/hgx_mt.hip). Such a
+ * stream is not keyed, so hgx_store_append refuses it. */
+int hgx_sample_fobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
+                       const int32_t *node_quota, const int32_t *edge_quota,
+                       const int32_t *neg_node_quota,
+                       const int32_t *neg_edge_quota, int64_t *n_records);
+int hgx_sample_hobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
+                       int S, int64_t *n_records);
 /* ---- weighted-Jaccard samples (HG2V_ADJ_JAC / HG2V_NEIGH_JAC) --------- *
  * Replaces WeightedJaccardSamples (hg2v_sample.py:395-510) with
  * SparseWeightedJaccard (:250-273) and GetAllCentroids (:276-326).

@@ -225,15 +225,14 @@ def test_embed_takes_the_store_path(plg, monkeypatch):
 def test_store_release_returns_the_memory(ctx, plg):
   """hgx_store_release frees the store's HBM (device free memory comes
   back) and leaves a usable context: the store grows again afterwards."""
-  import torch
   ctx.upload(plg)
   ctx.store_release()
-  free0 = torch.cuda.mem_get_info(ctx.device)[0]
+  free0 = ctx.mem_info()[0]
   ctx.store_reset(100_000_000)  # 1.2 GB of 12-byte entries
-  free1 = torch.cuda.mem_get_info(ctx.device)[0]
+  free1 = ctx.mem_info()[0]
   assert free0 - free1 >= 1_100_000_000
   ctx.store_release()
-  free2 = torch.cuda.mem_get_info(ctx.device)[0]
+  free2 = ctx.mem_info()[0]
   assert free2 - free1 >= 1_100_000_000
   assert ctx.store_info()[0] == 0
   _hobe(ctx, plg)

@@ -300,3 +300,28 @@ def test_incidence_samples_equal_the_proto_path():
     b = proto_samples(hg, list(hg.node), list(hg.edge))
     for x, y in zip(a, b):
       assert np.array_equal(x, y)
+
+
+def test_rng_modes_and_state_seed():
+  """rng is None or "mt19937" (ValueError otherwise, before any device
+  call); the mt19937 table-init seed is derived from numpy's state without
+  advancing it; reference-only runs refuse the product's extensions."""
+  from hypergraphembedding_amd import embedding
+  from hypergraphembedding_amd.runtime import check_rng, numpy_state_seed
+  assert check_rng(None) is None and check_rng("mt19937") == "mt19937"
+  with pytest.raises(ValueError):
+    check_rng("philox")
+  np.random.seed(12)
+  before = np.random.get_state()[1].copy(), np.random.get_state()[2]
+  s1 = numpy_state_seed()
+  s2 = numpy_state_seed()
+  after = np.random.get_state()
+  assert s1 == s2 and 0 <= s1 < 2**63
+  assert np.array_equal(before[0], after[1]) and before[1] == after[2]
+  np.random.seed(13)
+  assert numpy_state_seed() != s1
+  with pytest.raises(ValueError):
+    embedding.EmbedHg2vBoolean(None, 4, rng="mt19937",
+                               row_quota=(np.ones(2), np.ones(2)))
+  with pytest.raises(ValueError):
+    embedding.EmbedHg2vAlgDist(None, 4, rng="mt19937", group=object())
