@@ -211,10 +211,13 @@ def launch_ranks(n, timeout):
   def pump(stream):
     for line in iter(stream.readline, b""):
       s = line.decode(errors="replace")
-      if s.lstrip().startswith("{"):
+      # the JSON line to stdout; anything else rank 0's libraries print
+      # there (gloo's connection notes) to stderr
+      out = sys.stdout if s.lstrip().startswith("{") else sys.stderr
+      if out is sys.stdout:
         seen["json"] += 1
-      sys.stdout.write(s)
-      sys.stdout.flush()
+      out.write(s)
+      out.flush()
     stream.close()
 
   def stop_all(sig):
