@@ -104,6 +104,9 @@ def parse():
                  help="samples of the C5 combiner's CPU-baseline slice")
   p.add_argument("--no-c4", action="store_true",
                  help="skip the power-law 10M/5M measurements")
+  p.add_argument("--c4-full", action="store_true",
+                 help="opt-in: the whole C4 HOBE d=256 pipeline (every row "
+                      "sampled into the record store, one epoch; ~5 min)")
   p.add_argument("--no-extra", action="store_true",
                  help="skip the C2 FOBE and end-to-end measurements")
   p.add_argument("--c4-chunks", type=int, default=2,
@@ -163,6 +166,17 @@ def cpu_model():
   except OSError:
     pass
   return "unknown"
+
+
+_T0 = time.time()
+
+
+def progress(msg):
+  """A progress line on stderr (long legs: the GPU pool takes a command that
+  prints nothing for minutes for a hung one)."""
+  if os.environ.get("RANK", "0") == "0":
+    print(f"[bench {time.time() - _T0:7.1f} s] {msg}", file=sys.stderr,
+          flush=True)
 
 
 def timed_runs(fn, reps):
@@ -374,6 +388,7 @@ def main():
   bytes_iter = 8.0 * inc.nnz + (8.0 + 12.0 * k) * (inc.N + inc.E)
 
   # ---- algebraic distance (SpMV relaxation) ----
+  progress('C3 graph built; alg-dist')
   exch = {}
   if world > 1:
     alg_dist_sharded(ctx, inc, x0, y0, args.alg_iters)  # warm
@@ -392,6 +407,7 @@ def main():
   alg_gbps = bytes_iter * args.alg_iters / (alg_ms * 1e-3) / 1e9
 
   # ---- HOBE records (alg coords resident on the device) ----
+  progress('C3 HOBE sampling')
   ctx.upload(inc)
   ctx.alg_set(x0, y0)
   ctx.alg_run(args.alg_iters)
@@ -409,6 +425,7 @@ def main():
   sample_s = max_over_ranks(time.time() - t)
 
   # ---- training: the timed steps ----
+  progress('C3 training (timed steps)')
   ctx.model_init(args.dim, inc.N + 1, inc.E + 1, seed=7 + rank)
   for w in range(args.warmup):
     ctx.train(batch=args.batch, max_epochs=1, loss=_hgx.LOSS_MSE,
@@ -539,6 +556,7 @@ def main():
         "gpu_records_per_s": round(n / sample_s, 1) if sample_s > 0 else None}
 
   # ---- C2: FOBE d=128 on the same graph (BASELINE configs[1]) ----
+  progress('C2 FOBE + end-to-end legs')
   c2 = e2e = None
   if not args.no_extra:
     S, K = args.num_samples, args.num_neighbors
@@ -589,7 +607,12 @@ def main():
   # ---- power-law 10M/5M graph (C4 shape) ----
   c4 = None
   if not args.no_c4:
+    progress("C4 legs (alg-dist, 2% HOBE d=256 slice, C5 combiner)")
     c4 = bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded)
+  c4_full = None
+  if args.c4_full:
+    progress("c4-full leg")
+    c4_full = bench_c4_full(args, ctx, world, sync, max_over_ranks)
 
   ranks_seen = dist.get_world_size() if dist is not None else 1
   # HIP devices visible to this rank's libhgx (hipGetDeviceCount; torch's
@@ -647,6 +670,7 @@ def main():
         "c2_fobe_d128": c2,
         "end_to_end": e2e,
         "algdist_c4": c4,
+        "c4_full": c4_full,
         "graph_gen_s": round(gen_s, 2),
     }
     print(json.dumps(out), flush=True)
@@ -891,6 +915,92 @@ def bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded):
       c4["c5_combiner"] = bench_c5(args, ctx, big)
     sync()
   return c4
+
+
+def bench_c4_full(args, ctx, world, sync, max_over_ranks):
+  """--c4-full: the north star's 10M/5M HOBE d=256 embedding end to end, as
+  EmbedHg2vAlgDist runs it past RECORDS_BUDGET (embedding.py:389-416):
+  alg-dist k=10 x 20 iterations (node-row sharded over RCCL at N > 1),
+  AlgebraicDistanceSamples on EVERY node and edge row (S=200, K=5) sampled
+  once into the record store in strided row classes (row-sharded, entries
+  all-gathered, at N > 1), one global-shuffle epoch of d=256 Adagrad from
+  the store (Hg2vModel.fit_store). Timed per stage; the store is released
+  afterwards. At N > 1 every rank trains the same epoch (replicas)."""
+  from hypergraphembedding_amd import _hgx
+  from hypergraphembedding_amd.embedding import (STORE_CHUNK, fill_store,
+                                                 hobe_sharded)
+  from hypergraphembedding_amd.hg2v_model import Hg2vModel
+  from hypergraphembedding_amd.hg2v_sample import row_class_quota
+  from hypergraphembedding_amd.synthetic import powerlaw_hypergraph
+  S, K, d = args.num_samples, args.num_neighbors, 256
+  t = time.perf_counter()
+  g = powerlaw_hypergraph(seed=0)
+  gen_s = time.perf_counter() - t
+  ctx.store_release()  # the C4 slice's records: their HBM back
+  st = {}
+  sync()
+  t0 = time.perf_counter()
+  if world > 1:
+    hobe_sharded(g, d, K, S, args.batch, epochs=1, ctx=ctx, stats=st,
+                 edge_ranges=args.edge_ranges)
+    sync()
+    total = max_over_ranks(time.perf_counter() - t0)
+    stages = {"alg_dist_s": st.get("alg_s"), "sampling_s": st.get("sampling_s"),
+              "train_epoch_s": st.get("train_s")}
+    n = int(st.get("records", 0))
+  else:
+    ctx.upload(g)
+    rs = np.random.RandomState(1)
+    ctx.alg_set(rs.random_sample((g.N, 10)), rs.random_sample((g.E, 10)))
+    ctx.alg_run(args.alg_iters)
+    sync()
+    t1 = time.perf_counter()
+    bn = np.full(g.N, 2 * S, np.int64)
+    be = np.full(g.E, 2 * S, np.int64)
+    fq = (np.full(g.N, S, np.int32), np.full(g.E, S, np.int32))
+    def sample(off, stride):
+      m = ctx.sample_hobe(4000, K, S, *(row_class_quota(q, off, stride)
+                                        for q in fq))
+      progress(f"c4-full: row class {off} of {stride} sampled ({m} records)")
+      return m
+    try:
+      n = fill_store(ctx, g, sample, bn, be, STORE_CHUNK)
+      sync()
+      t2 = time.perf_counter()
+      model = Hg2vModel(g.N + 1, g.E + 1, d, K, _hgx.LOSS_MSE, _hgx.ACT_RELU,
+                        ctx=ctx, seed=11)
+      model.fit_store(STORE_CHUNK, batch_size=args.batch, epochs=1,
+                      min_delta=-1e30, seed=3,
+                      on_chunk=lambda ep, c, nc: progress(
+                          f"c4-full: chunk {c + 1} of {nc} trained"))
+      sync()
+      t3 = time.perf_counter()
+      free, tot = ctx.mem_info()
+      cs = model.chunk_stats
+    finally:
+      ctx.store_release()
+    total = t3 - t0
+    stages = {"alg_dist_s": round(t1 - t0, 3), "sampling_s": round(t2 - t1, 3),
+              "train_epoch_s": round(t3 - t2, 3)}
+    st["per_batch_us"] = round(sum(x[2] for x in cs) * 1e3 /
+                               max(sum(x[4] for x in cs), 1), 2)
+    st["chunks"] = len(cs)
+    st["device_mem_used_gb_at_epoch_end"] = round((tot - free) / 1e9, 1)
+  out = {"workload": "C4 HOBE d=256 end to end on the power-law 10M/5M graph: "
+                     "alg-dist k=10 x %d, every row sampled (S=%d, K=%d) into "
+                     "the record store, one global-shuffle epoch" %
+                     (args.alg_iters, S, K),
+         "records": n, "time_to_embedding_s": round(total, 2),
+         "stages_s": {k: (round(v, 3) if v is not None else None)
+                      for k, v in stages.items()},
+         "train_records_per_s": (round(n / stages["train_epoch_s"], 1)
+                                 if stages.get("train_epoch_s") else None),
+         "graph_gen_s": round(gen_s, 1), "ranks": world}
+  for k in ("per_batch_us", "chunks", "device_mem_used_gb_at_epoch_end",
+            "sampling_chunks"):
+    if k in st:
+      out[k] = st[k]
+  return out
 
 
 def bench_c5(args, ctx, big):

@@ -62,7 +62,7 @@ class Hg2vModel:
     return np.array(losses, np.float32)
 
   def fit_store(self, budget, batch_size=256, epochs=10, min_delta=1e-3,
-                lr=0.01, eps=1e-7, seed=None):
+                lr=0.01, eps=1e-7, seed=None, on_chunk=None):
     """fit() over the record store of the context (hgx_store_*): a stream
     sampled once and kept as 12-byte entries because its trainer records
     do not fit in HBM (the C4 HOBE stream: 5.9e9 records, 404 GB; the
@@ -77,7 +77,8 @@ class Hg2vModel:
     (Keras' batch-size-weighted mean) and EarlyStopping(min_delta,
     patience=0) applies to it. Epoch ep's seed comes from
     RandomState([seed, ep]). Returns the epoch losses; per epoch the
-    records may exceed 2^31."""
+    records may exceed 2^31. on_chunk(epoch, chunk, n_chunks), if given, is
+    called after every trained chunk (progress of long epochs)."""
     import numpy as np
     base = numpy_seed() % (2**32) if seed is None else seed
     best, losses = float("inf"), []
@@ -98,6 +99,8 @@ class Hg2vModel:
         lsum += self.ctx.train_loss_sum()
         n += m
         self.chunk_stats.append((ep, c) + tuple(self.ctx.train_stats()))
+        if on_chunk is not None:
+          on_chunk(ep, c, nc)
       self.records_per_epoch = n
       cur = lsum / max(n, 1)
       losses.append(cur)

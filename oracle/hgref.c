@@ -861,7 +861,9 @@ static void head_loss(int loss, float y, float yt, float *lv, float *g) {
  * one the device's fixed-point sums approach). Test infrastructure: the
  * trainer parity tests report the distance between the two as the
  * ambiguity the reference semantics leave. */
-static int g_dup_f64 = 0;
+/* per thread: the tests run both summation orders side by side from two
+ * Python threads (ctypes calls run on the calling thread) */
+static _Thread_local int g_dup_f64 = 0;
 void hgref_train_set_dup_f64(int on) { g_dup_f64 = on; }
 
 int hgref_train(int64_t n, int K, const int32_t *idx, const float *tgt, int d,

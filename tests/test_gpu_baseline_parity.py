@@ -43,7 +43,10 @@ def row_cos(a, b):
 
 
 def _threads():
-  return max(1, min(16, len(os.sched_getaffinity(0))))
+  # the checker's fastest count on the GPU boxes: bench.py's thread sweep
+  # of the same trainer measured 1.21M records/s at 8 threads, 0.98M at 16
+  # (profiles/r05/final3/bench.json)
+  return max(1, min(8, len(os.sched_getaffinity(0))))
 
 
 @pytest.mark.timeout(900)

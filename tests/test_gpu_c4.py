@@ -210,13 +210,20 @@ def _window_vs_oracle(ctx, g, loss, act, seed):
   cidx[:, ncols] = np.searchsorted(un, idx[:, ncols])
   cidx[:, ecols] = np.searchsorted(ue, idx[:, ecols])
   del idx
+  # both summation orders at once, one Python thread each (the oracle is
+  # single-threaded and ctypes releases the GIL; the order flag is
+  # thread-local in hgref.c)
+  from concurrent.futures import ThreadPoolExecutor
+
+  def oracle(f64):
+    return O.train(cidx, tgt, K, nt0, et0, loss, act, batch=256, max_epochs=1,
+                   perms=perms, min_delta=-1e30, dup_f64=f64)
   res = {}
-  for f64 in (True, False):
-    ont, oet, ol, _, _ = O.train(cidx, tgt, K, nt0, et0, loss, act, batch=256,
-                                 max_epochs=1, perms=perms, min_delta=-1e30,
-                                 dup_f64=f64)
-    assert np.allclose(gl, ol, rtol=1e-4), (f64, gl, ol)
-    res[f64] = (ont, oet)
+  with ThreadPoolExecutor(2) as pool:
+    for f64, (ont, oet, ol, _, _) in zip((True, False),
+                                         pool.map(oracle, (True, False))):
+      assert np.allclose(gl, ol, rtol=1e-4), (f64, gl, ol)
+      res[f64] = (ont, oet)
   def dist(a, b):
     d = np.concatenate([np.abs(a[0] - b[0]).ravel(), np.abs(a[1] - b[1]).ravel()])
     return d.max(), np.percentile(d, 99.99), np.percentile(d, 99.9)
