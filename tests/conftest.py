@@ -44,3 +44,32 @@ def tiny_inc():
 @pytest.fixture(scope="session")
 def small_inc():
   return golden_incidence("csr_small.npz")
+
+
+class Background:
+  """CPU checker work run beside the GPU tests (session-wide): a test runs
+  its device part, submits the oracle half here and a test at the end of
+  the session (tests/test_gpu_zz_deferred.py) asserts on the result. Four
+  workers: the C2 / C3 epoch checkers at 8 OpenMP threads each (the box's
+  CPU share is 16) and the two C4 windows' single-threaded oracles."""
+
+  def __init__(self):
+    from concurrent.futures import ThreadPoolExecutor
+    self.pool = ThreadPoolExecutor(4)
+    self.jobs = {}
+
+  def submit(self, key, fn):
+    self.jobs[key] = self.pool.submit(fn)
+
+  def result(self, key, fallback):
+    """The submitted job's result, or fallback() run here when the device
+    half did not run in this session (the deferred test run alone)."""
+    job = self.jobs.pop(key, None)
+    return job.result() if job is not None else fallback()
+
+
+@pytest.fixture(scope="session")
+def background():
+  b = Background()
+  yield b
+  b.pool.shutdown(wait=True)

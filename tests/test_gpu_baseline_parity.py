@@ -43,14 +43,16 @@ def row_cos(a, b):
 
 
 def _threads():
-  # the checker's fastest count on the GPU boxes: bench.py's thread sweep
-  # of the same trainer measured 1.21M records/s at 8 threads, 0.98M at 16
-  # (profiles/r05/final3/bench.json)
+  # each checker runs beside the other on the box's 16-core CPU share
+  # (conftest.Background: two workers)
   return max(1, min(8, len(os.sched_getaffinity(0))))
 
 
-@pytest.mark.timeout(900)
-def test_c3_full_hobe_epoch_vs_oracle():
+def _device_epoch(kind):
+  """One full epoch of the C3 HOBE (kind "c3") or C2 FOBE ("c2") stream on
+  the GPU from seeded tables and a seeded permutation. Returns what the
+  checker needs: the stream in batch order, the initial tables, the device
+  loss and tables."""
   from hypergraphembedding_amd import _hgx
   from hypergraphembedding_amd.synthetic import random_hypergraph
   inc = random_hypergraph(seed=0)
@@ -58,18 +60,26 @@ def test_c3_full_hobe_epoch_vs_oracle():
   ctx = _hgx.Context(0)
   try:
     ctx.upload(inc)
-    r = np.random.RandomState(4)
-    ctx.alg_set(r.random_sample((inc.N, 10)), r.random_sample((inc.E, 10)))
-    ctx.alg_run(20)
-    n = ctx.sample_hobe(17, K, S)
-    assert n > 55_000_000
-    rs = np.random.RandomState(12)
+    if kind == "c3":
+      r = np.random.RandomState(4)
+      ctx.alg_set(r.random_sample((inc.N, 10)), r.random_sample((inc.E, 10)))
+      ctx.alg_run(20)
+      n = ctx.sample_hobe(17, K, S)
+      assert n > 55_000_000
+      rs = np.random.RandomState(12)
+      loss, act = _hgx.LOSS_MSE, _hgx.ACT_RELU
+    else:
+      n = ctx.sample_fobe(31, K, np.full(inc.N, S, np.int32),
+                          np.full(inc.E, S, np.int32))
+      assert n > 30_000_000
+      rs = np.random.RandomState(14)
+      loss, act = _hgx.LOSS_KLD, _hgx.ACT_SIGMOID
     nt = rs.uniform(-0.05, 0.05, (inc.N + 1, d)).astype(np.float32)
     et = rs.uniform(-0.05, 0.05, (inc.E + 1, d)).astype(np.float32)
     perm = rs.permutation(n)
     ctx.model_init(d, inc.N + 1, inc.E + 1, node_tab=nt, edge_tab=et)
-    gl = ctx.train(batch=256, max_epochs=1, loss=_hgx.LOSS_MSE,
-                   act=_hgx.ACT_RELU, perms=perm[None, :], min_delta=-1e30)
+    gl = ctx.train(batch=256, max_epochs=1, loss=loss, act=act,
+                   perms=perm[None, :], min_delta=-1e30)
     fused, split = ctx.train_path_stats()
     assert split == 0 and fused == -(-n // 256)
     gnt, get_ = ctx.model_get()
@@ -78,58 +88,49 @@ def test_c3_full_hobe_epoch_vs_oracle():
     ctx.close()
   idx = np.ascontiguousarray(idx[perm])
   tgt = np.ascontiguousarray(tgt[perm])
-  del perm
-  ont, oet, oloss = O.train_mt(idx, tgt, K, nt, et, O.LOSS_MSE, O.ACT_RELU,
-                               epochs=1, threads=_threads(), copy=False,
-                               exact=True)
-  assert np.isclose(gl[0], oloss, rtol=1e-4), (gl, oloss)
-  for g, o, name in ((gnt, ont, "node"), (get_, oet, "edge")):
+  return dict(idx=idx, tgt=tgt, nt=nt, et=et, gl=gl, gnt=gnt, get=get_, K=K,
+              loss=O.LOSS_MSE if kind == "c3" else O.LOSS_KLD,
+              act=O.ACT_RELU if kind == "c3" else O.ACT_SIGMOID)
+
+
+def checker(data):
+  """The checker build of the trainer port (bit-for-bit hgref_train
+  rounding, threaded) on the device's stream, order and init; returns
+  (device loss, oracle loss, [(name, p50, p1, min cosine, max-abs)])."""
+  ont, oet, oloss = O.train_mt(data["idx"], data["tgt"], data["K"], data["nt"],
+                               data["et"], data["loss"], data["act"], epochs=1,
+                               threads=_threads(), copy=False, exact=True)
+  rows = []
+  for g, o, name in ((data["gnt"], ont, "node"), (data["get"], oet, "edge")):
     c = row_cos(g[1:], o[1:])
-    p50, p1 = np.percentile(c, 50), np.percentile(c, 1)
-    print(f"{name}: cosine p50 {p50:.8f} p1 {p1:.8f} min {c.min():.8f} "
-          f"max-abs {np.abs(g - o).max():.3e}")
+    rows.append((name, np.percentile(c, 50), np.percentile(c, 1), c.min(),
+                 np.abs(g - o).max()))
+  return data["gl"], oloss, rows
+
+
+def assert_checked(res):
+  """epoch loss rtol 1e-4, per-row cosine p50 >= 0.9999 and
+  p1 >= 0.999 on both tables."""
+  gl, oloss, rows = res
+  assert np.isclose(gl[0], oloss, rtol=1e-4), (gl, oloss)
+  for name, p50, p1, cmin, mx in rows:
+    print(f"{name}: cosine p50 {p50:.8f} p1 {p1:.8f} min {cmin:.8f} "
+          f"max-abs {mx:.3e}")
     assert p50 >= 0.9999 and p1 >= 0.999, (name, p50, p1)
 
 
 @pytest.mark.timeout(900)
-def test_c2_full_fobe_epoch_vs_oracle():
+def test_c3_full_hobe_epoch_device(background):
+  """C3's device epoch; the checker runs in the background and
+  test_gpu_zz_deferred.py::test_c3_full_hobe_epoch_vs_oracle asserts."""
+  data = _device_epoch("c3")
+  background.submit("c3", lambda: checker(data))
+
+
+@pytest.mark.timeout(900)
+def test_c2_full_fobe_epoch_device(background):
   """every record of the C2 FOBE stream (~34M: nn, ee
   and both node-edge blocks at S = 200, K = 5), d = 128, KLD + sigmoid, one
-  epoch on the device and by the checker with the same initial tables and
-  batch order."""
-  from hypergraphembedding_amd import _hgx
-  from hypergraphembedding_amd.synthetic import random_hypergraph
-  inc = random_hypergraph(seed=0)
-  K, S, d = 5, 200, 128
-  ctx = _hgx.Context(0)
-  try:
-    ctx.upload(inc)
-    n = ctx.sample_fobe(31, K, np.full(inc.N, S, np.int32),
-                        np.full(inc.E, S, np.int32))
-    assert n > 30_000_000
-    rs = np.random.RandomState(14)
-    nt = rs.uniform(-0.05, 0.05, (inc.N + 1, d)).astype(np.float32)
-    et = rs.uniform(-0.05, 0.05, (inc.E + 1, d)).astype(np.float32)
-    perm = rs.permutation(n)
-    ctx.model_init(d, inc.N + 1, inc.E + 1, node_tab=nt, edge_tab=et)
-    gl = ctx.train(batch=256, max_epochs=1, loss=_hgx.LOSS_KLD,
-                   act=_hgx.ACT_SIGMOID, perms=perm[None, :], min_delta=-1e30)
-    fused, split = ctx.train_path_stats()
-    assert split == 0 and fused == -(-n // 256)
-    gnt, get_ = ctx.model_get()
-    idx, tgt = ctx.records_get()
-  finally:
-    ctx.close()
-  idx = np.ascontiguousarray(idx[perm])
-  tgt = np.ascontiguousarray(tgt[perm])
-  del perm
-  ont, oet, oloss = O.train_mt(idx, tgt, K, nt, et, O.LOSS_KLD, O.ACT_SIGMOID,
-                               epochs=1, threads=_threads(), copy=False,
-                               exact=True)
-  assert np.isclose(gl[0], oloss, rtol=1e-4), (gl, oloss)
-  for g, o, name in ((gnt, ont, "node"), (get_, oet, "edge")):
-    c = row_cos(g[1:], o[1:])
-    p50, p1 = np.percentile(c, 50), np.percentile(c, 1)
-    print(f"{name}: cosine p50 {p50:.8f} p1 {p1:.8f} min {c.min():.8f} "
-          f"max-abs {np.abs(g - o).max():.3e}")
-    assert p50 >= 0.9999 and p1 >= 0.999, (name, p50, p1)
+  epoch on the device; checked by test_c2_full_fobe_epoch_vs_oracle."""
+  data = _device_epoch("c2")
+  background.submit("c2", lambda: checker(data))

@@ -194,3 +194,34 @@ def test_embed_hg2v_boolean_mt_end_to_end(tiny_hypergraph, tiny_inc, monkeypatch
     c = _row_cos(g, o)
     assert np.percentile(c, 50) >= 0.9999 and np.percentile(c, 1) >= 0.999, \
         (np.percentile(c, 50), np.percentile(c, 1))
+
+
+def test_fobe_mt_c2_equals_the_oracle_replica(ctx, capsys):
+  """C2 (random 100k/50k, S=200, K=5): the ~34M-record numpy-seeded FOBE
+  stream equals the oracle's MT19937 replica record for record, and numpy's
+  state afterwards equals the replica's. Timings of both are printed."""
+  import time
+  from hypergraphembedding_amd.synthetic import random_hypergraph
+  inc = random_hypergraph(seed=0)
+  S, K = 200, 5
+  q_n, q_e = np.full(inc.N, S, np.int32), np.full(inc.E, S, np.int32)
+  ctx.upload(inc)
+  np.random.seed(21)
+  t = time.perf_counter()
+  n = ctx.sample_fobe_mt(K, q_n, q_e)
+  ctx.synchronize()
+  t_dev = time.perf_counter() - t
+  assert n > 30_000_000
+  r = O.Rng(21)
+  t = time.perf_counter()
+  oidx, otgt = O.fobe_sample(r, inc, q_n, q_e, K)
+  t_cpu = time.perf_counter() - t
+  idx, tgt = ctx.records_get()
+  assert idx.shape == oidx.shape
+  assert np.array_equal(idx, oidx) and np.array_equal(tgt, otgt)
+  del idx, tgt, oidx, otgt
+  assert np.array_equal(_next_words(), _oracle_words(r))
+  with capsys.disabled():
+    print(f"\nC2 FOBE rng=mt19937: {n} records, device path {t_dev:.2f} s "
+          f"({n / t_dev / 1e6:.1f}M records/s), oracle replica (1 CPU "
+          f"thread) {t_cpu:.2f} s")
