@@ -82,7 +82,7 @@ def parse():
                       "WORLD_SIZE starts that many child ranks")
   p.add_argument("--launch-timeout", type=float, default=3000.0,
                  help="launcher: seconds before unfinished ranks are killed")
-  p.add_argument("--launch-selftest", choices=("ok", "fail"), default=None,
+  p.add_argument("--launch-selftest", choices=("ok", "fail", "hang"), default=None,
                  help=argparse.SUPPRESS)  # launcher test: trivial children
   p.add_argument("--edge-ranges", type=int, default=4,
                  help="C4 sharded alg-dist: edge ranges the exchange is "
@@ -204,6 +204,18 @@ def _kill_group(p, sig):
     pass
 
 
+def _die_with_parent():
+  """In a rank child before it starts: SIGKILL it if the launcher dies
+  (prctl PR_SET_PDEATHSIG), so a launcher killed outright leaves no rank
+  holding a GPU."""
+  import ctypes
+  import signal
+  try:
+    ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGKILL))
+  except OSError:
+    pass
+
+
 def launch_ranks(n, timeout):
   """Start n ranks of this script as child processes and wait for them.
 
@@ -251,6 +263,7 @@ def launch_ranks(n, timeout):
                  LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", ROLE_RANK=str(r),
                  MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
       p = subprocess.Popen(argv, env=env, start_new_session=True,
+                           preexec_fn=_die_with_parent,
                            stdout=subprocess.PIPE if r == 0 else sys.stderr)
       procs.append(p)
       if r == 0:
@@ -297,10 +310,13 @@ def launch_ranks(n, timeout):
 def launch_selftest(mode, world, rank):
   """--launch-selftest child: a gloo rendezvous on the CPU (no GPU), rank 0
   prints the ranks it saw; in mode 'fail' the last rank exits 3 and rank 0
-  blocks as a rank waiting on a collective would."""
+  blocks as a rank waiting on a collective would; in mode 'hang' every rank
+  blocks."""
   import torch
   import torch.distributed as dist
   print(f"[selftest] rank {rank} of {world}", file=sys.stderr, flush=True)
+  if mode == "hang":
+    time.sleep(600)
   if mode == "fail" and world > 1:
     if rank == world - 1:
       sys.exit(3)

@@ -70,3 +70,25 @@ def test_gpus_must_match_world_size():
               _env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
   assert p.returncode == 2
   assert "disagrees with WORLD_SIZE=2" in p.stderr.decode()
+
+
+def test_ranks_die_with_a_killed_launcher():
+  """A launcher killed with SIGKILL (no chance to clean up) takes its ranks
+  with it (PR_SET_PDEATHSIG): nothing is left holding a GPU."""
+  import signal
+  p = subprocess.Popen([sys.executable, BENCH, "--gpus", "2", "--launch-selftest",
+                        "hang", "--launch-timeout", "300"], env=_env(),
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+  # wait until both ranks announce themselves (then they block)
+  seen = b""
+  t = time.time()
+  while seen.count(b"[selftest] rank") < 2 and time.time() - t < 60:
+    seen += p.stderr.read1(4096)
+  assert seen.count(b"[selftest] rank") == 2
+  p.send_signal(signal.SIGKILL)
+  p.wait()
+  time.sleep(2)
+  out = subprocess.run(["ps", "-eo", "pid,args"], capture_output=True).stdout
+  left = [l for l in out.decode().splitlines()
+          if "--launch-selftest hang" in l]
+  assert not left, left
