@@ -31,7 +31,7 @@ F=$(find $O/pmc_FETCH_SIZE -name '*counter_collection.csv' | head -1)
 W=$(find $O/pmc_WRITE_SIZE -name '*counter_collection.csv' | head -1)
 python tools/pmc_train_summary.py "$F" "$W" $O/pmc_train.json 128 5 > /dev/null || exit 18
 rm -rf $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE
-# the --gpus N path rehearsed on one GPU: 2 ranks over gloo on cuda:0 (not
-# a scaling measurement: both ranks share one GPU)
-timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 1 --warmup 0 --one-device --dist-backend gloo --no-cpu --no-extra > $O/bench_2rank_gloo.json 2> $O/bench_2rank_gloo.err || { echo G2FAIL; exit 19; }
+# the --gpus N path rehearsed on one GPU: bench.py starts its 2 ranks itself
+# (gloo on cuda:0; not a scaling measurement: both ranks share one GPU)
+timeout -k 10 600 python3 -u bench.py --gpus 2 --steps 1 --warmup 0 --one-device --dist-backend gloo --no-cpu --no-extra > $O/bench_2rank_gloo.json 2> $O/bench_2rank_gloo.err || { echo G2FAIL; exit 19; }
 echo all-ok
