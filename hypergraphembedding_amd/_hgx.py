@@ -75,6 +75,7 @@ SIGNATURES = {
     "hgx_sample_fobe_mt": (_int, [_vp, _vp, _pint, _int, _vp, _vp, _vp, _vp,
                                   _pi64]),
     "hgx_sample_hobe_mt": (_int, [_vp, _vp, _pint, _int, _int, _pi64]),
+    "hgx_sample_jaccard_mt": (_int, [_vp, _vp, _pint, _int, _vp, _vp, _pi64]),
     "hgx_sample_last_stats": (_int, [_vp, _pi64, _pi64]),
     "hgx_sample_uniform_rows": (_int, [_vp, _pi64]),
     "hgx_features_set": (_int, [_vp, _vp, _vp]),
@@ -436,6 +437,13 @@ class Context:
     """AlgebraicDistanceSamples(run_in_parallel=False) drawing from numpy's
     global RandomState (hgx_sample_hobe_mt)."""
     return self._mt_call(lib().hgx_sample_hobe_mt, K, S)
+
+  def sample_jaccard_mt(self, K, node_q, edge_q):
+    """WeightedJaccardSamples(run_in_parallel=False) drawing from numpy's
+    global RandomState (hgx_sample_jaccard_mt; features_set first)."""
+    nq, eq = _c(node_q, np.int32), _c(edge_q, np.int32)
+    assert nq.size == self.inc.N and eq.size == self.inc.E
+    return self._mt_call(lib().hgx_sample_jaccard_mt, K, _ptr(nq), _ptr(eq))
 
   # weighted-Jaccard samplers
   def features_set(self, node_major, edge_major):

@@ -407,19 +407,14 @@ extern "C" int hgx_jaccard_probs(hgx_ctx *ctx, int kind, int64_t n,
   return HGX_OK;
 }
 
-extern "C" int hgx_sample_jaccard(hgx_ctx *ctx, uint64_t seed, int K,
-                                  const int32_t *node_quota,
-                                  const int32_t *edge_quota, int64_t *n_records) {
-  if (!ctx) return HGX_EINVAL;
-  HGX_CHECK(ctx, ctx->N > 0, HGX_ESTATE, "no incidence uploaded");
+// the three kind blocks' probabilities of a pair stream on the context
+// (records [0, o_ee) nn, [o_ee, o_ne) ee, [o_ne, total) node-edge): shared
+// by hgx_sample_jaccard and the numpy-seeded sampler (hgx_mt.hip)
+int hgx_jaccard_fill(hgx_ctx *ctx, int64_t o_ee, int64_t o_ne, int64_t total) {
   HGX_CHECK(ctx, ctx->features_ok, HGX_ESTATE, "hgx_features_set not called");
-  HGX_CHECK(ctx, K >= 1 && K <= 16, HGX_EUNSUP, "num_neighbors %d outside [1,16]", K);
-  HGX_HIP(ctx, hipSetDevice(ctx->device));
   HGX_TRY(ensure_centroids(ctx));
-  int64_t o_ee = 0, o_ne = 0, total = 0;
-  HGX_TRY(hgx_sample_pairs4(ctx, seed, K, node_quota, edge_quota, &o_ee, &o_ne, &total));
   const JacArgs J = jac_args(ctx);
-  const int R = 4 + 2 * K;
+  const int R = 4 + 2 * ctx->K;
   hipLaunchKernelGGL(jac_fill, dim3(grid_for(o_ee, 256)), dim3(256), 0, ctx->stream,
                      J, 0, (int64_t)0, o_ee, R, ctx->rec_idx.as<int>(),
                      ctx->rec_tgt.as<float>());
@@ -431,6 +426,21 @@ extern "C" int hgx_sample_jaccard(hgx_ctx *ctx, uint64_t seed, int K,
                      ctx->rec_tgt.as<float>());
   HGX_LAUNCH_CHECK(ctx);
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HGX_OK;
+}
+
+extern "C" int hgx_sample_jaccard(hgx_ctx *ctx, uint64_t seed, int K,
+                                  const int32_t *node_quota,
+                                  const int32_t *edge_quota, int64_t *n_records) {
+  if (!ctx) return HGX_EINVAL;
+  HGX_CHECK(ctx, ctx->N > 0, HGX_ESTATE, "no incidence uploaded");
+  HGX_CHECK(ctx, ctx->features_ok, HGX_ESTATE, "hgx_features_set not called");
+  HGX_CHECK(ctx, K >= 1 && K <= 16, HGX_EUNSUP, "num_neighbors %d outside [1,16]", K);
+  HGX_HIP(ctx, hipSetDevice(ctx->device));
+  HGX_TRY(ensure_centroids(ctx));
+  int64_t o_ee = 0, o_ne = 0, total = 0;
+  HGX_TRY(hgx_sample_pairs4(ctx, seed, K, node_quota, edge_quota, &o_ee, &o_ne, &total));
+  HGX_TRY(hgx_jaccard_fill(ctx, o_ee, o_ne, total));
   if (n_records) *n_records = total;
   return HGX_OK;
 }

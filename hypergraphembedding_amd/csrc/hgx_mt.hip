@@ -744,17 +744,17 @@ extern "C" int hgx_sample_fobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_po
   return HGX_OK;
 }
 
-extern "C" int hgx_sample_hobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
-                                  int S, int64_t *n_records) {
-  if (!ctx) return HGX_EINVAL;
-  MtRun M;
-  Mt st;
-  HGX_TRY(mt_begin(ctx, M, mt_key, mt_pos, st, K));
-  HGX_CHECK(ctx, ctx->k > 0, HGX_ESTATE, "HOBE needs the algebraic-distance coords on device");
-  HGX_CHECK(ctx, S >= 0, HGX_EINVAL, "num_samples must be >= 0 (hg2v_sample.py:647)");
-  const std::vector<int> qn(ctx->N, S), qe(ctx->E, S);
-  // AlgebraicDistanceSamples (hg2v_sample.py:658-715): nn, ee, A A^T A of
-  // node rows, A^T A A^T of edge rows (swapped) in the parent
+namespace {
+
+// AlgebraicDistanceSamples / WeightedJaccardSamples (run_in_parallel=False)
+// pair blocks drawing the stream: nn, ee, A A^T A of node rows, A^T A A^T of
+// edge rows (swapped) in the parent (hg2v_sample.py:658-705, 432-503), the
+// records emitted with targets 0, then the node-edge neighbour draws on the
+// forked worker's copy of the stream (:604-605, 371-372): `st` stays the
+// parent's. off = block bounds {0, o_ee, o_ne, o_en, total}.
+int pairs4_mt(MtRun &M, Mt &st, const std::vector<int> &qn, const std::vector<int> &qe,
+              int K, int64_t off[5]) {
+  hgx_ctx *ctx = M.ctx;
   MtPat nn, ee, ne_n, ne_e;
   nn.pattern = P_NN;
   ee.pattern = P_EE;
@@ -766,26 +766,65 @@ extern "C" int hgx_sample_hobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_po
   HGX_TRY(sample_pattern(M, ne_e, st, qe));
   std::vector<int> pv, pe;
   HGX_TRY(ne_pairs(M, ne_n, ne_e, pv, pe));
-  const int64_t o_ee = nn.total(), o_ne = o_ee + ee.total();
-  const int64_t o_en = o_ne + ne_n.total(), total = o_en + ne_e.total();
-  HGX_TRY(mt_alloc(ctx, total, K));
-  HGX_TRY(emit(M, REC_NN, nn, 0, 0.f));
-  HGX_TRY(emit(M, REC_EE, ee, o_ee, 0.f));
-  HGX_TRY(emit(M, REC_NE_NODE, ne_n, o_ne, 0.f));
-  HGX_TRY(emit(M, REC_NE_EDGE, ne_e, o_en, 0.f));
-  // the neighbour draws of DiffTypeDistanceSample run in the forked worker:
-  // a copy of the parent's stream (:604-605, run_in_parallel=False)
+  off[0] = 0;
+  off[1] = nn.total();
+  off[2] = off[1] + ee.total();
+  off[3] = off[2] + ne_n.total();
+  off[4] = off[3] + ne_e.total();
+  HGX_TRY(mt_alloc(ctx, off[4], K));
+  HGX_TRY(emit(M, REC_NN, nn, off[0], 0.f));
+  HGX_TRY(emit(M, REC_EE, ee, off[1], 0.f));
+  HGX_TRY(emit(M, REC_NE_NODE, ne_n, off[2], 0.f));
+  HGX_TRY(emit(M, REC_NE_EDGE, ne_e, off[3], 0.f));
   Mt worker = st;
-  HGX_TRY(neighbors(M, o_ne, pv, pe, worker));
-  HGX_TRY(hgx_hobe_prepare(ctx));
-  HGX_TRY(hgx_hobe_fill_probs(ctx, 0, 0, o_ee));
-  HGX_TRY(hgx_hobe_fill_probs(ctx, 1, o_ee, o_ne));
-  HGX_TRY(hgx_hobe_fill_probs(ctx, 2, o_ne, total));
-  const int64_t b[5] = {0, o_ee, o_ne, o_en, total};
-  for (int i = 0; i <= 4; i++) ctx->rec_bounds[i] = b[i];
+  HGX_TRY(neighbors(M, off[2], pv, pe, worker));
+  for (int i = 0; i <= 4; i++) ctx->rec_bounds[i] = off[i];
   ctx->n_rec_blocks = 4;
+  return HGX_OK;
+}
+
+}  // namespace
+
+int hgx_jaccard_fill(hgx_ctx *ctx, int64_t o_ee, int64_t o_ne, int64_t total);
+
+extern "C" int hgx_sample_hobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
+                                  int S, int64_t *n_records) {
+  if (!ctx) return HGX_EINVAL;
+  MtRun M;
+  Mt st;
+  HGX_TRY(mt_begin(ctx, M, mt_key, mt_pos, st, K));
+  HGX_CHECK(ctx, ctx->k > 0, HGX_ESTATE, "HOBE needs the algebraic-distance coords on device");
+  HGX_CHECK(ctx, S >= 0, HGX_EINVAL, "num_samples must be >= 0 (hg2v_sample.py:647)");
+  // AlgebraicDistanceSamples: quota S on every row (hg2v_sample.py:659-703)
+  const std::vector<int> qn(ctx->N, S), qe(ctx->E, S);
+  int64_t off[5];
+  HGX_TRY(pairs4_mt(M, st, qn, qe, K, off));
+  HGX_TRY(hgx_hobe_prepare(ctx));
+  HGX_TRY(hgx_hobe_fill_probs(ctx, 0, off[0], off[1]));
+  HGX_TRY(hgx_hobe_fill_probs(ctx, 1, off[1], off[2]));
+  HGX_TRY(hgx_hobe_fill_probs(ctx, 2, off[2], off[4]));
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   put_state(st, mt_key, mt_pos);
-  if (n_records) *n_records = total;
+  if (n_records) *n_records = off[4];
+  return HGX_OK;
+}
+
+extern "C" int hgx_sample_jaccard_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
+                                     const int32_t *node_quota, const int32_t *edge_quota,
+                                     int64_t *n_records) {
+  if (!ctx) return HGX_EINVAL;
+  MtRun M;
+  Mt st;
+  HGX_TRY(mt_begin(ctx, M, mt_key, mt_pos, st, K));
+  HGX_CHECK(ctx, ctx->features_ok, HGX_ESTATE, "hgx_features_set not called");
+  HGX_TRY(check_quota(ctx, node_quota, ctx->N, "node"));
+  HGX_TRY(check_quota(ctx, edge_quota, ctx->E, "edge"));
+  // WeightedJaccardSamples: quotas int(weight * S) (hg2v_sample.py:419-422)
+  int64_t off[5];
+  HGX_TRY(pairs4_mt(M, st, quota_vec(node_quota, ctx->N), quota_vec(edge_quota, ctx->E), K,
+                    off));
+  HGX_TRY(hgx_jaccard_fill(ctx, off[1], off[2], off[4]));
+  put_state(st, mt_key, mt_pos);
+  if (n_records) *n_records = off[4];
   return HGX_OK;
 }

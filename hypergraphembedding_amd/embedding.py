@@ -517,28 +517,31 @@ def EmbedHg2vAlgDist(hypergraph, dimension, alpha=0, num_neighbors=5,
 
 def _jaccard_embed(hypergraph, dimension, which, alpha, num_neighbors,
                    num_samples, batch_size, epochs, debug_summary_path,
-                   disable_pbar):
+                   disable_pbar, rng=None):
   """embedding.py:330-386: WeightedJaccardSamples over UniformWeight or
-  WeightByNeighborhood features, UnweightedFloatModel (relu, MSE)."""
+  WeightByNeighborhood features, UnweightedFloatModel (relu, MSE).
+  rng="mt19937": numpy's stream for the samples and the epoch orders."""
+  check_rng(rng)
 
   def sampler_fn(inc, ctx):
     ctx.upload(inc)
     fn, fe = ctx.incidence_weights(which, float(alpha))
-    return sample_jaccard(inc, fn, fe, num_neighbors, num_samples, ctx=ctx)
+    return sample_jaccard(inc, fn, fe, num_neighbors, num_samples, ctx=ctx,
+                          rng=rng)
 
   return _hypergraph2vec_skeleton(hypergraph, dimension, num_neighbors,
                                   sampler_fn, _hgx.LOSS_MSE, _hgx.ACT_RELU,
                                   batch_size, epochs, debug_summary_path,
-                                  disable_pbar)
+                                  disable_pbar, rng=rng)
 
 
 def EmbedHg2vAdjJaccard(hypergraph, dimension, num_neighbors=5,
                         num_samples=200, batch_size=256, epochs=10,
-                        debug_summary_path=None, disable_pbar=False):
+                        debug_summary_path=None, disable_pbar=False, rng=None):
   """embedding.py:330-355 (UniformWeight features)."""
   emb = _jaccard_embed(hypergraph, dimension, _hgx.WEIGHT_UNIFORM, 0.0,
                        num_neighbors, num_samples, batch_size, epochs,
-                       debug_summary_path, disable_pbar)
+                       debug_summary_path, disable_pbar, rng=rng)
   emb.method_name = "HG2V_ADJ_JAC"
   return emb
 
@@ -547,12 +550,12 @@ def EmbedHg2vNeighborhoodWeightedJaccard(hypergraph, dimension, alpha=0,
                                          num_neighbors=5, num_samples=200,
                                          batch_size=256, epochs=10,
                                          debug_summary_path=None,
-                                         disable_pbar=False):
+                                         disable_pbar=False, rng=None):
   """embedding.py:358-386 (WeightByNeighborhood(alpha) features)."""
   assert 0 <= alpha <= 1
   emb = _jaccard_embed(hypergraph, dimension, _hgx.WEIGHT_NEIGHBORHOOD, alpha,
                        num_neighbors, num_samples, batch_size, epochs,
-                       debug_summary_path, disable_pbar)
+                       debug_summary_path, disable_pbar, rng=rng)
   emb.method_name = "HG2V_NEIGH_JAC"
   return emb
 

@@ -432,18 +432,24 @@ def _incidence_values(inc, m, node_major):
 
 
 def sample_jaccard(inc, node_features, edge_features, num_neighbors,
-                   num_samples, ctx=None, seed=None):
+                   num_samples, ctx=None, seed=None, rng=None):
   """WeightedJaccardSamples on the device (features as per-incidence values,
-  node-major / edge-major); returns DeviceRecords."""
+  node-major / edge-major); returns DeviceRecords. rng="mt19937": numpy's
+  global stream (run_in_parallel=False semantics), the reference's records
+  bit for bit."""
   assert num_neighbors >= 1
   assert num_samples >= 0
+  check_rng(rng)
   ctx = ctx or get_context()
   ctx.upload(inc)
   ctx.features_set(node_features, edge_features)
   nq = _quotas(inc.node_weight, num_samples)
   eq = _quotas(inc.edge_weight, num_samples)
-  n = ctx.sample_jaccard(numpy_seed() if seed is None else seed,
-                         num_neighbors, nq, eq)
+  if rng == "mt19937":
+    n = ctx.sample_jaccard_mt(num_neighbors, nq, eq)
+  else:
+    n = ctx.sample_jaccard(numpy_seed() if seed is None else seed,
+                           num_neighbors, nq, eq)
   return DeviceRecords(ctx, inc, n, num_neighbors)
 
 

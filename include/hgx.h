@@ -222,6 +222,12 @@ int hgx_sample_fobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
                        const int32_t *neg_edge_quota, int64_t *n_records);
 int hgx_sample_hobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
                        int S, int64_t *n_records);
+/* WeightedJaccardSamples(run_in_parallel=False) (hg2v_sample.py:395-510)
+ * drawing numpy's stream, the per-row quotas int(weight * S) as for
+ * hgx_sample_jaccard (declared below) and its probabilities. */
+int hgx_sample_jaccard_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
+                          const int32_t *node_quota, const int32_t *edge_quota,
+                          int64_t *n_records);
 /* ---- weighted-Jaccard samples (HG2V_ADJ_JAC / HG2V_NEIGH_JAC) --------- *
  * Replaces WeightedJaccardSamples (hg2v_sample.py:395-510) with
  * SparseWeightedJaccard (:250-273) and GetAllCentroids (:276-326).

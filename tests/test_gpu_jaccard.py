@@ -130,3 +130,21 @@ def test_tiny_probs_and_centroids_vs_oracle(ctx, tiny_inc):
     b = rs.randint(0, nb, 3000)
     assert np.array_equal(ctx.jaccard_probs(kind, a, b),
                           O.jaccard_probs(kind, a, b, inc, fn, fe))
+
+
+@pytest.mark.parametrize("kind", ["uniform", "neigh"])
+def test_sampler_mt_is_the_reference_stream(ctx, small_inc, kind):
+  """rng="mt19937": np.random.seed(the fixture's seed), then the device
+  sampler drawing numpy's stream returns WeightedJaccardSamples' own
+  records (run_in_parallel=False), ids, neighbours and probabilities."""
+  z = golden("jaccard_small.npz")
+  inc, K = small_inc, int(z["K"])
+  ctx.upload(inc)
+  ctx.features_set(*_features(z, inc, kind))
+  nq, eq = _quotas(z, inc, kind)
+  np.random.seed(int(z[kind + "_seed"]))
+  n = ctx.sample_jaccard_mt(K, nq, eq)
+  idx, tgt = ctx.records_get()
+  assert n == z[kind + "_idx"].shape[0]
+  assert np.array_equal(idx, z[kind + "_idx"])
+  assert np.array_equal(tgt, z[kind + "_tgt"])
