@@ -70,7 +70,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFLOPS = 157.3  # f32-in MFMA = the FP32 vector peak (same guide)
 METRIC = ("training samples/sec + alg-dist SpMV GB/s, HOBE dim=128 at "
           "1/2/4/8 MI355X")
-PMC_TRAIN = os.path.join(ROOT, "profiles", "r05", "pmc_train.json")
+PMC_TRAIN = os.path.join(ROOT, "profiles", "r06", "pmc_train.json")
 # FETCH/WRITE passes of the C4 d = 256 step (tools/train_d256_pmc_prog.py)
 PMC_TRAIN_D256 = os.path.join(ROOT, "profiles", "r05", "pmc_train_d256.json")
 

@@ -29,7 +29,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
 done
 F=$(find $O/pmc_FETCH_SIZE -name '*counter_collection.csv' | head -1)
 W=$(find $O/pmc_WRITE_SIZE -name '*counter_collection.csv' | head -1)
-python tools/pmc_train_summary.py "$F" "$W" $O/pmc_train.json 128 5 > /dev/null || exit 18
+python tools/pmc_train_summary.py "$F" "$W" $O/pmc_train.json 128 6 > /dev/null || exit 18
 rm -rf $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE
 # the --gpus N path rehearsed on one GPU: bench.py starts its 2 ranks itself
 # (gloo on cuda:0; not a scaling measurement: both ranks share one GPU)
