@@ -225,3 +225,60 @@ def test_fobe_mt_c2_equals_the_oracle_replica(ctx, capsys):
     print(f"\nC2 FOBE rng=mt19937: {n} records, device path {t_dev:.2f} s "
           f"({n / t_dev / 1e6:.1f}M records/s), oracle replica (1 CPU "
           f"thread) {t_cpu:.2f} s")
+
+
+def test_embed_hg2v_alg_dist_mt_end_to_end(tiny_hypergraph, tiny_inc, monkeypatch):
+  """np.random.seed(0); EmbedHg2vAlgDist(youtube_tiny, 16, rng="mt19937"):
+  the alg-dist init from numpy (as EmbedAlgebraicDistance draws it), the
+  HOBE pairs and (run_in_parallel=False) neighbours of the reference record
+  for record, the probabilities from this device's coordinates (within
+  5e-4 of the reference's: its coordinates agree to 1e-4), numpy's state at
+  fit = the reference's parent state, Keras' epoch orders; the embedding vs
+  the CPU restatement trained on the reference stream from the same init
+  and orders: per-row cosine p50 >= 0.9999, p1 >= 0.999."""
+  from hypergraphembedding_amd import embedding
+  from hypergraphembedding_amd.hg2v_model import Hg2vModel
+  seen = {}
+
+  class Spy(Hg2vModel):
+    def fit(self, *a, **k):
+      seen["tables"] = self.ctx.model_get()
+      seen["records"] = self.ctx.records_get()
+      seen["state"] = np.random.get_state()
+      return super().fit(*a, **k)
+
+  monkeypatch.setattr(embedding, "Hg2vModel", Spy)
+  z = golden("algdist_tiny.npz")  # the reference's coordinates, seed 0
+  inc, K, S, d = tiny_inc, 5, 200, 16
+  np.random.seed(int(z["seed"]))
+  emb = embedding.EmbedHg2vAlgDist(tiny_hypergraph, d, rng="mt19937")
+  end_words = _next_words()
+  assert emb.method_name == "HG2V_ALG_DIST"
+  r = O.Rng(int(z["seed"]))
+  r.random((inc.N, 10))
+  r.random((inc.E, 10))
+  oidx, otgt = O.hobe_sample(r, inc, z["x_20"], z["y_20"], S, K)
+  idx, tgt = seen["records"]
+  assert np.array_equal(idx, oidx)
+  assert np.abs(tgt - otgt).max() <= 5e-4
+  rs = np.random.RandomState()
+  rs.set_state(seen["state"])
+  assert np.array_equal(rs.randint(0, 2**32, 16, dtype=np.uint32).astype(np.int64),
+                        _oracle_words(r))
+  rs.set_state(seen["state"])
+  perms = np.stack([rs.permutation(oidx.shape[0]) for _ in range(10)])
+  nt, et = seen["tables"]
+  ont, oet, ol, _, _ = O.train(oidx, otgt, K, nt, et, O.LOSS_MSE, O.ACT_RELU,
+                               batch=256, max_epochs=10, perms=perms,
+                               min_delta=1e-3)
+  rs.set_state(seen["state"])
+  for _ in range(len(ol)):
+    rs.permutation(oidx.shape[0])
+  assert np.array_equal(rs.randint(0, 2**32, 16, dtype=np.uint32).astype(np.int64),
+                        end_words)
+  gn = np.array([emb.node[int(i)].values for i in inc.node_ids], np.float32)
+  ge = np.array([emb.edge[int(i)].values for i in inc.edge_ids], np.float32)
+  for g, o in ((gn, ont[1:]), (ge, oet[1:])):
+    c = _row_cos(g, o)
+    assert np.percentile(c, 50) >= 0.9999 and np.percentile(c, 1) >= 0.999, \
+        (np.percentile(c, 50), np.percentile(c, 1))
