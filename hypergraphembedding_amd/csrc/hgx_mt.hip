@@ -367,12 +367,16 @@ int grid_of(int64_t work, int per, int cap = 65536) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((work + per - 1) / per, cap));
 }
 
+// host vector -> device buffer; complete on return (callers' vectors are
+// often locals that die right after)
 template <class T>
 int upload(hgx_ctx *ctx, DevBuf &b, const std::vector<T> &h) {
   HGX_TRY(hgx_ensure(ctx, b, sizeof(T) * (h.size() + 1)));
-  if (!h.empty())
+  if (!h.empty()) {
     HGX_HIP(ctx, hipMemcpyAsync(b.p, h.data(), sizeof(T) * h.size(),
                                 hipMemcpyHostToDevice, ctx->stream));
+    HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
   return HGX_OK;
 }
 
