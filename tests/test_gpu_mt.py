@@ -282,3 +282,30 @@ def test_embed_hg2v_alg_dist_mt_end_to_end(tiny_hypergraph, tiny_inc, monkeypatc
     c = _row_cos(g, o)
     assert np.percentile(c, 50) >= 0.9999 and np.percentile(c, 1) >= 0.999, \
         (np.percentile(c, 50), np.percentile(c, 1))
+
+
+def test_mt_zero_quotas_still_draw_their_permutations(ctx, small_inc):
+  """np.random.choice(cols, 0, replace=False) still draws permutation(|cols|)
+  in numpy's legacy RandomState: rows with quota 0 (weight-0 rows, S = 0)
+  consume the stream like the reference's. FOBE with a third of the rows at
+  quota 0 and HOBE with S = 0 against the oracle replica: records and the
+  state afterwards."""
+  inc, K = small_inc, 3
+  rs = np.random.RandomState(8)
+  nq = np.where(rs.random_sample(inc.N) < 0.33, 0, 7).astype(np.int32)
+  eq = np.where(rs.random_sample(inc.E) < 0.33, 0, 7).astype(np.int32)
+  ctx.upload(inc)
+  np.random.seed(31)
+  n = ctx.sample_fobe_mt(K, nq, eq)
+  r = O.Rng(31)
+  oidx, otgt = O.fobe_sample(r, inc, nq, eq, K)
+  idx, tgt = ctx.records_get()
+  assert n == oidx.shape[0] and np.array_equal(idx, oidx) and np.array_equal(tgt, otgt)
+  assert np.array_equal(_next_words(), _oracle_words(r))
+  z = golden("hobe_small.npz")
+  ctx.alg_set(z["alg_x"], z["alg_y"])
+  np.random.seed(32)
+  assert ctx.sample_hobe_mt(K, 0) == 0
+  r = O.Rng(32)
+  assert O.hobe_sample(r, inc, z["alg_x"], z["alg_y"], 0, K)[0].shape[0] == 0
+  assert np.array_equal(_next_words(), _oracle_words(r))
