@@ -598,6 +598,29 @@ def main():
           "per_batch_us": round(ms2 * 1e3 / max(bat2, 1), 2),
           "batch_steps": dict(zip(("train_step", "train_fwd_bwd+train_update"),
                                   ctx.train_path_stats()))}
+    # the same stream drawn from numpy's own MT19937 stream (rng="mt19937":
+    # BooleanSamples' records bit for bit, hgx_sample_fobe_mt); at N = 1 the
+    # oracle's single-threaded C replica of the reference's draws beside it
+    np.random.seed(2000 + rank)
+    sync()
+    t = time.perf_counter()
+    n_mt = ctx.sample_fobe_mt(K, q_n, q_e)
+    sync()
+    mt_s = time.perf_counter() - t
+    c2["mt19937_sampling"] = {"records": n_mt, "s": round(mt_s, 3),
+                              "records_per_s": round(n_mt / mt_s, 1)}
+    if rank == 0 and world == 1 and not args.no_cpu:
+      sys.path.insert(0, os.path.join(ROOT, "oracle"))
+      import oracle as O
+      t = time.perf_counter()
+      ridx, _ = O.fobe_sample(O.Rng(2000), inc, q_n, q_e, K)
+      r_s = time.perf_counter() - t
+      c2["mt19937_sampling"]["cpu_replica"] = {
+          "s": round(r_s, 3), "records_per_s": round(ridx.shape[0] / r_s, 1),
+          "cores": 1, "kind": "port",
+          "sample": "the whole C2 stream, oracle/hgref.c hgref_fobe_sample "
+                    "(the reference's MT19937 draws restated in C)"}
+      del ridx
 
     # ---- end to end: one real EmbedHg2vAlgDist call (embedding.py:389) ----
     from hypergraphembedding_amd.embedding import EmbedHg2vAlgDist
