@@ -53,8 +53,9 @@ namespace {
 constexpr int kMtN = 624, kMtM = 397;
 
 struct Mt {
-  uint32_t key[kMtN];
+  uint32_t key[kMtN];  // numpy's state: the untempered key block
   int pos;
+  uint32_t tw[kMtN];   // the block's tempered outputs (the draws' words)
 };
 
 void mt_twist(Mt &s) {
@@ -70,13 +71,25 @@ void mt_twist(Mt &s) {
   s.pos = 0;
 }
 
+// the tempered outputs of the current key block, all at once (vectorises)
+void mt_temper(Mt &s) {
+  for (int i = 0; i < kMtN; i++) {
+    uint32_t y = s.key[i];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    s.tw[i] = y ^ (y >> 18);
+  }
+}
+
+inline void mt_refill(Mt &s) {
+  mt_twist(s);
+  mt_temper(s);
+}
+
 inline uint32_t mt_next(Mt &s) {
-  if (s.pos >= kMtN) mt_twist(s);
-  uint32_t y = s.key[s.pos++];
-  y ^= y >> 11;
-  y ^= (y << 7) & 0x9d2c5680u;
-  y ^= (y << 15) & 0xefc60000u;
-  return y ^ (y >> 18);
+  if (s.pos >= kMtN) mt_refill(s);
+  return s.tw[s.pos++];
 }
 
 inline uint32_t mask_of(uint32_t v) {
@@ -95,6 +108,42 @@ inline uint32_t mt_interval(Mt &s, uint32_t max) {
   while ((v = (mt_next(s) & mask)) > max) {
   }
   return v;
+}
+
+// The draws random_interval(i) for i = hi, hi - 1, ..., lo, which share one
+// mask (lo = 2^b <= hi < 2^(b+1)), appended to out. The same values as
+// mt_interval one by one, without its data-dependent branch: every word is
+// masked, stored at out and kept (out advances, i counts down) iff it is
+// <= i; only the loop's exit is a branch. ~3x faster on the host.
+inline void mt_interval_run(Mt &s, uint32_t hi, uint32_t lo, uint32_t mask,
+                            uint32_t *&out) {
+  uint32_t i = hi;
+  while (i >= lo) {
+    if (s.pos >= kMtN) mt_refill(s);
+    const uint32_t *w = s.tw + s.pos;
+    const int n = kMtN - s.pos;
+    uint32_t *o = out;
+    int j = 0;
+    while (j < n && i >= lo) {
+      const uint32_t v = w[j++] & mask;
+      const uint32_t keep = v <= i;
+      *o = v;
+      o += keep;
+      i -= keep;
+    }
+    out = o;
+    s.pos += j;
+  }
+}
+
+// a Fisher-Yates row of length L: random_interval(i), i = L-1 .. 1
+inline void mt_permutation_draws(Mt &s, uint32_t L, uint32_t *&out) {
+  uint32_t hi = L - 1;
+  while (hi >= 1) {
+    const uint32_t lo = 1u << (31 - __builtin_clz(hi));
+    mt_interval_run(s, hi, lo, 2 * lo - 1, out);
+    hi = lo - 1;
+  }
 }
 
 // legacy randint(0, n), n <= 2^32 (masked bounded draw of rng = n - 1)
@@ -495,10 +544,12 @@ int sample_pattern(MtRun &M, MtPat &p, Mt &st, const std::vector<int> &q) {
     coff[r + 1] = coff[r] + L;
     p.roff[r + 1] = p.roff[r] + std::min(q[r], L);
   }
-  std::vector<uint32_t> D((size_t)doff[R]);
-  size_t k = 0;
+  // (one slack word: mt_interval_run stores every word it looks at)
+  std::vector<uint32_t> D((size_t)doff[R] + 1);
+  uint32_t *dp = D.data();
   for (int r = 0; r < R; r++)
-    for (int i = p.len[r] - 1; i >= 1; i--) D[k++] = mt_interval(st, (uint32_t)i);
+    if (p.len[r] > 1) mt_permutation_draws(st, (uint32_t)p.len[r], dp);
+  D.pop_back();
   const bool hop1 = p.pattern == P_A || p.pattern == P_AT;
   DevBuf dD, ddoff, dcoff, dq, arr, asc;
   auto done = [&](int rc) {
@@ -622,6 +673,7 @@ int mt_begin(hgx_ctx *ctx, MtRun &M, const uint32_t *key, const int32_t *pos, Mt
   HGX_HIP(ctx, hipSetDevice(ctx->device));
   std::copy(key, key + kMtN, st.key);
   st.pos = *pos;
+  mt_temper(st);  // the words left in numpy's current block
   M.ctx = ctx;
   M.rp_n.resize(ctx->N + 1);
   M.rp_e.resize(ctx->E + 1);
