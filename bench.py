@@ -12,7 +12,12 @@ incidence already resident in HBM. Reported beside it, from the same run:
     (oracle/cpu_train_mt.c) on a bounded slice of the same records;
   * "algdist": the relaxation (k=10, 20 iterations) in algorithmic GB/s;
   * "c2_fobe_d128": FOBE (HG2V_BOOLEAN) d=128 on the same graph
-    (configs[1]): sampling and one training epoch;
+    (configs[1]): sampling and one training epoch; `mt19937_sampling`:
+    the same stream drawn from numpy's MT19937 (rng="mt19937", the
+    reference's records bit for bit) and, at N = 1, the oracle's C replica;
+  * "c3_hobe_mt19937": C3's HOBE stream from numpy's MT19937 (60M records)
+    timed, its sha256 checked against the stream the oracle's C replica
+    reproduced record for record (profiles/r06/mt_c3/);
   * "end_to_end": one real EmbedHg2vAlgDist(graph, 128) call, timed from the
     compressed incidence to the HypergraphEmbedding message (alg-dist,
     sampling, fit with EarlyStopping, proto);
@@ -573,7 +578,7 @@ def main():
 
   # ---- C2: FOBE d=128 on the same graph (BASELINE configs[1]) ----
   progress('C2 FOBE + end-to-end legs')
-  c2 = e2e = None
+  c2 = e2e = c3mt = None
   if not args.no_extra:
     S, K = args.num_samples, args.num_neighbors
     q_n = np.full(inc.N, S, np.int32)  # int(weight * S), weights 1
@@ -621,6 +626,37 @@ def main():
           "sample": "the whole C2 stream, oracle/hgref.c hgref_fobe_sample "
                     "(the reference's MT19937 draws restated in C)"}
       del ridx
+    # C3's HOBE stream from numpy's MT19937 (AlgebraicDistanceSamples,
+    # run_in_parallel=False): tools/mt_c3_hobe.py's procedure, whose stream
+    # the oracle's C replica reproduced record for record
+    # (profiles/r06/mt_c3/mt_c3_hobe.json: its sha256 is the check here)
+    ref = os.path.join(ROOT, "profiles", "r06", "mt_c3", "mt_c3_hobe.json")
+    rs1 = np.random.RandomState(1)
+    ctx.alg_set(rs1.random_sample((inc.N, 10)), rs1.random_sample((inc.E, 10)))
+    ctx.alg_run(20)
+    ax, ay = ctx.alg_get()
+    ctx.alg_set(ax, ay)
+    np.random.seed(5)
+    sync()
+    t = time.perf_counter()
+    n_h = ctx.sample_hobe_mt(args.num_neighbors, args.num_samples)
+    sync()
+    h_s = time.perf_counter() - t
+    import hashlib
+    hidx, htgt = ctx.records_get()
+    hh = hashlib.sha256()
+    hh.update(np.ascontiguousarray(hidx, np.int32).tobytes())
+    hh.update(np.ascontiguousarray(htgt, np.float32).tobytes())
+    del hidx, htgt
+    c3mt = {"records": n_h, "s": round(h_s, 3),
+            "records_per_s": round(n_h / h_s, 1), "sha256": hh.hexdigest()}
+    if os.path.exists(ref):
+      with open(ref) as f:
+        rj = [json.loads(l) for l in f if l.startswith("{")][-1]
+      if args.num_neighbors == 5 and args.num_samples == 200:
+        c3mt["equals_oracle_replica_stream"] = rj.get("sha256") == c3mt["sha256"] \
+            and bool(rj.get("records_equal"))
+        c3mt["oracle_replica_s"] = rj.get("oracle_s")
 
     # ---- end to end: one real EmbedHg2vAlgDist call (embedding.py:389) ----
     from hypergraphembedding_amd.embedding import EmbedHg2vAlgDist
@@ -707,6 +743,7 @@ def main():
         "sampling": ("row-sharded over ranks + record all-gather" if world > 1
                      else "single GPU"),
         "c2_fobe_d128": c2,
+        "c3_hobe_mt19937": c3mt,
         "end_to_end": e2e,
         "algdist_c4": c4,
         "c4_full": c4_full,
