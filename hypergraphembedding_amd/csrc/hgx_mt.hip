@@ -40,6 +40,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <new>
 #include <vector>
 
 #include "hgx_internal.h"
@@ -446,6 +447,10 @@ int upload(hgx_ctx *ctx, DevBuf &b, const std::vector<T> &h) {
 
 enum MtPattern { P_A = 0, P_AT, P_NN, P_EE, P_NNE, P_EEN };
 
+// entries (= draws + rows) of one pattern held at once: 8.6e9 x 12 B of
+// device memory and 34 GB of host memory at most
+constexpr int64_t kMaxPatternEntries = int64_t(1) << 33;
+
 // One pattern's sample: per row the chosen columns (packed by roff) on the
 // device, plus what the host knows (row lengths, counts).
 struct MtPat {
@@ -559,6 +564,14 @@ int sample_pattern(MtRun &M, MtPat &p, Mt &st, const std::vector<int> &q) {
     coff[r + 1] = coff[r] + L;
     p.roff[r + 1] = p.roff[r] + std::min(q[r], L);
   }
+  // every draw of the pattern is held on the host, then on the device with
+  // the rows' column lists and Fisher-Yates scratch (12 B per draw): the
+  // mode is for the graphs the reference itself can sample (C4's 2-hop
+  // patterns have ~1e12 entries)
+  HGX_CHECK(ctx, coff[R] <= kMaxPatternEntries, HGX_EUNSUP,
+            "rng=mt19937: pattern %d has %lld entries, above the %lld this mode "
+            "holds (the reference materialises the same rows)",
+            p.pattern, (long long)coff[R], (long long)kMaxPatternEntries);
   // (one slack word: mt_interval_run stores every word it looks at)
   std::vector<uint32_t> D((size_t)doff[R] + 1);
   uint32_t *dp = D.data();
@@ -735,7 +748,7 @@ void put_state(const Mt &st, uint32_t *key, int32_t *pos) {
 
 }  // namespace
 
-extern "C" int hgx_sample_fobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
+static int hgx_sample_fobe_mt_impl(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
                                   const int32_t *node_quota, const int32_t *edge_quota,
                                   const int32_t *neg_node_quota,
                                   const int32_t *neg_edge_quota, int64_t *n_records) {
@@ -815,6 +828,19 @@ extern "C" int hgx_sample_fobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_po
   return HGX_OK;
 }
 
+extern "C" int hgx_sample_fobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
+                                  const int32_t *node_quota, const int32_t *edge_quota,
+                                  const int32_t *neg_node_quota,
+                                  const int32_t *neg_edge_quota, int64_t *n_records) {
+  if (!ctx) return HGX_EINVAL;
+  try {
+    return hgx_sample_fobe_mt_impl(ctx, mt_key, mt_pos, K, node_quota, edge_quota,
+                                   neg_node_quota, neg_edge_quota, n_records);
+  } catch (const std::bad_alloc &) {
+    return hgx_fail(ctx, HGX_ENOMEM, "rng=mt19937: host allocation failed");
+  }
+}
+
 namespace {
 
 // AlgebraicDistanceSamples / WeightedJaccardSamples (run_in_parallel=False)
@@ -858,7 +884,7 @@ int pairs4_mt(MtRun &M, Mt &st, const std::vector<int> &qn, const std::vector<in
 
 int hgx_jaccard_fill(hgx_ctx *ctx, int64_t o_ee, int64_t o_ne, int64_t total);
 
-extern "C" int hgx_sample_hobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
+static int hgx_sample_hobe_mt_impl(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
                                   int S, int64_t *n_records) {
   if (!ctx) return HGX_EINVAL;
   MtRun M;
@@ -880,7 +906,17 @@ extern "C" int hgx_sample_hobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_po
   return HGX_OK;
 }
 
-extern "C" int hgx_sample_jaccard_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
+extern "C" int hgx_sample_hobe_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
+                                  int S, int64_t *n_records) {
+  if (!ctx) return HGX_EINVAL;
+  try {
+    return hgx_sample_hobe_mt_impl(ctx, mt_key, mt_pos, K, S, n_records);
+  } catch (const std::bad_alloc &) {
+    return hgx_fail(ctx, HGX_ENOMEM, "rng=mt19937: host allocation failed");
+  }
+}
+
+static int hgx_sample_jaccard_mt_impl(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
                                      const int32_t *node_quota, const int32_t *edge_quota,
                                      int64_t *n_records) {
   if (!ctx) return HGX_EINVAL;
@@ -898,4 +934,15 @@ extern "C" int hgx_sample_jaccard_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt
   put_state(st, mt_key, mt_pos);
   if (n_records) *n_records = off[4];
   return HGX_OK;
+}
+
+extern "C" int hgx_sample_jaccard_mt(hgx_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int K,
+                                     const int32_t *node_quota, const int32_t *edge_quota,
+                                     int64_t *n_records) {
+  if (!ctx) return HGX_EINVAL;
+  try {
+    return hgx_sample_jaccard_mt_impl(ctx, mt_key, mt_pos, K, node_quota, edge_quota, n_records);
+  } catch (const std::bad_alloc &) {
+    return hgx_fail(ctx, HGX_ENOMEM, "rng=mt19937: host allocation failed");
+  }
 }
