@@ -143,6 +143,9 @@ extern "C" int hgx_set_tuning(hgx_ctx *ctx, const char *key, int64_t value) {
   } else if (k == "mlp_prefetch") {
     HGX_CHECK(ctx, value >= 0 && value <= 2, HGX_EINVAL, "mlp_prefetch must be 0, 1 or 2");
     t.mlp_prefetch = (int)value;
+  } else if (k == "mlp_wgrad_split") {
+    HGX_CHECK(ctx, value >= 0 && value <= 1, HGX_EINVAL, "mlp_wgrad_split must be 0 or 1");
+    t.mlp_wgrad_split = (int)value;
   } else if (k == "train_prep_overlap") {
     HGX_CHECK(ctx, value >= 0 && value <= 2, HGX_EINVAL, "train_prep_overlap must be 0, 1 or 2");
     t.train_prep_overlap = (int)value;

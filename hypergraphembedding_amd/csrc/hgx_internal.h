@@ -67,6 +67,10 @@ struct Tuning {
   // joint-layer launch), so its first layer and weight gradient read a dense
   // operand; 0 both gather
   int mlp_prefetch = 1;
+  // combiner MLP training: where the weight gradients of the layers after the
+  // pre layers run. 0 every gradient in one launch after the pre-layer
+  // deltas; 1 two launches (those layers', then the pre layers')
+  int mlp_wgrad_split = 0;
   // trainer: chunk c + 1 prepared (train_prep / train_place) on a second
   // stream while chunk c trains (1), on the same stream one chunk ahead
   // (2: queued before chunk c's batches, so the host never waits on the

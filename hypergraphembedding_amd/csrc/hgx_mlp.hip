@@ -1618,6 +1618,12 @@ int run_batch(hgx_mlp *m, const Ctx &c, const int *pn, const int *pe,
   }
   add(hd, dense(m->A_j, m->ldJ, 2 * NpJ), m->D_hm);
   add(lb, dense(m->A_hm, L[hd].Np, L[hd].Np), m->D_4);
+  if (ctx->tune.mlp_wgrad_split == 1) {
+    // the layers after the pre layers first, then the pre layers (same
+    // arithmetic per weight; only the launch grouping differs)
+    HGX_TRY(launch_wgrad(ctx, wj.data() + 2, wt.data() + 2, (int)wj.size() - 2, c));
+    return launch_wgrad(ctx, wj.data(), wt.data(), 2, c);
+  }
   return launch_wgrad(ctx, wj.data(), wt.data(), (int)wj.size(), c);
 }
 
