@@ -99,6 +99,36 @@ __device__ unsigned long long g_mlp_n[8];
 #endif
 constexpr int kMcap = 4096;   // activation rows (training uses the first 256)
 
+// Global stores of the launches' outputs (activations, deltas, prefetched
+// rows, weights and Adagrad state). HGX_MLP_WT=1: write-through (an
+// agent-scope relaxed atomic store is `global_store ... sc1`), so the output
+// leaves no dirty lines in the XCD's L2 for the kernel-end release to write
+// back before the next, dependent launch (MI355X_MICROARCH "boundary":
+// + bytes / 6 TB/s; "publish-large"); 0: plain stores (A/B builds). C5
+// combiner, interleaved A/B (tools/r06_mlp_wt.sh, profiles/r06/mlp_wt/):
+// 4.80 / 4.79M -> 4.94 / 4.95M samples/s, the MLP tests bit-exact.
+#ifndef HGX_MLP_WT
+#define HGX_MLP_WT 1
+#endif
+__device__ __forceinline__ void gst(float *p, float v) {
+  if (HGX_MLP_WT)
+    __hip_atomic_store(reinterpret_cast<unsigned *>(p), __float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+__device__ __forceinline__ void gst4(float *p, float4 v) {
+  if (HGX_MLP_WT) {
+    unsigned long long *q = reinterpret_cast<unsigned long long *>(p);
+    __hip_atomic_store(q, __builtin_bit_cast(unsigned long long, make_float2(v.x, v.y)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, __builtin_bit_cast(unsigned long long, make_float2(v.z, v.w)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *reinterpret_cast<float4 *>(p) = v;
+  }
+}
+
 enum { ACT_SIGMOID = HGX_ACT_SIGMOID, ACT_RELU = HGX_ACT_RELU };
 
 // exp for the sigmoid: Cephes expf's reduction and polynomial written as
@@ -440,8 +470,7 @@ __device__ __forceinline__ void fwd_prefetch(const FwdJob &J, const Ctx &c, int 
 #pragma unroll
   for (int i = 0; i < 4; i++)
     if (m[i] < kPfRows)
-      *reinterpret_cast<float4 *>(J.pfX + (int64_t)m[i] * J.pfld + k4[i]) =
-          src_fix4(sa, r[i], k4[i], v[i], true);
+      gst4(J.pfX + (int64_t)m[i] * J.pfld + k4[i], src_fix4(sa, r[i], k4[i], v[i], true));
 }
 
 // NCH > 0: exactly NCH reduction chunks, every chunk's operands loaded up
@@ -536,7 +565,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd(Jobs<FwdJob> js, Ctx c) {
     const int m = m0 + i0 + e;
     const bool valid = m < c.M && n < J.Nreal;
     const float y = valid ? ya[e] : 0.f;
-    J.Y[(int64_t)m * J.ldy + n] = y;
+    gst(&J.Y[(int64_t)m * J.ldy + n], y);
     if (J.loss) {
       float dz = 0.f;
       if (valid) {
@@ -544,7 +573,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd(Jobs<FwdJob> js, Ctx c) {
         lsum += diff * diff;
         dz = J.lw * 2.0f * diff / ((float)J.Nreal * (float)c.M) * act_d(J.act, y);
       }
-      J.dZ[(int64_t)m * J.lddz + n] = dz;
+      gst(&J.dZ[(int64_t)m * J.lddz + n], dz);
     }
   }
   if (J.loss) {
@@ -680,8 +709,8 @@ __device__ __forceinline__ void head_wave_t(const HeadJob &h, const Ctx &c, int 
 #pragma unroll
     for (int s = 0; s < 8; s++) {
       const int m = mb + s;
-      if (m < c.M && h.y && lane == 0) h.y[m] = ys[s];
-      if (h.loss && lane == 0) h.dz4[(int64_t)m * h.ld4] = dzs[s];
+      if (m < c.M && h.y && lane == 0) gst(&h.y[m], ys[s]);
+      if (h.loss && lane == 0) gst(&h.dz4[(int64_t)m * h.ld4], dzs[s]);
     }
   }
   if (!h.loss) return;
@@ -707,7 +736,7 @@ __device__ __forceinline__ void head_wave_t(const HeadJob &h, const Ctx &c, int 
         if (lane + 64 * kk < h.K)
 #pragma unroll
           for (int s = 0; s < 8; s++)
-            h.dZprev[(int64_t)(mb + s) * h.ldp + lane + 64 * kk] = dv[kk][s];
+            gst(&h.dZprev[(int64_t)(mb + s) * h.ldp + lane + 64 * kk], dv[kk][s]);
     }
   } else {
     for (int k = lane; k < h.K; k += 64) {
@@ -718,7 +747,7 @@ __device__ __forceinline__ void head_wave_t(const HeadJob &h, const Ctx &c, int 
         const bool valid = m < c.M;
         const float hvv = h.H[(int64_t)min(m, c.M - 1) * h.ldh + k];
         const float v = valid ? dzs[s] * wk * act_d(act_prev, hvv) : 0.f;
-        if (gstore) h.dZprev[(int64_t)m * h.ldp + k] = v;
+        if (gstore) gst(&h.dZprev[(int64_t)m * h.ldp + k], v);
         if (S) S[(srow + s) * sld + k] = v;
       }
     }
@@ -909,7 +938,7 @@ __global__ __launch_bounds__(kThreads) void mlp_bwd(Jobs<BwdJob> js, Ctx c, Head
   for (int e = 0; e < 4; e++) {
     const int m = m0 + i0 + e;
     const float d = (m < c.M && k < J.Kreal) ? v[e] * act_d(J.act, ypre[e]) : 0.f;
-    J.dZ[(int64_t)m * J.ldo + k] = d;
+    gst(&J.dZ[(int64_t)m * J.ldo + k], d);
   }
   if constexpr (NCH > 0) {
     TSTAMP(5);
@@ -956,12 +985,12 @@ __device__ __forceinline__ void wgrad_bias(const WgJob &J, const Ctx &c, int n0,
     for (int q = 0; q < 8; q++) g += bs[q * 32 + t];
     const int nn = n0 + t;
     if (c.grad_only) {
-      J.b[nn] = g;
+      gst(&J.b[nn], g);
       return;
     }
     const float na = ba + g * g;
-    J.ab[nn] = na;
-    J.b[nn] = bb - (c.lr * g) / (sqrtf(na) + c.eps);
+    gst(&J.ab[nn], na);
+    gst(&J.b[nn], bb - (c.lr * g) / (sqrtf(na) + c.eps));
   }
 }
 
@@ -1060,7 +1089,7 @@ __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
   const int n = n0 + j;
   if (c.grad_only) {
 #pragma unroll
-    for (int e = 0; e < 4; e++) J.W[(int64_t)(k0 + i0 + e) * J.ldw + n] = v[e];
+    for (int e = 0; e < 4; e++) gst(&J.W[(int64_t)(k0 + i0 + e) * J.ldw + n], v[e]);
   } else {
     // the four Adagrad steps first (their square roots and divisions
     // interleave), then the stores. Plain sqrtf is correctly rounded on
@@ -1076,8 +1105,8 @@ __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
 #pragma unroll
     for (int e = 0; e < 4; e++) {
       const int64_t q = (int64_t)(k0 + i0 + e) * J.ldw + n;
-      J.aW[q] = na[e];
-      J.W[q] = nw[e];
+      gst(&J.aW[q], na[e]);
+      gst(&J.W[q], nw[e]);
     }
   }
   if constexpr (NCH > 0) {
