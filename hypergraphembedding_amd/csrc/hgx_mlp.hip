@@ -1102,11 +1102,16 @@ __global__ __launch_bounds__(kThreads) void mlp_wgrad(Jobs<WgJob> js, Ctx c) {
       na[e] = pA[e] + g * g;
       nw[e] = pW[e] - (c.lr * g) / (sqrtf(na[e]) + c.eps);
     }
+#ifndef HGX_MLP_PROBE_ST
+#define HGX_MLP_PROBE_ST 0
+#endif
 #pragma unroll
     for (int e = 0; e < 4; e++) {
       const int64_t q = (int64_t)(k0 + i0 + e) * J.ldw + n;
-      gst(&J.aW[q], na[e]);
-      gst(&J.W[q], nw[e]);
+      // probe builds only (results wrong): 1 no accumulator stores, 2 no
+      // weight-gradient tile stores at all
+      if (HGX_MLP_PROBE_ST == 0) gst(&J.aW[q], na[e]);
+      if (HGX_MLP_PROBE_ST < 2) gst(&J.W[q], nw[e]);
     }
   }
   if constexpr (NCH > 0) {
