@@ -49,10 +49,14 @@ then killed). A `--gpus` that disagrees with WORLD_SIZE is refused. The
 line carries `ranks_seen` (dist.get_world_size()) and `devices_seen`
 (torch.cuda.device_count()).
 
---c4-full (opt-in, not in the default run; ~5 min on one GPU): the WHOLE
-C4 pipeline timed as `c4_full` -- alg-dist (k=10, 20 iterations; sharded at
-N > 1), HOBE sampling of every row into the record store, one
-global-shuffle d=256 epoch from the store (embedding.py:389-416's path).
+`c4_full` (in the default run at N = 1, ~4.5 min of its ~7.5, started only
+if it still fits `--time-budget`, 600 s; `--no-c4-full` skips it,
+`--c4-full` forces it, also at N > 1): the WHOLE C4 pipeline --
+alg-dist (k=10, 20 iterations; sharded at N > 1), HOBE sampling of every row
+into the record store, one global-shuffle d=256 epoch from the store
+(embedding.py:389-416's path) -- timed as `c4_full_time_to_embedding_s`.
+At N > 1 its epoch is a replica on every rank, so it is skipped by default
+there (the ranks would all train the same 223 s epoch).
 """
 
 import argparse
@@ -71,6 +75,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+T_START = time.time()
+# wall time of the whole-C4 leg with its graph build and store release (one
+# MI355X: 270 s measured, profiles/r06/bench_default_c4full/) plus margin
+C4_FULL_EST_S = 330.0
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFLOPS = 157.3  # f32-in MFMA = the FP32 vector peak (same guide)
 METRIC = ("training samples/sec + alg-dist SpMV GB/s, HOBE dim=128 at "
@@ -110,8 +118,14 @@ def parse():
   p.add_argument("--no-c4", action="store_true",
                  help="skip the power-law 10M/5M measurements")
   p.add_argument("--c4-full", action="store_true",
-                 help="opt-in: the whole C4 HOBE d=256 pipeline (every row "
-                      "sampled into the record store, one epoch; ~5 min)")
+                 help="run the whole C4 HOBE d=256 pipeline (every row "
+                      "sampled into the record store, one epoch; ~4.5 min) "
+                      "even at N > 1 or with --no-c4")
+  p.add_argument("--no-c4-full", action="store_true",
+                 help="skip the whole-C4 pipeline (default at N = 1)")
+  p.add_argument("--time-budget", type=float, default=600.0,
+                 help="seconds the whole run should stay within: the default "
+                      "whole-C4 leg (~300 s) starts only if it fits")
   p.add_argument("--no-extra", action="store_true",
                  help="skip the C2 FOBE and end-to-end measurements")
   p.add_argument("--c4-chunks", type=int, default=2,
@@ -685,9 +699,15 @@ def main():
     progress("C4 legs (alg-dist, 2% HOBE d=256 slice, C5 combiner)")
     c4 = bench_c4(args, ctx, rank, world, sync, max_over_ranks, alg_dist_sharded)
   c4_full = None
-  if args.c4_full:
-    progress("c4-full leg")
-    c4_full = bench_c4_full(args, ctx, world, sync, max_over_ranks)
+  if args.c4_full or (world == 1 and not args.no_c4 and not args.no_c4_full):
+    spent = time.time() - T_START
+    if not args.c4_full and spent + C4_FULL_EST_S > args.time_budget:
+      # the default leg would not fit the run's time budget on this box
+      c4_full = {"skipped": f"{spent:.0f} s spent before the leg, ~{C4_FULL_EST_S:.0f} s "
+                            f"needed, budget {args.time_budget:.0f} s (--c4-full forces it)"}
+    else:
+      progress("c4-full leg")
+      c4_full = bench_c4_full(args, ctx, world, sync, max_over_ranks)
 
   ranks_seen = dist.get_world_size() if dist is not None else 1
   # HIP devices visible to this rank's libhgx (hipGetDeviceCount; torch's
@@ -711,6 +731,8 @@ def main():
         # embedding (alg-dist + sampling + one epoch, sharded at N > 1)
         "distinct_records_per_s": round(n * args.steps / elapsed, 1),
         "c4_time_to_embedding_s": tte4,
+        # the whole C4 pipeline (every row sampled, one epoch; c4_full)
+        "c4_full_time_to_embedding_s": (c4_full or {}).get("time_to_embedding_s"),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -18,7 +18,7 @@ fi
 [ $PART = tests ] && exit 0
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || exit 14
 echo bench-ok
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_bench -o run --output-format csv -- python3 bench.py --no-cpu > $O/bench_prof.json 2> $O/bench_prof.err || exit 15
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_bench -o run --output-format csv -- python3 bench.py --no-cpu --no-c4-full > $O/bench_prof.json 2> $O/bench_prof.err || exit 15
 find $O/prof_bench -name '*stats.csv' -exec cp {} $O/ \;
 rm -rf $O/prof_bench
 echo prof-ok
