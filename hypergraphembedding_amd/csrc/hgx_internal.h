@@ -41,6 +41,9 @@ struct Tuning {
   int64_t sample_reject_w = 1 << 15;
   // 3-hop rejection proposal: 0 auto, 1 paths (Karp-Luby), 2 uniform columns
   int sample_mode3 = 0;
+  // mode 0: a row takes uniform columns when its path count W is at least
+  // the column count times 2^sample_mode3_shift (paths otherwise)
+  int sample_mode3_shift = 1;
   // trainer: 1 fused one-launch batch step where a batch packs, 0 the
   // two-kernel step for every batch
   int train_fused = 1;

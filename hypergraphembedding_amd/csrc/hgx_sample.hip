@@ -570,6 +570,7 @@ struct RejectArgs {
   const int64_t *ps;         // 3-hop: exclusive scan over l2's incidences of
                              // |l3 row of the incidence's column| (nnz + 1)
   int mode3;                 // 0 auto, 1 paths, 2 uniform columns
+  int mode3_shift;           // auto: uniform columns when W >= ncols * 2^mode3_shift
   int *stats;                // [0] rejection rows, [1] stalled, [3] uniform-mode rows
   Bloom bloom;               // member filters of the edges (3-hop patterns)
   long long *diag;           // debug builds: per-row {pattern, row, mode, n1, q, W,
@@ -818,7 +819,11 @@ __global__ __launch_bounds__(kSB) void reject_rows(RejectArgs A) {
     }
     int mode = 0;
     if (A.levels == 3)
-      mode = (A.mode3 == 2 || (A.mode3 == 0 && W >= (long long)A.ncols)) ? 2 : 1;
+      mode = (A.mode3 == 2 ||
+              (A.mode3 == 0 && (A.mode3_shift >= 0 ? W >= ((long long)A.ncols << A.mode3_shift)
+                                                   : (W << -A.mode3_shift) >= (long long)A.ncols)))
+                 ? 2
+                 : 1;
     const bool small = n1 <= kSB;
     if (mode != 2 && small) {  // exact path draws: prefix of weights in LDS
       long long x = 0;
@@ -1323,6 +1328,7 @@ int run_pattern(hgx_ctx *ctx, int pattern, const int32_t *host_quota,
     r.reject_w = reject_w;
     r.ps = ps.as<int64_t>();
     r.mode3 = ctx->tune.sample_mode3;
+    r.mode3_shift = ctx->tune.sample_mode3_shift;
     r.stats = ctr + 5;
     if (a.levels == 3)
       r.bloom = Bloom{ctx->bloom_off.as<long long>(), ctx->bloom_bits.as<unsigned>()};
