@@ -67,6 +67,8 @@ int hgx_mem_info(hgx_ctx *ctx, int64_t *free_bytes, int64_t *total_bytes);
  *                      sampled by rejection (default 32768; 0 = expand all)
  *   "sample_mode3"     3-hop rejection proposal: 0 auto, 1 paths
  *                      (Karp-Luby), 2 uniform columns
+ *   "sample_mode3_shift" auto rule: uniform columns when a row's path
+ *                      count >= columns x 2^shift (default 1, -10..10)
  *   "train_fused"      1 fused one-launch batch step (default), 0 the
  *                      two-kernel step for every batch
  *   "train_lanes"      fused step at padded d = 128: lanes per record
@@ -89,6 +91,9 @@ int hgx_mem_info(hgx_ctx *ctx, int64_t *free_bytes, int64_t *total_bytes);
  *                      hidden-layer launch (default, bit-identical), 2 of its
  *                      joint-layer launch (measured 0.4% slower), 0 the
  *                      first layer and its weight gradient gather them
+ *   "mlp_wgrad_split"  combiner MLP training: 0 every weight gradient in one
+ *                      launch (default), 1 two launches (the layers after the
+ *                      pre layers, then the pre layers; measured slower)
  *   "train_prep_overlap" trainer: 1 prepare chunk c + 1 (train_prep /
  *                      train_place) on a second stream while chunk c trains,
  *                      0 in line before each chunk (default); the same
