@@ -250,9 +250,10 @@ class Context:
 
   def set_tuning(self, key, value):
     """Pick between exact implementations (hgx_set_tuning): sample_reject_w,
-    sample_mode3, sample_mode3_shift, train_fused, train_lanes, train_tb,
-    train_prep_overlap, train_prep_cus, alg_long, alg_ks, alg_push,
-    mlp_fuse_head, mlp_prefetch, mlp_wgrad_split, stream_cus."""
+    sample_mode3, sample_mode3_shift, sample_mode3_shift_e, train_fused,
+    train_lanes, train_tb, train_prep_overlap, train_prep_cus, alg_long,
+    alg_ks, alg_push, mlp_fuse_head, mlp_prefetch, mlp_wgrad_split,
+    stream_cus."""
     self._chk(lib().hgx_set_tuning(self.h, key.encode(), int(value)))
 
   # ---- incidence ----

@@ -116,6 +116,10 @@ extern "C" int hgx_set_tuning(hgx_ctx *ctx, const char *key, int64_t value) {
   if (k == "sample_reject_w") {
     HGX_CHECK(ctx, value >= 0, HGX_EINVAL, "sample_reject_w must be >= 0");
     t.sample_reject_w = value;
+  } else if (k == "sample_mode3_shift_e") {
+    HGX_CHECK(ctx, value >= -10 && value <= 10, HGX_EINVAL,
+              "sample_mode3_shift_e must be in [-10, 10]");
+    t.sample_mode3_shift_e = (int)value;
   } else if (k == "sample_mode3_shift") {
     HGX_CHECK(ctx, value >= -10 && value <= 10, HGX_EINVAL,
               "sample_mode3_shift must be in [-10, 10]");

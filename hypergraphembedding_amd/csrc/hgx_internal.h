@@ -41,9 +41,12 @@ struct Tuning {
   int64_t sample_reject_w = 1 << 15;
   // 3-hop rejection proposal: 0 auto, 1 paths (Karp-Luby), 2 uniform columns
   int sample_mode3 = 0;
-  // mode 0: a row takes uniform columns when its path count W is at least
-  // the column count times 2^sample_mode3_shift (paths otherwise)
+  // mode 0: a node row of the 3-hop pattern (A A^T A) takes uniform columns
+  // when its path count W is at least the column count times
+  // 2^sample_mode3_shift (paths otherwise); an edge row (A^T A A^T) by
+  // sample_mode3_shift_e. Defaults from a sweep on the C4 graph
   int sample_mode3_shift = 1;
+  int sample_mode3_shift_e = 1;
   // trainer: 1 fused one-launch batch step where a batch packs, 0 the
   // two-kernel step for every batch
   int train_fused = 1;

@@ -1328,7 +1328,8 @@ int run_pattern(hgx_ctx *ctx, int pattern, const int32_t *host_quota,
     r.reject_w = reject_w;
     r.ps = ps.as<int64_t>();
     r.mode3 = ctx->tune.sample_mode3;
-    r.mode3_shift = ctx->tune.sample_mode3_shift;
+    r.mode3_shift = pattern == PAT_EEN ? ctx->tune.sample_mode3_shift_e
+                                       : ctx->tune.sample_mode3_shift;
     r.stats = ctr + 5;
     if (a.levels == 3)
       r.bloom = Bloom{ctx->bloom_off.as<long long>(), ctx->bloom_bits.as<unsigned>()};

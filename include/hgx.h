@@ -67,8 +67,10 @@ int hgx_mem_info(hgx_ctx *ctx, int64_t *free_bytes, int64_t *total_bytes);
  *                      sampled by rejection (default 32768; 0 = expand all)
  *   "sample_mode3"     3-hop rejection proposal: 0 auto, 1 paths
  *                      (Karp-Luby), 2 uniform columns
- *   "sample_mode3_shift" auto rule: uniform columns when a row's path
- *                      count >= columns x 2^shift (default 1, -10..10)
+ *   "sample_mode3_shift" auto rule for node rows: uniform columns when a
+ *                      row's path count >= columns x 2^shift (default 1,
+ *                      -10..10); "sample_mode3_shift_e" the same for edge
+ *                      rows (default 1)
  *   "train_fused"      1 fused one-launch batch step (default), 0 the
  *                      two-kernel step for every batch
  *   "train_lanes"      fused step at padded d = 128: lanes per record

@@ -26,7 +26,8 @@ def main():
   p.add_argument("--E", type=int, default=5_000_000)
   p.add_argument("--no-train", action="store_true")
   p.add_argument("--mode3", type=int, default=0)
-  p.add_argument("--mode3-shift", type=int, default=0)
+  p.add_argument("--mode3-shift", type=int, default=1)
+  p.add_argument("--mode3-shift-e", type=int, default=1)
   a = p.parse_args()
   from hypergraphembedding_amd import _hgx
   from hypergraphembedding_amd.synthetic import powerlaw_hypergraph
@@ -38,6 +39,7 @@ def main():
   ctx = _hgx.Context(0)
   ctx.set_tuning("sample_mode3", a.mode3)
   ctx.set_tuning("sample_mode3_shift", a.mode3_shift)
+  ctx.set_tuning("sample_mode3_shift_e", a.mode3_shift_e)
   ctx.upload(g)
   rs = np.random.RandomState(1)
   ctx.alg_set(rs.random_sample((g.N, 10)).astype(np.float32),
