@@ -1606,7 +1606,10 @@ extern "C" int hgx_sample_hobe_rows(hgx_ctx *ctx, uint64_t seed, int K,
   HGX_TRY(hgx_hobe_prepare(ctx));
   HGX_TRY(hgx_hobe_fill_probs(ctx, 0, 0, o_ee));
   HGX_TRY(hgx_hobe_fill_probs(ctx, 1, o_ee, o_ne));
-  HGX_TRY(hgx_hobe_fill_probs(ctx, 2, o_ne, total));
+  // the node rows' and the edge rows' node-edge pairs as two launches (the
+  // same per-pair work; their times apart in a kernel trace)
+  HGX_TRY(hgx_hobe_fill_probs(ctx, 2, o_ne, o_en));
+  HGX_TRY(hgx_hobe_fill_probs(ctx, 2, o_en, total));
   set_blocks(ctx, {0, o_ee, o_ne, o_en, total});
   HGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->smp_family = 1;
